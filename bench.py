@@ -1,0 +1,210 @@
+"""bench.py — Newton-iteration throughput of the MI355X MacroC hot path (BASELINE.json metric).
+
+One "step" = the Newton iteration of time step 1 that performs the solve (src/main.c:61-79 of
+the reference): VecZeroEntries(u) + apply_bc_on_u(U = -0.001), then set_strains, homogenize
+(isotropic-elastic Gauss-point callback), assembly_res + VecNorm, assembly_jac (+ Dirichlet
+rows/columns), KSPSolve(CG, Jacobi, rtol 1e-8) and u += du — every step redoes all of it from
+the same state, nothing is cached across steps.  Workload: 256^3 nodes per GPU
+(BASELINE configs[2]; weak scaling: N GPUs own a global grid of 256*(px,py,pz)).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line (see the contract in the task statement / DESIGN.md §6).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+# torch first: the library then binds to the HIP runtime torch already loaded (one runtime per
+# process); torch is only plumbing here (process group for barriers / max-over-ranks).
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import numpy as np  # noqa: E402
+
+import macroc_amd as M  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def rank_grid(n):
+    return {1: (1, 1, 1), 2: (2, 1, 1), 4: (2, 2, 1), 8: (2, 2, 2), 16: (4, 2, 2)}.get(n) or (n, 1, 1)
+
+
+def cpu_baseline(N, gpu_its, rtol, ndofs_target, nelem_target, nnz_target):
+    """Oracle (scalar C restatement, 1 thread) on an N^3 sample of the same workload; its
+    per-element assembly time and per-(CG iteration x nonzero) time are scaled to the target
+    grid with the GPU run's CG iteration count."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from oracle import oracle as O
+
+    P = O.Problem(N, N, N, rtol=rtol)
+    P.apply_bc_u(P.get_displacement(0))
+    P.apply_bc_u(P.get_displacement(1))
+    t0 = time.perf_counter()
+    P.set_strains()
+    P.homogenize()
+    P.assembly_res()
+    P.norm_b()
+    t1 = time.perf_counter()
+    P.assembly_jac()
+    t2 = time.perf_counter()
+    out = P.solve()
+    t3 = time.perf_counter()
+    P.update_u()
+    t4 = time.perf_counter()
+    nelem = (N - 1) ** 3
+    t_elem = ((t1 - t0) + (t2 - t1)) / nelem
+    t_it_nnz = (t3 - t2) / max(out["its"], 1) / P.nnz
+    t_vec = (t4 - t3) / P.ndofs
+    t_target = t_elem * nelem_target + t_it_nnz * gpu_its * nnz_target + t_vec * ndofs_target
+    P.close()
+    return {
+        "value": ndofs_target / t_target,
+        "unit": "DOF/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"oracle/ (scalar C restatement, gcc -O2, 1 thread) full Newton iteration on {N}^3 "
+                   f"({out['its']} CG its, {t3 - t0:.1f} s); per-element assembly time and per-(CG-iteration x "
+                   f"nonzero) time scaled to the GPU workload with its {gpu_its} CG iterations"),
+        "sample_seconds": t4 - t0,
+        "extrapolated_step_seconds": t_target,
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--grid", type=int, default=256, help="nodes per direction per GPU")
+    ap.add_argument("--rtol", type=float, default=1e-8)
+    ap.add_argument("--cpu-sample", type=int, default=40, help="oracle sample grid (0 = skip)")
+    ap.add_argument("--no-check", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    px, py, pz = rank_grid(world)
+    G = args.grid
+    NX, NY, NZ = G * px, G * py, G * pz
+    argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
+            "-da_processors_z", pz, "-ts", 2, "-ksp_rtol", repr(args.rtol), "-device", local]
+    comm_id = None
+    if world > 1:
+        obj = [M.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm_id = obj[0]
+    t_setup = time.perf_counter()
+    m = M.Macroc(argv, rank=rank, nranks=world, comm_id=comm_id)
+    m.set_timing(True)
+    info = m.info
+    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s, device GB {info['device_bytes'] / 1e9:.1f}, "
+        f"local {info['nx']}x{info['ny']}x{info['nz']}")
+    U = m.get_displacement(1)
+
+    def step():
+        m.zero_u()
+        m.apply_bc_on_u(U)
+        m.set_strains()
+        m.homogenize()
+        res = m.assembly_res()
+        m.assembly_jac()
+        its, rn, reason = m.solve_Ax()
+        m.update_u()
+        return res, its, rn, reason
+
+    def barrier_sync():
+        m.synchronize()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    for w in range(args.warmup):
+        t = time.perf_counter()
+        r = step()
+        log(f"[rank {rank}] warmup {w}: {time.perf_counter() - t:.2f}s its={r[1]}")
+    barrier_sync()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        res, its, rn, reason = step()
+        log(f"[rank {rank}] step {s}: its={its} reason={reason} |RES|={res:.6e} rnorm={rn:.3e}")
+    barrier_sync()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt[0])
+    tm = m.timing()
+    spmv_avg_ms = tm["spmv_ms_total"] / max(tm["spmv_launches"], 1)
+    spmv_bytes = tm["spmv_bytes_per_launch"]
+    achieved = spmv_bytes / (spmv_avg_ms * 1e-3) / 1e9
+
+    check = None
+    if not args.no_check:
+        # size-independent property: true residual of the solve, |A du - b| / |b| (collective)
+        b, du = m.b(), m.du()
+        r = m.spmv(du) - b
+        loc = np.array([r @ r, b @ b])
+        if world > 1:
+            tt = torch.tensor(loc)
+            dist.all_reduce(tt)
+            loc = tt.numpy()
+        check = {"true_rel_residual": float(np.sqrt(loc[0] / loc[1])), "ksp_reason": int(reason)}
+
+    ndofs = 3 * NX * NY * NZ
+    ms_step = dt / args.steps * 1e3
+    if rank == 0:
+        cpu = None
+        if world == 1 and args.cpu_sample > 0:
+            try:
+                cpu = cpu_baseline(args.cpu_sample, its, args.rtol, ndofs, (NX - 1) * (NY - 1) * (NZ - 1),
+                                   info["nnz_global"])
+            except Exception as e:  # the baseline is reported, never the product path
+                cpu = {"error": repr(e)}
+        line = {
+            "metric": "Newton-iter DOF/s (assembly+CG) at 256^3 grid per GPU; SpMV achieved HBM GB/s",
+            "value": ndofs / (ms_step * 1e-3),
+            "unit": "DOF/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (reference defaults: lx=50 ly=1 lz=50, BC_CIRCLE, E=1e7 nu=0.25, time step 1)",
+            "config": {"workload": f"MacroC Newton iteration, time step 1, CG/Jacobi rtol {args.rtol:g}",
+                       "grid": [NX, NY, NZ], "grid_per_gpu": [G, G, G], "processors": [px, py, pz],
+                       "dofs": ndofs, "nnz": info["nnz_global"], "parallelism": f"dmda{px}x{py}x{pz}"},
+            "cg_its": its,
+            "ms_per_cg_iter": tm["solve_ms"] / max(its, 1),
+            "phases_ms": {k: tm[k] for k in ("strains_ms", "homogenize_ms", "residual_ms", "jacobian_ms",
+                                             "solve_ms", "update_ms")},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                         "kernel": "k_spmv (stencil-block SpMV inside CG)", "bytes_per_launch": spmv_bytes,
+                         "avg_launch_ms": spmv_avg_ms, "launches_timed": tm["spmv_launches"]},
+            "cpu_baseline": cpu,
+            "check": check,
+        }
+        print(json.dumps(line), flush=True)
+    m.finish()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,175 @@
+/*
+ * macroc_amd.h — C-ABI of the MI355X-native MacroC Newton inner loop.
+ *
+ * One context = one MPI-style rank = one GPU subdomain of the DMDA box decomposition.
+ * Every entry point returns 0 on success and a non-zero code on failure, mirroring the
+ * reference's PetscErrorCode convention (src/assembly.c:37-42 ... CHKERRQ); the message of
+ * the last failure is available from mcx_last_error().  Host buffers are caller-owned;
+ * the context owns all device memory.  A context is not thread-safe; different contexts
+ * may be driven from different threads.  No torch / HIP types appear in this interface.
+ *
+ * Reference interface each entry replaces (paths relative to GG1991/macroc):
+ *   mcx_default_opts / mcx_parse_args  <- init() defaults + PetscOptionsGet, DMSetFromOptions,
+ *                                         KSPSetFromOptions   src/init.c:47-83,93,156
+ *   mcx_init                          <- init() grid/Mat/Vec/KSP part  src/init.c:85-171,
+ *                                         bc_init src/bcs.c:154-195
+ *   mcx_finalize                      <- finish()  src/init.c:222-237
+ *   mcx_get_displacement              <- get_displacement  src/bcs.c:52-58
+ *   mcx_apply_bc_u                    <- apply_bc_on_u  src/bcs.c:29-45 (-> :61-146)
+ *   mcx_set_strains                   <- set_strains  src/assembly.c:25-66
+ *   mcx_homogenize                    <- micropp_C_homogenize  src/main.c:62 (device-batched
+ *                                         constitutive callback, see mcx_material_set)
+ *   mcx_assembly_res                  <- assembly_res + VecNorm  src/assembly.c:120-176,
+ *                                         src/main.c:67
+ *   mcx_assembly_jac                  <- assembly_jac + apply_bc_on_jac  src/assembly.c:69-117,
+ *                                         src/bcs.c:341-347
+ *   mcx_solve                         <- solve_Ax -> KSPSolve(CG, Jacobi)  src/assembly.c:179-192
+ *   mcx_update_u                      <- VecAXPY(u, 1., du)  src/main.c:79
+ *   mcx_material_set                  <- micropp_C_material_set  src/init.c:196-201
+ */
+#ifndef MACROC_AMD_H
+#define MACROC_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MCX_COMM_ID_BYTES 128 /* size of an ncclUniqueId */
+
+enum { MCX_BC_BENDING = 0, MCX_BC_CIRCLE = 1 }; /* include/macroc.h:58 */
+
+/* KSPConvergedReason (PETSc) */
+enum {
+  MCX_KSP_CONVERGED_ITERATING = 0,
+  MCX_KSP_CONVERGED_RTOL = 2,
+  MCX_KSP_CONVERGED_ATOL = 3,
+  MCX_KSP_DIVERGED_ITS = -3,
+  MCX_KSP_DIVERGED_DTOL = -4,
+  MCX_KSP_DIVERGED_INDEFINITE_PC = -8,
+  MCX_KSP_DIVERGED_NANORINF = -9,
+  MCX_KSP_DIVERGED_INDEFINITE_MAT = -10
+};
+
+/* constitutive models behind the Gauss-point callback */
+enum { MCX_MAT_ELASTIC = 0 };
+
+typedef struct {
+  int64_t NX, NY, NZ;          /* -da_grid_x/y/z          (default 40 3 40, include/macroc.h:44-46) */
+  int px, py, pz;              /* -da_processors_x/y/z    (0 = PETSC_DECIDE) */
+  double lx, ly, lz;           /* -lx -ly -lz             (50 1 50) */
+  double dt, final_time;       /* -dt                     (0.001, FINAL_TIME 1.0) */
+  int ts;                      /* -ts                     (1) */
+  int vtu_freq;                /* -vtu_freq               (-1; VTU output is out of scope) */
+  int bc_type;                 /* -bc_type                (BC_CIRCLE) */
+  double rad;                  /* load-circle radius      (1.0, src/init.c:141) */
+  int newton_max_its;          /* -newton_max_its         (5) */
+  double newton_min_tol;       /* -newton_min_tol         (0.1) */
+  double newton_rel_tol;       /* -newton_rel_tol         (1e-4) */
+  double ksp_rtol, ksp_abstol, ksp_dtol; /* -ksp_rtol -ksp_atol -ksp_divtol (1e-5 1e-50 1e4) */
+  int ksp_max_it;              /* -ksp_max_it             (10000) */
+  int micro_n, micro_type;     /* -micro_n -micro_type    (2, 1) */
+  double micro_mat_1[4];       /* -micro_mat_1 E,nu,Sy,Ka (1e7,.25,1e4,1e7) */
+  double micro_mat_2[4];       /* -micro_mat_2 */
+  int device;                  /* HIP device of this rank (-1: rank % device count) */
+  int ksp_monitor;             /* -ksp_monitor: keep the residual history */
+} mcx_opts;
+
+typedef struct {
+  int64_t NX, NY, NZ;
+  int px, py, pz;              /* rank grid actually used */
+  int rank, nranks;
+  int64_t xs, ys, zs, nx, ny, nz;   /* owned node corners (DMDAGetCorners) */
+  int64_t Xs, Ys, Zs, Nx, Ny, Nz;   /* ghost corners (DMDAGetGhostCorners) */
+  int64_t ndofs_global;
+  int64_t ndofs_local;          /* 3*nx*ny*nz, PETSc-global rows owned */
+  int64_t dof_offset;           /* first global PETSc row of this rank */
+  int64_t nnz_local;            /* AIJ nonzeros of the owned rows (pattern of DMCreateMatrix) */
+  int64_t nnz_global;
+  int64_t nelem_local;          /* DMDAGetElementsSizes product (PETSc-owned elements) */
+  int64_t nelem_ext;            /* elements evaluated on this device (owned + upper ghost layer) */
+  double dx, dy, dz, wg;        /* src/init.c:137-140 */
+  int64_t device_bytes;         /* device memory held by the context */
+  int device;
+} mcx_info;
+
+typedef struct {
+  /* wall milliseconds of the last call of each phase (HIP events on the compute stream) */
+  double strains_ms, homogenize_ms, residual_ms, jacobian_ms, solve_ms, update_ms;
+  /* SpMV kernel inside the last mcx_solve: launches counted and summed device time */
+  int64_t spmv_launches;
+  double spmv_ms_total;
+  int64_t spmv_bytes_per_launch; /* algorithmic bytes of one SpMV (values + x once + y once) */
+} mcx_timing;
+
+const char* mcx_last_error(void);
+const char* mcx_version(void);
+
+void mcx_default_opts(mcx_opts* o);
+/* parse the reference's command-line surface (PETSc options-DB names); unknown flags are
+   warned about on stderr and ignored, like the reference's options DB */
+int mcx_parse_args(mcx_opts* o, int argc, const char* const* argv);
+
+/* rank 0 creates the communicator id, the host transports it to every rank (MPI_Bcast,
+   torch.distributed, a file ...).  Only needed when nranks > 1. */
+int mcx_comm_unique_id(void* id /* MCX_COMM_ID_BYTES */);
+
+/* Host-only planning (no GPU needed): the DMDA decomposition a rank would get, and its
+   forward-halo plan — neighbour ranks and, per neighbour, the natural node ids
+   (i + j*NX + k*NX*NY) sent and received, in message order.  Pass NULL arrays to query
+   counts (*nnbr <= 26; *nsend / *nrecv = total nodes). */
+int mcx_plan(const mcx_opts* o, int rank, int nranks, mcx_info* info);
+int mcx_plan_halo(const mcx_opts* o, int rank, int nranks, int* nnbr, int* nbr_rank, int64_t* send_cnt,
+                  int64_t* recv_cnt, int64_t* send_nat, int64_t* recv_nat, int64_t* nsend, int64_t* nrecv);
+
+int mcx_init(const mcx_opts* o, int rank, int nranks, const void* comm_id, void** ctx);
+int mcx_finalize(void* ctx);
+int mcx_get_info(void* ctx, mcx_info* info);
+
+/* Gauss-point constitutive model (micropp_C_material_set(id,E,nu,Sy,Ka,type)) */
+int mcx_material_set(void* ctx, int id, double E, double nu, double Sy, double Ka, int type);
+
+double mcx_get_displacement(void* ctx, int time_s);
+int mcx_zero_u(void* ctx);                 /* VecZeroEntries(u)  src/init.c:103 */
+int mcx_apply_bc_u(void* ctx, double U);
+int mcx_set_strains(void* ctx);
+int mcx_homogenize(void* ctx);
+int mcx_assembly_res(void* ctx, double* norm2);
+int mcx_assembly_jac(void* ctx);
+int mcx_solve(void* ctx, int* its, double* rnorm, int* reason);
+int mcx_update_u(void* ctx);
+
+/* src/main.c:57-82 for one time step; returns Newton iterations done, per-iteration
+   |RES|, KSP its and KSP rnorm in caller arrays of length >= newton_max_its (may be NULL) */
+int mcx_time_step(void* ctx, int time_s, int* newton_its, double* res, int* ksp_its, double* ksp_rnorm);
+
+/* ---- data access (owned rows, PETSc-local order, host buffers) ---- */
+int mcx_get_u(void* ctx, double* host);      /* ndofs_local */
+int mcx_set_u(void* ctx, const double* host);
+int mcx_get_b(void* ctx, double* host);
+int mcx_get_du(void* ctx, double* host);
+/* strains / stresses of the PETSc-owned elements, [ie*8+gp][6] (micropp gp index) */
+int mcx_get_strain(void* ctx, double* host);
+int mcx_get_stress(void* ctx, double* host);
+/* global PETSc DOF of every owned local DOF, and its natural (i + j*NX + k*NX*NY)*3+d index */
+int mcx_owned_dofs(void* ctx, int64_t* petsc, int64_t* natural);
+/* owned rows of A in AIJ form: rowptr (ndofs_local+1, local offsets), global column ids
+   sorted ascending, values (any pointer may be NULL) */
+int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals);
+/* sorted global PETSc ids of the owned Dirichlet DOFs; *n in: capacity, out: count */
+int mcx_dump_dirichlet(void* ctx, int64_t* idx, int64_t* n);
+/* y = A x on owned rows (collective when nranks > 1) */
+int mcx_spmv(void* ctx, const double* x_host, double* y_host);
+/* KSP residual history of the last solve (ksp_monitor); *n in: capacity, out: count */
+int mcx_get_ksp_history(void* ctx, double* hist, int64_t* n);
+
+int mcx_set_timing(void* ctx, int on);
+int mcx_get_timing(void* ctx, mcx_timing* t);
+int mcx_synchronize(void* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

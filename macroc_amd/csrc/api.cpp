@@ -1,0 +1,757 @@
+// api.cpp — C-ABI (include/macroc_amd.h) of the MI355X MacroC Newton inner loop.
+// Host control mirrors the reference driver (src/main.c:49-109); all numerics run in the
+// HIP kernels of kernels.hip on the context's stream.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "mcx_internal.h"
+
+namespace mcx {
+
+static thread_local std::string g_err;
+void set_error(const std::string& s) { g_err = s; }
+
+template <class T>
+static int dalloc(Ctx& c, T** p, int64_t n) {
+  if (n <= 0) n = 1;
+  MCX_HIP(hipMalloc((void**)p, sizeof(T) * n));
+  MCX_HIP(hipMemsetAsync(*p, 0, sizeof(T) * n, c.stream));
+  c.device_bytes += (int64_t)sizeof(T) * n;
+  return 0;
+}
+
+static void elastic_C(double E, double nu, double C[36]) {
+  const double lam = E * nu / ((1. + nu) * (1. - 2. * nu));
+  const double mu = E / (2. * (1. + nu));
+  for (int q = 0; q < 36; q++) C[q] = 0.;
+  for (int a = 0; a < 3; a++)
+    for (int b = 0; b < 3; b++) C[a * 6 + b] = lam + (a == b ? 2. * mu : 0.);
+  for (int a = 3; a < 6; a++) C[a * 6 + a] = mu;
+}
+
+struct PhaseTimer {
+  Ctx& c;
+  double* out;
+  PhaseTimer(Ctx& cc, double* o) : c(cc), out(o) {
+    if (c.timing) (void)hipEventRecord(c.ev_a, c.stream);
+  }
+  ~PhaseTimer() {
+    if (!c.timing) return;
+    (void)hipEventRecord(c.ev_b, c.stream);
+    (void)hipEventSynchronize(c.ev_b);
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, c.ev_a, c.ev_b);
+    *out = ms;
+  }
+};
+
+static int free_ctx(Ctx* c) {
+  if (!c) return 0;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  void* ptrs[] = {c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->V, c->eps, c->sig, c->ctan,
+                  c->Ke, c->be, c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
+                  c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (c->h_cg) (void)hipHostFree(c->h_cg);
+  for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+  if (c->ev_a) (void)hipEventDestroy(c->ev_a);
+  if (c->ev_b) (void)hipEventDestroy(c->ev_b);
+  for (int q = 0; q < 2; q++)
+    if (c->ev_chunk[q]) (void)hipEventDestroy(c->ev_chunk[q]);
+  comm_destroy(*c);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return 0;
+}
+
+static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void* comm_id) {
+  c.o = *o;
+  c.rank = rank;
+  c.nranks = nranks;
+  int ndev = 0;
+  MCX_HIP(hipGetDeviceCount(&ndev));
+  if (ndev <= 0) {
+    set_error("no HIP device visible");
+    return 11;
+  }
+  c.device = o->device >= 0 ? o->device : rank % ndev;
+  MCX_HIP(hipSetDevice(c.device));
+  int rc = setup_decomposition(c);
+  if (rc) return rc;
+  MCX_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+  MCX_HIP(hipEventCreate(&c.ev_a));
+  MCX_HIP(hipEventCreate(&c.ev_b));
+  for (int q = 0; q < 2; q++) MCX_HIP(hipEventCreateWithFlags(&c.ev_chunk[q], hipEventDisableTiming));
+  if ((rc = comm_init(c, comm_id))) return rc;
+  if ((rc = build_halo_plan(c))) return rc;
+  if ((rc = upload_constants(c))) return rc;
+  const Geo& g = c.g;
+  const int64_t npad = (int64_t)g.PX * g.PY * g.PZ * 3, nown3 = 3 * (int64_t)g.nown, E = g.nelem;
+  if ((rc = dalloc(c, &c.u_pad, npad)) || (rc = dalloc(c, &c.p_pad, npad)) || (rc = dalloc(c, &c.b, nown3)) ||
+      (rc = dalloc(c, &c.du, nown3)) || (rc = dalloc(c, &c.r, nown3)) || (rc = dalloc(c, &c.z, nown3)) ||
+      (rc = dalloc(c, &c.w, nown3)) || (rc = dalloc(c, &c.dinv, nown3)) || (rc = dalloc(c, &c.tmp, nown3)) ||
+      (rc = dalloc(c, &c.V, c.ngroups * NPAIR * 128)) || (rc = dalloc(c, &c.eps, 6 * 8 * E)) ||
+      (rc = dalloc(c, &c.sig, 6 * 8 * E)) || (rc = dalloc(c, &c.ctan, 36 * 8 * E)) ||
+      (rc = dalloc(c, &c.Ke, (int64_t)NKE * E)) || (rc = dalloc(c, &c.be, 24 * E)) ||
+      (rc = dalloc(c, &c.partials, 2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64)) ||
+      (rc = dalloc(c, &c.red, 16)) || (rc = dalloc(c, &c.red_loc, 16)) || (rc = dalloc(c, &c.cg, 1)) ||
+      (rc = dalloc(c, &c.hist, (int64_t)o->ksp_max_it + 2)))
+    return rc;
+  MCX_HIP(hipHostMalloc((void**)&c.h_cg, sizeof(CgState) * 2, hipHostMallocDefault));
+  std::memset(c.h_cg, 0, sizeof(CgState) * 2);
+  c.mat.kind = MCX_MAT_ELASTIC;
+  c.mat.E = o->micro_mat_1[0];
+  c.mat.nu = o->micro_mat_1[1];
+  elastic_C(c.mat.E, c.mat.nu, c.mat.C);
+  c.nnz_local = count_nnz_rows(c, g.xs, g.ys, g.zs, g.nx, g.ny, g.nz);
+  c.nnz_global = count_nnz_rows(c, 0, 0, 0, o->NX, o->NY, o->NZ);
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  return 0;
+}
+
+// ---------------------------------------------------------------- phases
+static int cg_solve(Ctx& c, int* its, double* rnorm, int* reason) {
+  launch_jacobi(c);  // PCSetUp_Jacobi happens inside KSPSolve in the reference
+  CgState s{};
+  s.rtol = c.o.ksp_rtol;
+  s.abstol = c.o.ksp_abstol;
+  s.dtol = c.o.ksp_dtol;
+  s.maxits = c.o.ksp_max_it;
+  s.hist_on = c.o.ksp_monitor ? 1 : 0;
+  c.h_cg[0] = s;
+  MCX_HIP(hipMemcpyAsync(c.cg, &c.h_cg[0], sizeof(CgState), hipMemcpyHostToDevice, c.stream));
+  launch_cg_init(c);
+  int rc = cg_finish_init(c);
+  if (rc) return rc;
+  // spmv event pairs (timing mode): the first kTimed iterations
+  const int kTimed = 256;
+  if (c.timing && c.ev_pool.empty()) {
+    c.ev_pool.resize(2 * kTimed);
+    for (auto& e : c.ev_pool) MCX_HIP(hipEventCreate(&e));
+  }
+  // chunks of CH iterations; the host polls the previous chunk's CgState while the next chunk
+  // runs (kernels of a converged solve return at once)
+  const int CH = 8;
+  int issued = 0, slot = 0, pending = -1;
+  const int cap = c.o.ksp_max_it + 4 * CH;
+  while (true) {
+    for (int q = 0; q < CH; q++, issued++) {
+      hipEvent_t e0 = nullptr, e1 = nullptr;
+      if (c.timing && issued < kTimed) {
+        e0 = c.ev_pool[2 * issued];
+        e1 = c.ev_pool[2 * issued + 1];
+      }
+      if ((rc = cg_iteration(c, e0, e1))) return rc;
+    }
+    MCX_HIP(hipMemcpyAsync(&c.h_cg[slot], c.cg, sizeof(CgState), hipMemcpyDeviceToHost, c.stream));
+    MCX_HIP(hipEventRecord(c.ev_chunk[slot], c.stream));
+    if (pending >= 0) {
+      MCX_HIP(hipEventSynchronize(c.ev_chunk[pending]));
+      if (c.h_cg[pending].reason) break;
+    }
+    pending = slot;
+    slot ^= 1;
+    if (issued > cap) break;
+  }
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  CgState fin;
+  MCX_HIP(hipMemcpy(&fin, c.cg, sizeof(CgState), hipMemcpyDeviceToHost));
+  if (!fin.reason) {
+    set_error("CG loop ended without a converged reason");
+    return 30;
+  }
+  *its = fin.its;
+  *rnorm = fin.dp;
+  *reason = fin.reason;
+  c.last_its = fin.its;
+  if (c.o.ksp_monitor) {
+    c.last_hist.resize(fin.its + 1);
+    MCX_HIP(hipMemcpy(c.last_hist.data(), c.hist, sizeof(double) * (fin.its + 1), hipMemcpyDeviceToHost));
+  }
+  if (c.timing) {
+    int n = std::min(fin.its, std::min(issued, kTimed));
+    double tot = 0.;
+    for (int q = 0; q < n; q++) {
+      float ms = 0.f;
+      MCX_HIP(hipEventElapsedTime(&ms, c.ev_pool[2 * q], c.ev_pool[2 * q + 1]));
+      tot += ms;
+    }
+    c.t.spmv_launches = n;
+    c.t.spmv_ms_total = tot;
+  }
+  return 0;
+}
+
+}  // namespace mcx
+
+using namespace mcx;
+
+#define CTX(p) Ctx& c = *reinterpret_cast<Ctx*>(p)
+#define GUARD(p)                      \
+  if (!(p)) {                         \
+    set_error("null context");        \
+    return 1;                         \
+  }                                   \
+  MCX_HIP(hipSetDevice(reinterpret_cast<Ctx*>(p)->device))
+
+extern "C" {
+
+const char* mcx_last_error(void) { return g_err.c_str(); }
+const char* mcx_version(void) { return "macroc_amd 0.1 (gfx950)"; }
+
+void mcx_default_opts(mcx_opts* o) {
+  std::memset(o, 0, sizeof(*o));
+  o->NX = 40;  // include/macroc.h:44-46
+  o->NY = 3;
+  o->NZ = 40;
+  o->lx = 50.0;  // include/macroc.h:47-49
+  o->ly = 1.0;
+  o->lz = 50.0;
+  o->dt = 0.001;
+  o->final_time = 1.0;
+  o->ts = 1;
+  o->vtu_freq = -1;
+  o->bc_type = MCX_BC_CIRCLE;  // src/init.c:64
+  o->rad = 1.0;
+  o->newton_max_its = 5;
+  o->newton_min_tol = 1.0e-1;
+  o->newton_rel_tol = 1.0e-4;
+  o->ksp_rtol = 1.0e-5;  // src/init.c:147-148
+  o->ksp_abstol = 1.0e-50;
+  o->ksp_dtol = 1.0e4;
+  o->ksp_max_it = 10000;
+  o->micro_n = 2;
+  o->micro_type = 1;
+  const double mat[4] = {1.0e7, 0.25, 1.0e4, 1.0e7};  // src/init.c:31-32
+  std::memcpy(o->micro_mat_1, mat, sizeof(mat));
+  std::memcpy(o->micro_mat_2, mat, sizeof(mat));
+  o->device = -1;
+}
+
+int mcx_parse_args(mcx_opts* o, int argc, const char* const* argv) {
+  for (int a = 0; a < argc; a++) {
+    const char* k = argv[a];
+    const char* v = (a + 1 < argc) ? argv[a + 1] : nullptr;
+    auto I = [&](const char* name, auto* f) {
+      if (std::strcmp(k, name)) return false;
+      if (!v) return false;
+      *f = (std::remove_reference_t<decltype(*f)>)std::atoll(v);
+      a++;
+      return true;
+    };
+    auto D = [&](const char* name, double* f) {
+      if (std::strcmp(k, name)) return false;
+      if (!v) return false;
+      *f = std::atof(v);
+      a++;
+      return true;
+    };
+    auto A4 = [&](const char* name, double* f) {
+      if (std::strcmp(k, name)) return false;
+      if (!v) return false;
+      std::string s(v);
+      size_t pos = 0;
+      for (int q = 0; q < 4 && pos <= s.size(); q++) {
+        size_t e = s.find(',', pos);
+        f[q] = std::atof(s.substr(pos, e == std::string::npos ? std::string::npos : e - pos).c_str());
+        if (e == std::string::npos) break;
+        pos = e + 1;
+      }
+      a++;
+      return true;
+    };
+    if (I("-da_grid_x", &o->NX) || I("-da_grid_y", &o->NY) || I("-da_grid_z", &o->NZ) ||
+        I("-da_processors_x", &o->px) || I("-da_processors_y", &o->py) || I("-da_processors_z", &o->pz) ||
+        D("-lx", &o->lx) || D("-ly", &o->ly) || D("-lz", &o->lz) || D("-dt", &o->dt) || I("-ts", &o->ts) ||
+        I("-vtu_freq", &o->vtu_freq) || I("-bc_type", &o->bc_type) || I("-newton_max_its", &o->newton_max_its) ||
+        D("-newton_min_tol", &o->newton_min_tol) || D("-newton_rel_tol", &o->newton_rel_tol) ||
+        D("-ksp_rtol", &o->ksp_rtol) || D("-ksp_atol", &o->ksp_abstol) || D("-ksp_divtol", &o->ksp_dtol) ||
+        I("-ksp_max_it", &o->ksp_max_it) || I("-micro_n", &o->micro_n) || I("-micro_type", &o->micro_type) ||
+        A4("-micro_mat_1", o->micro_mat_1) || A4("-micro_mat_2", o->micro_mat_2) || I("-device", &o->device))
+      continue;
+    if (!std::strcmp(k, "-ksp_monitor")) {
+      o->ksp_monitor = 1;
+      continue;
+    }
+    if (!std::strcmp(k, "-ksp_type") || !std::strcmp(k, "-pc_type")) {
+      if (v && std::strcmp(v, !std::strcmp(k, "-ksp_type") ? "cg" : "jacobi")) {
+        set_error(std::string("only -ksp_type cg / -pc_type jacobi are implemented, got ") + v);
+        return 2;
+      }
+      a++;
+      continue;
+    }
+    std::fprintf(stderr, "WARNING! There are options you set that were not used: %s\n", k);
+  }
+  return 0;
+}
+
+int mcx_init(const mcx_opts* o, int rank, int nranks, const void* comm_id, void** ctx) {
+  if (!o || !ctx || nranks < 1 || rank < 0 || rank >= nranks) {
+    set_error("mcx_init: bad arguments");
+    return 1;
+  }
+  Ctx* c = new Ctx();
+  int rc = init_ctx(*c, o, rank, nranks, comm_id);
+  if (rc) {
+    std::string e = g_err;
+    free_ctx(c);
+    g_err = e;
+    *ctx = nullptr;
+    return rc;
+  }
+  *ctx = c;
+  return 0;
+}
+
+int mcx_finalize(void* ctx) { return free_ctx(reinterpret_cast<Ctx*>(ctx)); }
+
+static void fill_info(const Ctx& c, mcx_info* in) {
+  const Geo& g = c.g;
+  std::memset(in, 0, sizeof(*in));
+  in->NX = g.NX;
+  in->NY = g.NY;
+  in->NZ = g.NZ;
+  in->px = c.m;
+  in->py = c.n;
+  in->pz = c.p;
+  in->rank = c.rank;
+  in->nranks = c.nranks;
+  in->xs = g.xs;
+  in->ys = g.ys;
+  in->zs = g.zs;
+  in->nx = g.nx;
+  in->ny = g.ny;
+  in->nz = g.nz;
+  in->Xs = std::max(g.xs - 1, 0);
+  in->Ys = std::max(g.ys - 1, 0);
+  in->Zs = std::max(g.zs - 1, 0);
+  in->Nx = std::min(g.xs + g.nx + 1, g.NX) - in->Xs;
+  in->Ny = std::min(g.ys + g.ny + 1, g.NY) - in->Ys;
+  in->Nz = std::min(g.zs + g.nz + 1, g.NZ) - in->Zs;
+  in->ndofs_global = 3 * c.rank_node_off[c.nranks];
+  in->ndofs_local = 3 * (int64_t)g.nown;
+  in->dof_offset = 3 * c.rank_node_off[c.rank];
+  in->nnz_local = c.nnz_local;
+  in->nnz_global = c.nnz_global;
+  int64_t cnt[3];
+  int s[3] = {g.xs, g.ys, g.zs}, w[3] = {g.nx, g.ny, g.nz};
+  for (int d = 0; d < 3; d++) {
+    int lo = s[d] > 0 ? s[d] - 1 : s[d];
+    cnt[d] = std::max(0, s[d] + w[d] - 1 - lo);
+  }
+  in->nelem_local = cnt[0] * cnt[1] * cnt[2];
+  in->nelem_ext = g.nelem;
+  in->dx = g.dx;
+  in->dy = c.dy;
+  in->dz = g.dz;
+  in->wg = g.wg;
+  in->device_bytes = c.device_bytes;
+  in->device = c.device;
+}
+
+
+int mcx_get_info(void* ctx, mcx_info* in) {
+  GUARD(ctx);
+  CTX(ctx);
+  fill_info(c, in);
+  return 0;
+}
+
+int mcx_plan(const mcx_opts* o, int rank, int nranks, mcx_info* in) {
+  if (!o || !in || nranks < 1 || rank < 0 || rank >= nranks) {
+    set_error("mcx_plan: bad arguments");
+    return 1;
+  }
+  Ctx c;
+  c.o = *o;
+  c.rank = rank;
+  c.nranks = nranks;
+  c.device = -1;
+  int rc = setup_decomposition(c);
+  if (rc) return rc;
+  c.nnz_local = count_nnz_rows(c, c.g.xs, c.g.ys, c.g.zs, c.g.nx, c.g.ny, c.g.nz);
+  c.nnz_global = count_nnz_rows(c, 0, 0, 0, o->NX, o->NY, o->NZ);
+  fill_info(c, in);
+  return 0;
+}
+
+int mcx_plan_halo(const mcx_opts* o, int rank, int nranks, int* nnbr, int* nbr_rank, int64_t* send_cnt,
+                  int64_t* recv_cnt, int64_t* send_nat, int64_t* recv_nat, int64_t* nsend, int64_t* nrecv) {
+  if (!o || nranks < 1 || rank < 0 || rank >= nranks) {
+    set_error("mcx_plan_halo: bad arguments");
+    return 1;
+  }
+  Ctx c;
+  c.o = *o;
+  c.rank = rank;
+  c.nranks = nranks;
+  int rc = setup_decomposition(c);
+  if (rc) return rc;
+  std::vector<int> sidx, ridx;
+  plan_halo(c, sidx, ridx);
+  const HaloPlan& h = c.halo;
+  if (nnbr) *nnbr = (int)h.nbr_rank.size();
+  if (nsend) *nsend = h.nsend;
+  if (nrecv) *nrecv = h.nrecv;
+  for (size_t q = 0; q < h.nbr_rank.size(); q++) {
+    if (nbr_rank) nbr_rank[q] = h.nbr_rank[q];
+    if (send_cnt) send_cnt[q] = h.send_cnt[q];
+    if (recv_cnt) recv_cnt[q] = h.recv_cnt[q];
+  }
+  if (send_nat)
+    for (int64_t t = 0; t < h.nsend; t++) send_nat[t] = pad_to_natural(c, sidx[t]);
+  if (recv_nat)
+    for (int64_t t = 0; t < h.nrecv; t++) recv_nat[t] = pad_to_natural(c, ridx[t]);
+  return 0;
+}
+
+int mcx_material_set(void* ctx, int id, double E, double nu, double Sy, double Ka, int type) {
+  GUARD(ctx);
+  CTX(ctx);
+  (void)Sy;
+  (void)Ka;
+  (void)type;
+  if (id == 0) {
+    c.mat.E = E;
+    c.mat.nu = nu;
+    elastic_C(E, nu, c.mat.C);
+  } else if (id == 1 && (E != c.mat.E || nu != c.mat.nu)) {
+    set_error("two distinct materials need the MicroPP micro-structure (out of scope); use equal materials");
+    return 3;
+  }
+  return 0;
+}
+
+double mcx_get_displacement(void* ctx, int time_s) {
+  Ctx& c = *reinterpret_cast<Ctx*>(ctx);
+  // src/bcs.c:52-58 with the missing `return` restored
+  double time = time_s * c.o.dt;
+  return -1.0 * (time / c.o.final_time);
+}
+
+int mcx_zero_u(void* ctx) {
+  GUARD(ctx);
+  CTX(ctx);
+  MCX_HIP(hipMemsetAsync(c.u_pad, 0, sizeof(double) * 3 * (size_t)c.g.PX * c.g.PY * c.g.PZ, c.stream));
+  return 0;
+}
+
+int mcx_apply_bc_u(void* ctx, double U) {
+  GUARD(ctx);
+  CTX(ctx);
+  launch_apply_bc_u(c, U);
+  MCX_HIP(hipGetLastError());
+  return 0;
+}
+
+int mcx_set_strains(void* ctx) {
+  GUARD(ctx);
+  CTX(ctx);
+  PhaseTimer t(c, &c.t.strains_ms);
+  int rc = halo_exchange(c, c.u_pad);  // DMGlobalToLocal (src/assembly.c:40-41)
+  if (rc) return rc;
+  launch_strains(c);
+  MCX_HIP(hipGetLastError());
+  return 0;
+}
+
+int mcx_homogenize(void* ctx) {
+  GUARD(ctx);
+  CTX(ctx);
+  PhaseTimer t(c, &c.t.homogenize_ms);
+  launch_homogenize(c);
+  MCX_HIP(hipGetLastError());
+  return 0;
+}
+
+int mcx_assembly_res(void* ctx, double* norm2) {
+  GUARD(ctx);
+  CTX(ctx);
+  {
+    PhaseTimer t(c, &c.t.residual_ms);
+    launch_residual(c);
+    launch_reduce(c, 1, (int)node_blocks(c), c.red);
+    MCX_HIP(hipGetLastError());
+  }
+  double nrm = 0.;
+  MCX_HIP(hipMemcpyAsync(&c.h_cg[0].dp, c.red, sizeof(double), hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  nrm = c.h_cg[0].dp;
+  if (norm2) *norm2 = nrm;
+  return 0;
+}
+
+int mcx_assembly_jac(void* ctx) {
+  GUARD(ctx);
+  CTX(ctx);
+  PhaseTimer t(c, &c.t.jacobian_ms);
+  launch_element_ke(c);
+  launch_gather_matrix(c);
+  MCX_HIP(hipGetLastError());
+  return 0;
+}
+
+int mcx_solve(void* ctx, int* its, double* rnorm, int* reason) {
+  GUARD(ctx);
+  CTX(ctx);
+  int i0 = 0, r0 = 0;
+  double n0 = 0.;
+  int rc;
+  {
+    PhaseTimer t(c, &c.t.solve_ms);
+    rc = cg_solve(c, &i0, &n0, &r0);
+  }
+  if (rc) return rc;
+  MCX_HIP(hipGetLastError());
+  if (its) *its = i0;
+  if (rnorm) *rnorm = n0;
+  if (reason) *reason = r0;
+  return 0;
+}
+
+int mcx_update_u(void* ctx) {
+  GUARD(ctx);
+  CTX(ctx);
+  PhaseTimer t(c, &c.t.update_ms);
+  launch_update_u(c);
+  MCX_HIP(hipGetLastError());
+  return 0;
+}
+
+int mcx_time_step(void* ctx, int time_s, int* newton_its, double* res, int* ksp_its, double* ksp_rnorm) {
+  GUARD(ctx);
+  CTX(ctx);
+  int rc;
+  double U = mcx_get_displacement(ctx, time_s);
+  if ((rc = mcx_apply_bc_u(ctx, U))) return rc;
+  double norm = 0., norm_0 = 0.;
+  int it = 0;
+  while (it < c.o.newton_max_its) {
+    if ((rc = mcx_set_strains(ctx)) || (rc = mcx_homogenize(ctx)) || (rc = mcx_assembly_res(ctx, &norm))) return rc;
+    if (res) res[it] = norm;
+    if (it == 0) norm_0 = norm;
+    if (norm < c.o.newton_min_tol || norm < norm_0 * c.o.newton_rel_tol) break;
+    int kits = 0, reason = 0;
+    double rn = 0.;
+    if ((rc = mcx_assembly_jac(ctx)) || (rc = mcx_solve(ctx, &kits, &rn, &reason)) || (rc = mcx_update_u(ctx)))
+      return rc;
+    if (ksp_its) ksp_its[it] = kits;
+    if (ksp_rnorm) ksp_rnorm[it] = rn;
+    it++;
+  }
+  if (newton_its) *newton_its = it;
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  return 0;
+}
+
+// ---------------------------------------------------------------- data access
+int mcx_get_u(void* ctx, double* host) {
+  GUARD(ctx);
+  CTX(ctx);
+  launch_copy_pad_to_owned(c, c.u_pad, c.tmp);
+  MCX_HIP(hipMemcpyAsync(host, c.tmp, sizeof(double) * 3 * c.g.nown, hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  return 0;
+}
+
+int mcx_set_u(void* ctx, const double* host) {
+  GUARD(ctx);
+  CTX(ctx);
+  MCX_HIP(hipMemcpyAsync(c.tmp, host, sizeof(double) * 3 * c.g.nown, hipMemcpyHostToDevice, c.stream));
+  launch_copy_owned_to_pad(c, c.tmp, c.u_pad);
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  return 0;
+}
+
+static int get_owned(Ctx& c, const double* d, double* host) {
+  MCX_HIP(hipMemcpyAsync(host, d, sizeof(double) * 3 * c.g.nown, hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  return 0;
+}
+
+int mcx_get_b(void* ctx, double* host) {
+  GUARD(ctx);
+  CTX(ctx);
+  return get_owned(c, c.b, host);
+}
+
+int mcx_get_du(void* ctx, double* host) {
+  GUARD(ctx);
+  CTX(ctx);
+  return get_owned(c, c.du, host);
+}
+
+static int get_gp(Ctx& c, const double* d, double* host) {
+  const Geo& g = c.g;
+  const int64_t E = g.nelem;
+  std::vector<double> all(6 * 8 * E);
+  MCX_HIP(hipMemcpyAsync(all.data(), d, sizeof(double) * all.size(), hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  // PETSc-owned elements: lower-left node in [xs - (xs>0), xe - 2] per direction
+  int lo[3], hi[3], s[3] = {g.xs, g.ys, g.zs}, w[3] = {g.nx, g.ny, g.nz};
+  for (int dd = 0; dd < 3; dd++) {
+    lo[dd] = s[dd] > 0 ? s[dd] - 1 : s[dd];
+    hi[dd] = s[dd] + w[dd] - 2;
+  }
+  int64_t ie = 0;
+  for (int ez = lo[2]; ez <= hi[2]; ez++)
+    for (int ey = lo[1]; ey <= hi[1]; ey++)
+      for (int ex = lo[0]; ex <= hi[0]; ex++, ie++) {
+        int64_t le = (ex - g.ex0) + (int64_t)(ey - g.ey0) * g.nex + (int64_t)(ez - g.ez0) * g.nex * g.ney;
+        for (int gp = 0; gp < 8; gp++)
+          for (int k = 0; k < 6; k++) host[(ie * 8 + gp) * 6 + k] = all[((int64_t)k * 8 + gp) * E + le];
+      }
+  return 0;
+}
+
+int mcx_get_strain(void* ctx, double* host) {
+  GUARD(ctx);
+  CTX(ctx);
+  return get_gp(c, c.eps, host);
+}
+
+int mcx_get_stress(void* ctx, double* host) {
+  GUARD(ctx);
+  CTX(ctx);
+  return get_gp(c, c.sig, host);
+}
+
+int mcx_owned_dofs(void* ctx, int64_t* petsc, int64_t* natural) {
+  GUARD(ctx);
+  CTX(ctx);
+  const Geo& g = c.g;
+  const int64_t off = 3 * c.rank_node_off[c.rank];
+  for (int64_t n = 0; n < g.nown; n++) {
+    int64_t i = n % g.nx, j = (n / g.nx) % g.ny, k = n / ((int64_t)g.nx * g.ny);
+    int64_t nat = (g.xs + i) + (g.ys + j) * (int64_t)g.NX + (g.zs + k) * (int64_t)g.NX * g.NY;
+    for (int d = 0; d < 3; d++) {
+      if (petsc) petsc[3 * n + d] = off + 3 * n + d;
+      if (natural) natural[3 * n + d] = 3 * nat + d;
+    }
+  }
+  return 0;
+}
+
+int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
+  GUARD(ctx);
+  CTX(ctx);
+  const Geo& g = c.g;
+  std::vector<double> V;
+  if (vals) {
+    V.resize(c.ngroups * NPAIR * 128);
+    MCX_HIP(hipMemcpyAsync(V.data(), c.V, sizeof(double) * V.size(), hipMemcpyDeviceToHost, c.stream));
+    MCX_HIP(hipStreamSynchronize(c.stream));
+  }
+  int64_t pos = 0;
+  if (rowptr) rowptr[0] = 0;
+  std::vector<std::pair<int64_t, double>> row;
+  for (int64_t n = 0; n < g.nown; n++) {
+    int64_t i = n % g.nx, j = (n / g.nx) % g.ny, k = n / ((int64_t)g.nx * g.ny);
+    int64_t gi = g.xs + i, gj = g.ys + j, gk = g.zs + k;
+    for (int r = 0; r < 3; r++) {
+      row.clear();
+      for (int nb = 0; nb < 27; nb++) {
+        int64_t hi = gi + nb % 3 - 1, hj = gj + (nb / 3) % 3 - 1, hk = gk + nb / 9 - 1;
+        if (hi < 0 || hj < 0 || hk < 0 || hi >= g.NX || hj >= g.NY || hk >= g.NZ) continue;
+        int64_t col0 = 3 * petsc_node(c, hi, hj, hk);
+        for (int cc = 0; cc < 3; cc++) {
+          double v = 0.;
+          if (vals) {
+            int s = nb * 9 + r * 3 + cc;
+            v = V[(n >> 6) * (NPAIR * 128) + (int64_t)(s >> 1) * 128 + 2 * (n & 63) + (s & 1)];
+          }
+          row.emplace_back(col0 + cc, v);
+        }
+      }
+      std::sort(row.begin(), row.end(), [](auto& a, auto& b) { return a.first < b.first; });
+      for (auto& e : row) {
+        if (colidx) colidx[pos] = e.first;
+        if (vals) vals[pos] = e.second;
+        pos++;
+      }
+      if (rowptr) rowptr[3 * n + r + 1] = pos;
+    }
+  }
+  return 0;
+}
+
+int mcx_dump_dirichlet(void* ctx, int64_t* idx, int64_t* n) {
+  GUARD(ctx);
+  CTX(ctx);
+  const Geo& g = c.g;
+  const int64_t off = 3 * c.rank_node_off[c.rank];
+  int64_t cnt = 0;
+  for (int64_t q = 0; q < g.nown; q++) {
+    int i = (int)(q % g.nx), j = (int)((q / g.nx) % g.ny), k = (int)(q / ((int64_t)g.nx * g.ny));
+    int m = dirichlet_mask_host(g, g.xs + i, g.ys + j, g.zs + k);
+    for (int d = 0; d < 3; d++)
+      if (m >> d & 1) {
+        if (idx && cnt < *n) idx[cnt] = off + 3 * q + d;
+        cnt++;
+      }
+  }
+  if (idx && cnt > *n) {
+    *n = cnt;
+    set_error("mcx_dump_dirichlet: capacity too small");
+    return 4;
+  }
+  *n = cnt;
+  return 0;
+}
+
+int mcx_spmv(void* ctx, const double* x_host, double* y_host) {
+  GUARD(ctx);
+  CTX(ctx);
+  MCX_HIP(hipMemcpyAsync(c.tmp, x_host, sizeof(double) * 3 * c.g.nown, hipMemcpyHostToDevice, c.stream));
+  launch_copy_owned_to_pad(c, c.tmp, c.p_pad);
+  int rc = halo_exchange(c, c.p_pad);
+  if (rc) return rc;
+  launch_spmv(c, c.p_pad, c.tmp, false, false);
+  MCX_HIP(hipGetLastError());
+  MCX_HIP(hipMemcpyAsync(y_host, c.tmp, sizeof(double) * 3 * c.g.nown, hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  return 0;
+}
+
+int mcx_get_ksp_history(void* ctx, double* hist, int64_t* n) {
+  GUARD(ctx);
+  CTX(ctx);
+  int64_t have = (int64_t)c.last_hist.size();
+  int64_t k = std::min(have, *n);
+  if (hist) std::memcpy(hist, c.last_hist.data(), sizeof(double) * k);
+  *n = have;
+  return 0;
+}
+
+int mcx_set_timing(void* ctx, int on) {
+  GUARD(ctx);
+  CTX(ctx);
+  c.timing = on != 0;
+  return 0;
+}
+
+int mcx_get_timing(void* ctx, mcx_timing* t) {
+  GUARD(ctx);
+  CTX(ctx);
+  *t = c.t;
+  // algorithmic bytes of one SpMV in this format: the stencil-block values actually present
+  // (AIJ nonzeros of the owned rows x 8 B), x read once, y written once
+  t->spmv_bytes_per_launch = c.nnz_local * 8 + 2 * 3 * (int64_t)c.g.nown * 8;
+  return 0;
+}
+
+int mcx_synchronize(void* ctx) {
+  GUARD(ctx);
+  CTX(ctx);
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  return 0;
+}
+
+}  // extern "C"

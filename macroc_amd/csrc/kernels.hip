@@ -1,0 +1,798 @@
+// kernels.hip — gfx950 kernels of the MacroC Newton inner loop.
+//
+// HBM layout (one rank = one GPU subdomain):
+//   * node vectors u, p: padded ghosted box [PX*PY*PZ][3] (1 ghost layer, zeros outside
+//     the physical domain) — stencil kernels never branch on the boundary;
+//   * owned vectors b, du, r, z, w, dinv: PETSc-local order [nx*ny*nz][3];
+//   * matrix: "stencil blocks" — for every owned node the 27 neighbour 3x3 blocks (243
+//     slots, slot = nb*9 + r*3 + c, nb = (dz+1)*9 + (dy+1)*3 + (dx+1)); stored AoSoA as
+//     [node/64][122 slot pairs][node%64] double2 so one wave reads 1 KiB contiguous per load.
+//     The column of a slot is implicit (DMDA box stencil), so no index array is read;
+//   * Gauss-point arrays: [component][gp][element] (element fastest, coalesced).
+// Compiled with -ffp-contract=off: each product / sum is rounded as the reference writes it,
+// so element kinematics, strains, stresses, element matrices, the assembled matrix, the
+// residual and the SpMV are bit-identical to the CPU restatement on one rank.
+#include <cmath>
+
+#include "mcx_internal.h"
+
+namespace mcx {
+
+__constant__ double cB[8][6][24];
+
+static constexpr int TPB = 256;
+
+// ---------------------------------------------------------------------------- helpers
+__device__ __forceinline__ void node_ijk(const Geo& g, int n, int& i, int& j, int& k) {
+  i = n % g.nx;
+  int t = n / g.nx;
+  j = t % g.ny;
+  k = t / g.ny;
+}
+
+__device__ __forceinline__ int pad_of(const Geo& g, int i, int j, int k) {
+  return (i + 1) + (j + 1) * g.PX + (k + 1) * g.PX * g.PY;
+}
+
+// Dirichlet DOFs of a global node as a bit mask (bit d = DOF d).  The union over ranks of
+// bc_init_circle's ghost-corner lists (src/bcs.c:254-338) is exactly: the four y=0 edges,
+// all DOFs; dof 1 of the y=LY nodes inside the load circle (cell-centre offset dx/2, :324-327).
+// bc_init_bending (:198-251): faces x=0 and x=LX, all DOFs.
+__host__ __device__ inline int dirichlet_mask(const Geo& g, int gi, int gj, int gk) {
+  if (g.bc_type == MCX_BC_CIRCLE) {
+    if (gj == 0 && (gi == 0 || gi == g.NX - 1 || gk == 0 || gk == g.NZ - 1)) return 7;
+    if (gj == g.NY - 1) {
+      double x = g.lx / 2. - ((double)gi * g.dx + g.dx / 2.);
+      double z = g.lz / 2. - ((double)gk * g.dz + g.dz / 2.);
+      if ((x * x + z * z) < (g.rad * g.rad)) return 2;
+    }
+    return 0;
+  }
+  if (g.bc_type == MCX_BC_BENDING) return (gi == 0 || gi == g.NX - 1) ? 7 : 0;
+  return 0;
+}
+
+// local Q1 node number of offset (ox,oy,oz) in {0,1}^3: order ---,+--,++-,-+-,--+,+-+,+++,-++
+__device__ __forceinline__ int q1_local(int ox, int oy, int oz) {
+  return 4 * oz + (oy ? (ox ? 2 : 3) : (ox ? 1 : 0));
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// deterministic block sum (fixed tree); result valid in thread 0
+template <int NT>
+__device__ __forceinline__ double block_sum(double v, double* sh) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  double r = 0.;
+  if (threadIdx.x == 0) {
+    for (int q = 0; q < NT / 64; q++) r += sh[q];
+  }
+  __syncthreads();
+  return r;
+}
+
+// XCD-aware remap: consecutive logical blocks land on one XCD (its L2 sees the stencil
+// neighbours' x lines); observed dispatch is round-robin over the 8 XCDs (speed only).
+__device__ __forceinline__ int xcd_remap(int b, int nblk_padded) {
+  const int per = nblk_padded >> 3;
+  return (b & 7) * per + (b >> 3);
+}
+
+static inline int64_t pad8(int64_t n) { return (n + 7) / 8 * 8; }
+
+// ---------------------------------------------------------------------------- BC on u
+// apply_bc_on_u -> bc_apply_on_u_circle / _bending (src/bcs.c:29-146)
+__global__ void k_apply_bc_u(Geo g, double* __restrict__ u, double U) {
+  int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  int gi = g.xs + i, gj = g.ys + j, gk = g.zs + k;
+  int m = dirichlet_mask(g, gi, gj, gk);
+  if (!m) return;
+  int pc = pad_of(g, i, j, k);
+  for (int d = 0; d < 3; d++) {
+    if (!(m >> d & 1)) continue;
+    double v;
+    if (g.bc_type == MCX_BC_CIRCLE) v = (m == 2) ? U : 0.;
+    else v = (gi == g.NX - 1 && d == 1) ? U : 0.;
+    u[3 * pc + d] = v;
+  }
+}
+
+// ---------------------------------------------------------------------------- strains
+// set_strains (src/assembly.c:25-66): eps_gp = B_gp . u_e; zero B entries skipped (adding
+// +-0 is exact, so the sum is bit-identical to the reference's full 24-term loop).
+__global__ void k_strains(Geo g, const double* __restrict__ u, double* __restrict__ eps) {
+  int64_t le = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (le >= g.nelem) return;
+  int lex = (int)(le % g.nex), t = (int)(le / g.nex), ley = t % g.ney, lez = t / g.ney;
+  int ex = g.ex0 + lex, ey = g.ey0 + ley, ez = g.ez0 + lez;
+  const int PXY = g.PX * g.PY;
+  int p0 = (ex - g.xs + 1) + (ey - g.ys + 1) * g.PX + (ez - g.zs + 1) * PXY;
+  const int noff[8] = {0, 1, 1 + g.PX, g.PX, PXY, 1 + PXY, 1 + g.PX + PXY, g.PX + PXY};
+  double ue[24];
+#pragma unroll
+  for (int a = 0; a < 8; a++)
+#pragma unroll
+    for (int d = 0; d < 3; d++) ue[3 * a + d] = u[3 * (p0 + noff[a]) + d];
+  const int64_t E = g.nelem;
+#pragma unroll
+  for (int gp = 0; gp < 8; gp++) {
+#pragma unroll
+    for (int kk = 0; kk < 6; kk++) {
+      double s = 0.;
+#pragma unroll
+      for (int jj = 0; jj < 24; jj++) {
+        const int d = jj % 3;
+        const bool nz = (kk < 3) ? (d == kk) : (kk == 3 ? d != 2 : (kk == 4 ? d != 1 : d != 0));
+        if (nz) s += cB[gp][kk][jj] * ue[jj];
+      }
+      eps[((int64_t)kk * 8 + gp) * E + le] = s;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- material
+// Gauss-point callback, isotropic linear elastic (MicroPP surrogate): sigma = C eps,
+// ctan = C, per Gauss point (micropp_C_homogenize / get_stress3 / get_ctan3).
+__global__ void k_homogenize_elastic(int64_t ngp, Material mat, const double* __restrict__ eps,
+                                     double* __restrict__ sig, double* __restrict__ ctan) {
+  int64_t q = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (q >= ngp) return;
+  double e[6];
+#pragma unroll
+  for (int l = 0; l < 6; l++) e[l] = eps[l * ngp + q];
+#pragma unroll
+  for (int k = 0; k < 6; k++) {
+    double s = 0.;
+#pragma unroll
+    for (int l = 0; l < 6; l++) s += mat.C[k * 6 + l] * e[l];
+    sig[k * ngp + q] = s;
+  }
+#pragma unroll
+  for (int kl = 0; kl < 36; kl++) ctan[kl * ngp + q] = mat.C[kl];
+}
+
+// ---------------------------------------------------------------------------- residual
+// assembly_res (src/assembly.c:142-154): be[i] += B[j][i] * sigma[j] * wg, gp outer, j inner
+__global__ void k_element_res(Geo g, const double* __restrict__ sig, double* __restrict__ be) {
+  int64_t le = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (le >= g.nelem) return;
+  const int64_t E = g.nelem, NG = 8 * E;
+  double acc[24];
+#pragma unroll
+  for (int i = 0; i < 24; i++) acc[i] = 0.;
+#pragma unroll
+  for (int gp = 0; gp < 8; gp++) {
+    double s[6];
+#pragma unroll
+    for (int jj = 0; jj < 6; jj++) s[jj] = sig[jj * NG + gp * E + le];
+#pragma unroll
+    for (int i = 0; i < 24; i++) {
+      const int d = i % 3;
+#pragma unroll
+      for (int jj = 0; jj < 6; jj++) {
+        const bool nz = (jj < 3) ? (d == jj) : (jj == 3 ? d != 2 : (jj == 4 ? d != 1 : d != 0));
+        if (nz) acc[i] += cB[gp][jj][i] * s[jj] * g.wg;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 24; i++) be[i * E + le] = acc[i];
+}
+
+// b_node = sum over adjacent elements in ascending element order (the order the reference's
+// element loop adds into b_loc, :156-161), Dirichlet rows zeroed (apply_bc_on_res), then
+// VecScale(b,-1) (:171-173).  Emits per-block partial sums of b.b for VecNorm.
+__global__ __launch_bounds__(TPB) void k_gather_res(Geo g, const double* __restrict__ be, double* __restrict__ b,
+                                                    double* __restrict__ part) {
+  __shared__ double sh[TPB / 64];
+  int n = blockIdx.x * TPB + threadIdx.x;
+  double nrm = 0.;
+  if (n < g.nown) {
+    int i, j, k;
+    node_ijk(g, n, i, j, k);
+    int gi = g.xs + i, gj = g.ys + j, gk = g.zs + k;
+    double acc[3] = {0., 0., 0.};
+    for (int ez = gk - 1; ez <= gk; ez++) {
+      if (ez < 0 || ez > g.NZ - 2) continue;
+      for (int ey = gj - 1; ey <= gj; ey++) {
+        if (ey < 0 || ey > g.NY - 2) continue;
+        for (int ex = gi - 1; ex <= gi; ex++) {
+          if (ex < 0 || ex > g.NX - 2) continue;
+          int64_t le = (ex - g.ex0) + (int64_t)(ey - g.ey0) * g.nex + (int64_t)(ez - g.ez0) * g.nex * g.ney;
+          int a = q1_local(gi - ex, gj - ey, gk - ez);
+#pragma unroll
+          for (int r = 0; r < 3; r++) acc[r] += be[(3 * a + r) * g.nelem + le];
+        }
+      }
+    }
+    int m = dirichlet_mask(g, gi, gj, gk);
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+      double v = (m >> r & 1) ? 0. : acc[r];
+      v = v * -1.;
+      b[3 * n + r] = v;
+      nrm += v * v;
+    }
+  }
+  double s = block_sum<TPB>(nrm, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// ---------------------------------------------------------------------------- Jacobian
+// assembly_jac's 4-nest (src/assembly.c:94-99): Ke[i][j] += B[k][i]*C[k][l]*B[l][j]*wg with
+// gp, k, l ascending, evaluated as ((B*C)*B)*wg.  One thread = (element, node a, half of the
+// column nodes b): 4 column blocks x 9 = 36 accumulators.  Zero B terms are skipped (exact).
+// Grid: blocks b -> (XCD group, a, half, element group) so the 16 blocks that read one
+// element group's ctan share an XCD's L2.
+__constant__ int cK[3][3] = {{0, 3, 4}, {1, 3, 5}, {2, 4, 5}};  // rows k with B[k][3a+r] != 0
+
+template <int BH>
+__device__ __forceinline__ void ke_body(const Geo& g, int64_t le, int a, const double* __restrict__ ctan,
+                                        double* __restrict__ Ke) {
+  const int64_t E = g.nelem, NG = 8 * E;
+  double acc[4][9];
+#pragma unroll
+  for (int bb = 0; bb < 4; bb++)
+#pragma unroll
+    for (int q = 0; q < 9; q++) acc[bb][q] = 0.;
+  const double wg = g.wg;
+  for (int gp = 0; gp < 8; gp++) {
+    // B[k][3a+r] for the 9 non-zero (r,k): wave-uniform scalar loads
+    double Ba[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+      for (int kq = 0; kq < 3; kq++) Ba[r][kq] = cB[gp][cK[r][kq]][3 * a + r];
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+#pragma unroll
+      for (int l = 0; l < 6; l++) {
+        const double Ckl = ctan[(k * 6 + l) * NG + gp * E + le];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+          // position of k in K(r), compile-time
+          const int kq = (k == r) ? 0 : ((k == 3 || (k == 4 && r == 2)) ? 1 : 2);
+          const bool krow = (k == r) || (r == 0 && (k == 3 || k == 4)) || (r == 1 && (k == 3 || k == 5)) ||
+                            (r == 2 && (k == 4 || k == 5));
+          if (!krow) continue;
+          const double t0 = Ba[r][kq] * Ckl;
+#pragma unroll
+          for (int c = 0; c < 3; c++) {
+            const bool lcol = (l == c) || (c == 0 && (l == 3 || l == 4)) || (c == 1 && (l == 3 || l == 5)) ||
+                              (c == 2 && (l == 4 || l == 5));
+            if (!lcol) continue;
+#pragma unroll
+            for (int bb = 0; bb < 4; bb++) {
+              const int bnode = BH * 4 + bb;
+              acc[bb][r * 3 + c] += t0 * cB[gp][l][3 * bnode + c] * wg;
+            }
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int bb = 0; bb < 4; bb++) {
+    const int bnode = BH * 4 + bb;
+#pragma unroll
+    for (int q = 0; q < 9; q++) Ke[((int64_t)(a * 8 + bnode) * 9 + q) * E + le] = acc[bb][q];
+  }
+}
+
+__global__ __launch_bounds__(TPB) void k_element_ke(Geo g, const double* __restrict__ ctan, double* __restrict__ Ke,
+                                                    int64_t ngroups) {
+  // block -> (xcd, a, half, element group): blocks sharing an element group are 8 apart
+  const int64_t b = blockIdx.x;
+  const int x = (int)(b & 7);
+  const int64_t t = b >> 3;
+  const int ah = (int)(t & 15);
+  const int64_t grp = (t >> 4) * 8 + x;
+  if (grp >= ngroups) return;
+  const int64_t le = grp * TPB + threadIdx.x;
+  if (le >= g.nelem) return;
+  const int a = ah >> 1;
+  if (ah & 1) ke_body<1>(g, le, a, ctan, Ke);
+  else ke_body<0>(g, le, a, ctan, Ke);
+}
+
+// MatSetValuesLocal(ADD) + MatAssembly + MatZeroRowsColumns(diag=1) (src/assembly.c:106-112,
+// src/bcs.c:341-347) as a deterministic gather: thread = (owned node, neighbour block nb);
+// the 9 entries are 0 + Ke_e1 + Ke_e2 + ... over the shared elements in ascending element
+// order (the reference's insertion order on one rank), then Dirichlet rows/columns.
+__global__ __launch_bounds__(TPB) void k_gather_matrix(Geo g, const double* __restrict__ Ke, double* __restrict__ V) {
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  const int nb = blockIdx.y;
+  if (n >= g.nown) return;
+  const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  const int gi = g.xs + i, gj = g.ys + j, gk = g.zs + k;
+  const int hi = gi + dx, hj = gj + dy, hk = gk + dz;
+  double val[9];
+#pragma unroll
+  for (int q = 0; q < 9; q++) val[q] = 0.;
+  if (hi >= 0 && hj >= 0 && hk >= 0 && hi < g.NX && hj < g.NY && hk < g.NZ) {
+    for (int ez = gk - 1 + (dz > 0); ez <= gk + (dz < 0 ? -1 : 0); ez++) {
+      if (ez < 0 || ez > g.NZ - 2) continue;
+      for (int ey = gj - 1 + (dy > 0); ey <= gj + (dy < 0 ? -1 : 0); ey++) {
+        if (ey < 0 || ey > g.NY - 2) continue;
+        for (int ex = gi - 1 + (dx > 0); ex <= gi + (dx < 0 ? -1 : 0); ex++) {
+          if (ex < 0 || ex > g.NX - 2) continue;
+          const int64_t le = (ex - g.ex0) + (int64_t)(ey - g.ey0) * g.nex + (int64_t)(ez - g.ez0) * g.nex * g.ney;
+          const int a = q1_local(gi - ex, gj - ey, gk - ez);
+          const int bn = q1_local(hi - ex, hj - ey, hk - ez);
+          const double* src = Ke + (int64_t)((a * 8 + bn) * 9) * g.nelem + le;
+#pragma unroll
+          for (int q = 0; q < 9; q++) val[q] += src[(int64_t)q * g.nelem];
+        }
+      }
+    }
+    const int rm = dirichlet_mask(g, gi, gj, gk), cm = dirichlet_mask(g, hi, hj, hk);
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        if (rm >> r & 1) val[r * 3 + c] = (nb == 13 && r == c) ? 1.0 : 0.0;
+        else if (cm >> c & 1) val[r * 3 + c] = 0.0;
+      }
+  }
+  double* Vg = V + (int64_t)(n >> 6) * (NPAIR * 128) + 2 * (n & 63);
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    const int s = nb * 9 + q;
+    Vg[(s >> 1) * 128 + (s & 1)] = val[q];
+  }
+}
+
+// PCSetUp_Jacobi: diag, VecReciprocal (non-zeros only), zeros -> 1
+__global__ void k_jacobi(Geo g, const double* __restrict__ V, double* __restrict__ dinv) {
+  int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  const double* Vg = V + (int64_t)(n >> 6) * (NPAIR * 128) + 2 * (n & 63);
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const int s = 13 * 9 + r * 4;
+    double d = Vg[(s >> 1) * 128 + (s & 1)];
+    if (d != 0.0) d = 1.0 / d;
+    if (d == 0.0) d = 1.0;
+    dinv[3 * n + r] = d;
+  }
+}
+
+// ---------------------------------------------------------------------------- SpMV
+// y = A x for the owned rows.  One thread = one node = 3 rows; 122 x 16-B coalesced loads of
+// the stencil blocks, x gathered from the padded box (L1/L2 resident neighbours).  Each row
+// sums its slots in ascending (nb, c) = ascending global column on one rank, the order of
+// MatMult_SeqAIJ, so y is bit-identical to the CPU AIJ product.  DOT: per-block p.w.
+template <int S>
+__device__ __forceinline__ void slot_acc(double v, const double (&xv)[27][3], double& y0, double& y1, double& y2) {
+  constexpr int nb = S / 9, r = (S % 9) / 3, c = S % 3;
+  if (r == 0) y0 += v * xv[nb][c];
+  else if (r == 1) y1 += v * xv[nb][c];
+  else y2 += v * xv[nb][c];
+}
+
+template <int Q>
+struct PairLoop {
+  static __device__ __forceinline__ void run(const double2* __restrict__ v, const double (&xv)[27][3], double& y0,
+                                             double& y1, double& y2) {
+    PairLoop<Q - 1>::run(v, xv, y0, y1, y2);
+    const double2 a = v[(Q - 1) * 64];
+    slot_acc<2 * (Q - 1)>(a.x, xv, y0, y1, y2);
+    if constexpr (2 * (Q - 1) + 1 < NSLOT) slot_acc<2 * (Q - 1) + 1>(a.y, xv, y0, y1, y2);
+  }
+};
+template <>
+struct PairLoop<0> {
+  static __device__ __forceinline__ void run(const double2* __restrict__, const double (&)[27][3], double&, double&,
+                                             double&) {}
+};
+
+template <bool DOT, bool GATED>
+__global__ __launch_bounds__(TPB) void k_spmv(Geo g, const double2* __restrict__ V, const double* __restrict__ x,
+                                              double* __restrict__ y, double* __restrict__ part,
+                                              const CgState* __restrict__ cg, int nblk_padded) {
+  __shared__ double sh[TPB / 64];
+  if (GATED && cg->reason) return;
+  const int lb = xcd_remap(blockIdx.x, nblk_padded);
+  const int n = lb * TPB + threadIdx.x;
+  double dot = 0.;
+  if (n < g.nown) {
+    int i, j, k;
+    node_ijk(g, n, i, j, k);
+    const int PX = g.PX, PXY = g.PX * g.PY;
+    const int pc = (i + 1) + (j + 1) * PX + (k + 1) * PXY;
+    double xv[27][3];
+#pragma unroll
+    for (int nb = 0; nb < 27; nb++) {
+      const int off = (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
+      const double* xp = x + 3 * (int64_t)(pc + off);
+      xv[nb][0] = xp[0];
+      xv[nb][1] = xp[1];
+      xv[nb][2] = xp[2];
+    }
+    const double2* v = V + (int64_t)(n >> 6) * (NPAIR * 64) + (n & 63);
+    double y0 = 0., y1 = 0., y2 = 0.;
+    PairLoop<NPAIR>::run(v, xv, y0, y1, y2);
+    y[3 * n + 0] = y0;
+    y[3 * n + 1] = y1;
+    y[3 * n + 2] = y2;
+    if (DOT) dot = xv[13][0] * y0 + xv[13][1] * y1 + xv[13][2] * y2;
+  }
+  if (DOT) {
+    double s = block_sum<TPB>(dot, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+  }
+}
+
+// ---------------------------------------------------------------------------- CG vectors
+// KSPSolve_CG (PETSc, KSP_NORM_PRECONDITIONED, zero guess) + PCApply_Jacobi, with the scalar
+// recurrences kept on the device (CgState) so the host only polls every few iterations.
+__device__ __forceinline__ int converged_default(const CgState* s, double rn) {
+  if (isnan(rn) || isinf(rn)) return MCX_KSP_DIVERGED_NANORINF;
+  if (rn <= s->ttol) return rn < s->abstol ? MCX_KSP_CONVERGED_ATOL : MCX_KSP_CONVERGED_RTOL;
+  if (rn >= s->dtol * s->rnorm0) return MCX_KSP_DIVERGED_DTOL;
+  return 0;
+}
+
+// r <- b; x <- 0; z <- D^-1 r; partials z.z, z.r
+__global__ __launch_bounds__(TPB) void k_cg_init(Geo g, const double* __restrict__ bvec, const double* __restrict__ dinv,
+                                                 double* __restrict__ x, double* __restrict__ r,
+                                                 double* __restrict__ z, double* __restrict__ part, int nparts) {
+  __shared__ double sh[TPB / 64];
+  int n = blockIdx.x * TPB + threadIdx.x;
+  double zz = 0., zr = 0.;
+  if (n < g.nown) {
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      const int q = 3 * n + d;
+      const double rv = bvec[q];
+      const double zv = rv * dinv[q];
+      x[q] = 0.;
+      r[q] = rv;
+      z[q] = zv;
+      zz += zv * zv;
+      zr += zv * rv;
+    }
+  }
+  double s0 = block_sum<TPB>(zz, sh);
+  double s1 = block_sum<TPB>(zr, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = s0;
+    part[nparts + blockIdx.x] = s1;
+  }
+}
+
+// p <- z (i == 0) or z + (beta/betaold) p   (VecCopy / VecAYPX)
+__global__ void k_cg_pupdate(Geo g, const double* __restrict__ z, double* __restrict__ ppad,
+                             const CgState* __restrict__ cg) {
+  if (cg->reason) return;
+  int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  const int pc = pad_of(g, i, j, k);
+  if (cg->i == 0) {
+#pragma unroll
+    for (int d = 0; d < 3; d++) ppad[3 * pc + d] = z[3 * n + d];
+  } else {
+    const double bc = cg->bcoef;
+#pragma unroll
+    for (int d = 0; d < 3; d++) ppad[3 * pc + d] = z[3 * n + d] + bc * ppad[3 * pc + d];
+  }
+}
+
+// x += a p; r += (-a) w; z = D^-1 r; partials z.z, z.r
+__global__ __launch_bounds__(TPB) void k_cg_update(Geo g, const double* __restrict__ ppad, const double* __restrict__ w,
+                                                   const double* __restrict__ dinv, double* __restrict__ x,
+                                                   double* __restrict__ r, double* __restrict__ z,
+                                                   double* __restrict__ part, int nparts,
+                                                   const CgState* __restrict__ cg) {
+  __shared__ double sh[TPB / 64];
+  if (cg->reason) return;
+  const double a = cg->alpha, ma = -a;
+  int n = blockIdx.x * TPB + threadIdx.x;
+  double zz = 0., zr = 0.;
+  if (n < g.nown) {
+    int i, j, k;
+    node_ijk(g, n, i, j, k);
+    const int pc = pad_of(g, i, j, k);
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      const int q = 3 * n + d;
+      x[q] = x[q] + a * ppad[3 * pc + d];
+      const double rv = r[q] + ma * w[q];
+      r[q] = rv;
+      const double zv = rv * dinv[q];
+      z[q] = zv;
+      zz += zv * zv;
+      zr += zv * rv;
+    }
+  }
+  double s0 = block_sum<TPB>(zz, sh);
+  double s1 = block_sum<TPB>(zr, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = s0;
+    part[nparts + blockIdx.x] = s1;
+  }
+}
+
+// CG scalar steps (thread 0 of the reduction block)
+__device__ void cg_logic_init(CgState* s, double zz, double zr, double* hist) {
+  const double dp = sqrt(zz);
+  s->dp = dp;
+  if (s->hist_on) hist[0] = dp;
+  s->ttol = fmax(s->rtol * dp, s->abstol);
+  s->rnorm0 = dp;
+  s->i = 0;
+  s->its = 0;
+  s->dpi = 0.;
+  s->betaold = 0.;
+  s->reason = converged_default(s, dp);
+  if (s->reason) return;
+  s->beta = zr;
+  s->its = 1;
+  if (zr == 0.0) s->reason = MCX_KSP_CONVERGED_ATOL;
+}
+
+__device__ void cg_logic_alpha(CgState* s, double dpi) {
+  if (s->reason) return;
+  const double dpiold = s->dpi;
+  s->dpiold = dpiold;
+  s->dpi = dpi;
+  s->betaold = s->beta;
+  if (dpi == 0.0 || (s->i > 0 && dpi * dpiold <= 0.0)) {
+    s->reason = MCX_KSP_DIVERGED_INDEFINITE_MAT;
+    return;
+  }
+  s->alpha = s->beta / dpi;
+}
+
+__device__ void cg_logic_beta(CgState* s, double zz, double zr, double* hist) {
+  if (s->reason) return;
+  const double dp = sqrt(zz);
+  s->dp = dp;
+  if (s->hist_on) hist[s->i + 1] = dp;
+  int rs = converged_default(s, dp);
+  if (rs) {
+    s->reason = rs;
+    return;
+  }
+  s->beta = zr;
+  s->i += 1;
+  if (s->i >= s->maxits) {
+    s->reason = MCX_KSP_DIVERGED_ITS;
+    return;
+  }
+  s->its = s->i + 1;
+  if (zr == 0.0) {
+    s->reason = MCX_KSP_CONVERGED_ATOL;
+    return;
+  }
+  if (zr * s->betaold < 0.0) {
+    s->reason = MCX_KSP_DIVERGED_INDEFINITE_PC;
+    return;
+  }
+  s->bcoef = zr / s->betaold;
+}
+
+enum { RED_STORE = 0, RED_INIT = 1, RED_ALPHA = 2, RED_BETA = 3, RED_NORM = 4 };
+
+// one block: out[v] = sum_i part[v*nparts + i] (fixed order); then optional CG logic.
+// mode RED_STORE writes the local sums only (an all-reduce + k_cg_logic follows).
+__global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ part, int nparts, int nvals,
+                                                 double* __restrict__ out, int mode, CgState* cg,
+                                                 double* __restrict__ hist, int gated) {
+  __shared__ double sh[16];
+  if (gated && cg->reason) return;
+  double res[2] = {0., 0.};
+  for (int v = 0; v < nvals; v++) {
+    double acc = 0.;
+    for (int q = threadIdx.x; q < nparts; q += 1024) acc += part[(int64_t)v * nparts + q];
+    res[v] = block_sum<1024>(acc, sh);
+  }
+  if (threadIdx.x) return;
+  for (int v = 0; v < nvals; v++) out[v] = res[v];
+  if (mode == RED_INIT) cg_logic_init(cg, res[0], res[1], hist);
+  else if (mode == RED_ALPHA) cg_logic_alpha(cg, res[0]);
+  else if (mode == RED_BETA) cg_logic_beta(cg, res[0], res[1], hist);
+  else if (mode == RED_NORM) out[0] = sqrt(res[0]);
+}
+
+__global__ void k_cg_logic(const double* __restrict__ red, int mode, CgState* cg, double* __restrict__ hist,
+                           double* __restrict__ out) {
+  if (threadIdx.x) return;
+  if (mode == RED_INIT) cg_logic_init(cg, red[0], red[1], hist);
+  else if (mode == RED_ALPHA) cg_logic_alpha(cg, red[0]);
+  else if (mode == RED_BETA) cg_logic_beta(cg, red[0], red[1], hist);
+  else if (mode == RED_NORM) out[0] = sqrt(red[0]);
+}
+
+// ---------------------------------------------------------------------------- misc vectors
+__global__ void k_update_u(Geo g, double* __restrict__ u, const double* __restrict__ du) {
+  int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  const int pc = pad_of(g, i, j, k);
+#pragma unroll
+  for (int d = 0; d < 3; d++) u[3 * pc + d] = u[3 * pc + d] + 1. * du[3 * n + d];
+}
+
+__global__ void k_owned_to_pad(Geo g, const double* __restrict__ src, double* __restrict__ pad) {
+  int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  const int pc = pad_of(g, i, j, k);
+#pragma unroll
+  for (int d = 0; d < 3; d++) pad[3 * pc + d] = src[3 * n + d];
+}
+
+__global__ void k_pad_to_owned(Geo g, const double* __restrict__ pad, double* __restrict__ dst) {
+  int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  const int pc = pad_of(g, i, j, k);
+#pragma unroll
+  for (int d = 0; d < 3; d++) dst[3 * n + d] = pad[3 * pc + d];
+}
+
+__global__ void k_pack(const int* __restrict__ idx, int64_t cnt, const double* __restrict__ pad, double* __restrict__ buf) {
+  int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (t >= cnt) return;
+  const int p = idx[t];
+#pragma unroll
+  for (int d = 0; d < 3; d++) buf[3 * t + d] = pad[3 * (int64_t)p + d];
+}
+
+__global__ void k_unpack(const int* __restrict__ idx, int64_t cnt, const double* __restrict__ buf, double* __restrict__ pad) {
+  int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (t >= cnt) return;
+  const int p = idx[t];
+#pragma unroll
+  for (int d = 0; d < 3; d++) pad[3 * (int64_t)p + d] = buf[3 * t + d];
+}
+
+// ============================================================================ launchers
+static inline unsigned nblk(int64_t n) { return (unsigned)((n + TPB - 1) / TPB); }
+
+int dirichlet_mask_host(const Geo& g, int gi, int gj, int gk) { return dirichlet_mask(g, gi, gj, gk); }
+
+int64_t node_blocks(const Ctx& c) { return nblk(c.g.nown); }
+int64_t spmv_grid_blocks(const Ctx& c) { return pad8(nblk(c.g.nown)); }
+
+int upload_constants(Ctx& c) {
+  double B[8][6][24];
+  compute_B_table(B);
+  MCX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(cB), B, sizeof(B)));
+  return 0;
+}
+
+void launch_apply_bc_u(Ctx& c, double U) {
+  hipLaunchKernelGGL(k_apply_bc_u, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.u_pad, U);
+}
+
+void launch_strains(Ctx& c) {
+  hipLaunchKernelGGL(k_strains, dim3(nblk(c.g.nelem)), dim3(TPB), 0, c.stream, c.g, c.u_pad, c.eps);
+}
+
+void launch_homogenize(Ctx& c) {
+  int64_t ngp = 8 * c.g.nelem;
+  hipLaunchKernelGGL(k_homogenize_elastic, dim3(nblk(ngp)), dim3(TPB), 0, c.stream, ngp, c.mat, c.eps, c.sig, c.ctan);
+}
+
+void launch_residual(Ctx& c) {
+  hipLaunchKernelGGL(k_element_res, dim3(nblk(c.g.nelem)), dim3(TPB), 0, c.stream, c.g, c.sig, c.be);
+  hipLaunchKernelGGL(k_gather_res, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.be, c.b, c.partials);
+}
+
+void launch_element_ke(Ctx& c) {
+  int64_t ngroups = nblk(c.g.nelem);
+  int64_t blocks = pad8(ngroups) * 16;
+  hipLaunchKernelGGL(k_element_ke, dim3((unsigned)blocks), dim3(TPB), 0, c.stream, c.g, c.ctan, c.Ke, ngroups);
+}
+
+void launch_gather_matrix(Ctx& c) {
+  hipLaunchKernelGGL(k_gather_matrix, dim3(nblk(c.g.nown), 27), dim3(TPB), 0, c.stream, c.g, c.Ke, c.V);
+}
+
+void launch_jacobi(Ctx& c) {
+  hipLaunchKernelGGL(k_jacobi, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.V, c.dinv);
+}
+
+void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
+  int nb = (int)spmv_grid_blocks(c);
+  const double2* V = reinterpret_cast<const double2*>(c.V);
+  if (dot && gated)
+    hipLaunchKernelGGL((k_spmv<true, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials, c.cg, nb);
+  else if (dot)
+    hipLaunchKernelGGL((k_spmv<true, false>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials, c.cg, nb);
+  else
+    hipLaunchKernelGGL((k_spmv<false, false>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials, c.cg, nb);
+}
+
+void launch_update_u(Ctx& c) {
+  hipLaunchKernelGGL(k_update_u, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.u_pad, c.du);
+}
+
+void launch_copy_owned_to_pad(Ctx& c, const double* owned, double* pad) {
+  hipLaunchKernelGGL(k_owned_to_pad, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, owned, pad);
+}
+
+void launch_copy_pad_to_owned(Ctx& c, const double* pad, double* owned) {
+  hipLaunchKernelGGL(k_pad_to_owned, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, pad, owned);
+}
+
+void launch_pack(Ctx& c, const double* xpad) {
+  if (!c.halo.nsend) return;
+  hipLaunchKernelGGL(k_pack, dim3(nblk(c.halo.nsend)), dim3(TPB), 0, c.stream, c.halo.d_send_idx, c.halo.nsend, xpad,
+                     c.halo.d_sendbuf);
+}
+
+void launch_unpack(Ctx& c, double* xpad) {
+  if (!c.halo.nrecv) return;
+  hipLaunchKernelGGL(k_unpack, dim3(nblk(c.halo.nrecv)), dim3(TPB), 0, c.stream, c.halo.d_recv_idx, c.halo.nrecv,
+                     c.halo.d_recvbuf, xpad);
+}
+
+// reduce partials into out (and, for RED_NORM, out[0] = sqrt); multi-rank: local sums are
+// all-reduced over RCCL first.
+static int reduce_and_logic(Ctx& c, int nvals, int nparts, int mode, bool gated) {
+  if (c.nranks == 1) {
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, c.stream, c.partials, nparts, nvals, c.red, mode, c.cg, c.hist,
+                       gated ? 1 : 0);
+    return 0;
+  }
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, c.stream, c.partials, nparts, nvals, c.red_loc, (int)RED_STORE,
+                     c.cg, c.hist, gated ? 1 : 0);
+  int rc = allreduce_sum(c, c.red_loc, c.red, nvals);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_cg_logic, dim3(1), dim3(64), 0, c.stream, c.red, mode, c.cg, c.hist, c.red);
+  return 0;
+}
+
+void launch_reduce(Ctx& c, int nvals, int nparts, double* out) {
+  (void)out;
+  reduce_and_logic(c, nvals, nparts, RED_NORM, false);
+}
+
+void launch_cg_init(Ctx& c) {
+  int nb = (int)nblk(c.g.nown);
+  hipLaunchKernelGGL(k_cg_init, dim3(nb), dim3(TPB), 0, c.stream, c.g, c.b, c.dinv, c.du, c.r, c.z, c.partials, nb);
+}
+
+int cg_finish_init(Ctx& c) {
+  int nb = (int)nblk(c.g.nown);
+  return reduce_and_logic(c, 2, nb, RED_INIT, false);
+}
+
+int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1) {
+  const int nbn = (int)nblk(c.g.nown);
+  const int nbs = (int)spmv_grid_blocks(c);
+  hipLaunchKernelGGL(k_cg_pupdate, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.cg);
+  int rc = halo_exchange(c, c.p_pad);
+  if (rc) return rc;
+  if (ev0) MCX_HIP(hipEventRecord(ev0, c.stream));
+  launch_spmv(c, c.p_pad, c.w, true, true);
+  if (ev1) MCX_HIP(hipEventRecord(ev1, c.stream));
+  rc = reduce_and_logic(c, 1, nbs, RED_ALPHA, true);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_cg_update, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.p_pad, c.w, c.dinv, c.du, c.r, c.z,
+                     c.partials, nbn, c.cg);
+  rc = reduce_and_logic(c, 2, nbn, RED_BETA, true);
+  return rc;
+}
+
+}  // namespace mcx

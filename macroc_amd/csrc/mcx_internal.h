@@ -1,0 +1,158 @@
+// mcx_internal.h — context, geometry and kernel-launcher declarations of the MI355X
+// MacroC hot path.  See DESIGN.md for the HBM layout; include/macroc_amd.h for the ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/macroc_amd.h"
+
+namespace mcx {
+
+constexpr int NGP = 8, NPE = 8, NVOI = 6;
+constexpr int NSLOT = 243;   // 27 neighbour blocks x 3x3
+constexpr int NPAIR = 122;   // slots stored as double2 pairs (slot 243 = zero pad)
+constexpr int GROUP = 64;    // nodes per AoSoA group (= one wavefront)
+constexpr int NKE = 576;     // 24x24 element matrix
+
+void set_error(const std::string& s);
+
+// Geometry of one rank's subdomain, passed by value to every kernel.
+struct Geo {
+  int NX, NY, NZ;          // global node counts
+  int xs, ys, zs;          // first owned node (global)
+  int nx, ny, nz;          // owned node counts
+  int PX, PY, PZ;          // padded box = owned + 1 ghost layer each side
+  int nown;                // nx*ny*nz
+  int ex0, ey0, ez0;       // first element evaluated on this device (global)
+  int nex, ney, nez;       // extended element counts (owned + upper ghost layer)
+  int64_t nelem;           // nex*ney*nez
+  int bc_type;
+  double lx, lz, dx, dz, rad, wg;
+};
+
+// device-side state of the CG loop (PETSc KSPSolve_CG scalars)
+struct CgState {
+  double beta, betaold, dpi, dpiold, alpha, dp, ttol, rnorm0, bcoef;
+  double rtol, abstol, dtol;
+  int i, its, reason, maxits, hist_on, pad;
+};
+
+struct Material {
+  int kind;
+  double E, nu;
+  double C[36];            // isotropic elastic tangent (Voigt, engineering shear)
+};
+
+struct HaloPlan {
+  std::vector<int> nbr_rank;          // neighbour ranks (<= 26)
+  std::vector<int64_t> send_off, send_cnt, recv_off, recv_cnt;  // in nodes
+  int* d_send_idx = nullptr;          // padded node index of each sent node
+  int* d_recv_idx = nullptr;          // padded node index of each received node
+  double* d_sendbuf = nullptr;
+  double* d_recvbuf = nullptr;
+  int64_t nsend = 0, nrecv = 0;
+};
+
+struct Ctx {
+  mcx_opts o;
+  int rank = 0, nranks = 1, device = 0;
+  int m = 1, n = 1, p = 1, pi = 0, pj = 0, pk = 0;
+  std::vector<int64_t> wx, wy, wz, sx, sy, sz;  // ownership widths / starts per rank column
+  std::vector<int64_t> rank_node_off;           // nranks + 1
+  Geo g{};
+  double dy = 0;
+  Material mat{};
+  hipStream_t stream = nullptr;
+  void* comm = nullptr;                         // ncclComm_t when nranks > 1
+  HaloPlan halo;
+
+  // device arrays
+  double* u_pad = nullptr;   // displacement, padded ghosted box [PX*PY*PZ][3]
+  double* p_pad = nullptr;   // CG search direction, padded
+  double* b = nullptr;       // residual (owned, PETSc-local order)
+  double* du = nullptr;      // CG solution x
+  double* r = nullptr;
+  double* z = nullptr;
+  double* w = nullptr;
+  double* dinv = nullptr;    // Jacobi inverse diagonal
+  double* V = nullptr;       // stencil-block matrix, AoSoA [ngroups][NPAIR][64] double2
+  double* eps = nullptr;     // [6][8][nelem]
+  double* sig = nullptr;     // [6][8][nelem]
+  double* ctan = nullptr;    // [36][8][nelem]
+  double* Ke = nullptr;      // [576][nelem] element matrices (assembly scratch)
+  double* be = nullptr;      // [24][nelem] element residuals
+  double* partials = nullptr;
+  double* red = nullptr;     // reduction results (device)
+  double* red_loc = nullptr; // local sums before all-reduce
+  CgState* cg = nullptr;
+  double* hist = nullptr;
+  double* tmp = nullptr;     // owned-vector scratch for host copies
+  CgState* h_cg = nullptr;   // pinned mirror
+  int64_t ngroups = 0;
+  int64_t device_bytes = 0;
+  int64_t nnz_local = 0, nnz_global = 0;
+
+  // timing
+  bool timing = false;
+  mcx_timing t{};
+  std::vector<hipEvent_t> ev_pool;
+  hipEvent_t ev_a = nullptr, ev_b = nullptr;
+  hipEvent_t ev_chunk[2] = {nullptr, nullptr};
+  int last_its = 0;
+  std::vector<double> last_hist;
+};
+
+// ---- decomposition (dmda.cpp)
+int dmda_decide(int64_t M, int64_t N, int64_t P, int size, int* m, int* n, int* p);
+int setup_decomposition(Ctx& c);
+int64_t petsc_node(const Ctx& c, int64_t i, int64_t j, int64_t k);
+int build_halo_plan(Ctx& c);
+void plan_halo(Ctx& c, std::vector<int>& sidx, std::vector<int>& ridx);
+int64_t pad_to_natural(const Ctx& c, int p);
+int64_t count_nnz_rows(const Ctx& c, int64_t xs, int64_t ys, int64_t zs, int64_t nx, int64_t ny, int64_t nz);
+void compute_B_table(double B[8][6][24]);
+
+// ---- communication (comm.cpp)
+int comm_init(Ctx& c, const void* id);
+void comm_destroy(Ctx& c);
+int halo_exchange(Ctx& c, double* xpad);
+int allreduce_sum(Ctx& c, const double* in, double* out, int count);
+
+// ---- kernel launchers (kernels.hip)
+int upload_constants(Ctx& c);
+void launch_apply_bc_u(Ctx& c, double U);
+void launch_strains(Ctx& c);
+void launch_homogenize(Ctx& c);
+void launch_residual(Ctx& c);          // b + partial sums of b.b
+void launch_element_ke(Ctx& c);
+void launch_gather_matrix(Ctx& c);
+void launch_jacobi(Ctx& c);
+void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated);
+void launch_update_u(Ctx& c);
+void launch_reduce(Ctx& c, int nvals, int nparts, double* out);
+void launch_cg_init(Ctx& c);
+int cg_iteration(Ctx& c, hipEvent_t spmv_start, hipEvent_t spmv_stop);
+int cg_finish_init(Ctx& c);
+void launch_pack(Ctx& c, const double* xpad);
+void launch_unpack(Ctx& c, double* xpad);
+void launch_copy_owned_to_pad(Ctx& c, const double* owned, double* pad);
+void launch_copy_pad_to_owned(Ctx& c, const double* pad, double* owned);
+int64_t spmv_grid_blocks(const Ctx& c);
+int64_t node_blocks(const Ctx& c);
+int dirichlet_mask_host(const Geo& g, int gi, int gj, int gk);
+
+}  // namespace mcx
+
+#define MCX_HIP(call)                                                                  \
+  do {                                                                                 \
+    hipError_t e_ = (call);                                                            \
+    if (e_ != hipSuccess) {                                                            \
+      mcx::set_error(std::string(#call) + ": " + hipGetErrorString(e_) + " @" +        \
+                     __FILE__ + ":" + std::to_string(__LINE__));                       \
+      return 10;                                                                       \
+    }                                                                                  \
+  } while (0)

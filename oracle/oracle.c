@@ -965,3 +965,41 @@ int orc_run(orc_problem* P, const char* log_path, double* t_newton_solve_s) {
   if (t_newton_solve_s) *t_newton_solve_s = t_first;
   return 0;
 }
+
+/* DMDA natural -> PETSc node numbering for any M,N,P >= 1 (used to pin the known answer of
+   tests/test_dm_1.c:5-19, a 2-D 5x2 DMDA on 2 ranks = M=5,N=2,P=1) */
+int orc_petsc_numbering(int64_t M, int64_t N, int64_t P, int size, int m, int n, int p, int64_t* out) {
+  if (orc_dmda_decide(M, N, P, size, &m, &n, &p)) return 1;
+  int64_t dims[3] = {M, N, P};
+  int procs[3] = {m, n, p};
+  int64_t *w[3], *s[3];
+  for (int d = 0; d < 3; d++) {
+    w[d] = malloc(procs[d] * sizeof(int64_t));
+    s[d] = malloc(procs[d] * sizeof(int64_t));
+    int64_t acc = 0;
+    for (int q = 0; q < procs[d]; q++) {
+      w[d][q] = dims[d] / procs[d] + ((dims[d] % procs[d]) > q);
+      s[d][q] = acc;
+      acc += w[d][q];
+    }
+  }
+  int64_t* off = malloc((size + 1) * sizeof(int64_t));
+  off[0] = 0;
+  for (int r = 0; r < size; r++) {
+    int a = r % m, b = (r % (m * n)) / m, c = r / (m * n);
+    off[r + 1] = off[r] + w[0][a] * w[1][b] * w[2][c];
+  }
+  for (int64_t k = 0; k < P; k++)
+    for (int64_t j = 0; j < N; j++)
+      for (int64_t i = 0; i < M; i++) {
+        int a = 0, b = 0, c = 0;
+        while (a + 1 < m && s[0][a + 1] <= i) a++;
+        while (b + 1 < n && s[1][b + 1] <= j) b++;
+        while (c + 1 < p && s[2][c + 1] <= k) c++;
+        int r = a + b * m + c * m * n;
+        out[i + j * M + k * M * N] = off[r] + (i - s[0][a]) + (j - s[1][b]) * w[0][a] + (k - s[2][c]) * w[0][a] * w[1][b];
+      }
+  for (int d = 0; d < 3; d++) { free(w[d]); free(s[d]); }
+  free(off);
+  return 0;
+}

@@ -101,6 +101,7 @@ int64_t orc_rank_dirichlet(const orc_problem* P, int r, int64_t* ix, int64_t cap
 /* sorted unique union of all ranks' non-negative Dirichlet DOFs; returns count */
 int64_t orc_dirichlet_set(const orc_problem* P, int64_t* out, int64_t cap);
 void orc_csr_pattern(const orc_problem* P, int64_t* rowptr, int32_t* colidx);
+int orc_petsc_numbering(int64_t M, int64_t N, int64_t P, int size, int m, int n, int p, int64_t* out);
 
 /* element kinematics */
 void orc_calc_B(int gp, double B[6][24]);

@@ -80,6 +80,8 @@ def lib():
         L.orc_dmda_decide.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int,
                                       C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.orc_run.argtypes = [P, C.c_char_p, d]
+        L.orc_petsc_numbering.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int,
+                                          C.POINTER(C.c_int64)]
         _LIB = L
     return _LIB
 
@@ -100,6 +102,15 @@ def dmda_decide(M, N, P, size, m=0, n=0, p=0):
     if rc:
         raise ValueError(f"no DMDA partition (code {rc})")
     return mm.value, nn.value, pp.value
+
+
+def petsc_numbering(M, N, P, size, m=0, n=0, p=0):
+    """natural node index -> PETSc global node index (DMDA, any dims)."""
+    out = np.zeros(M * N * P, dtype=np.int64)
+    rc = lib().orc_petsc_numbering(M, N, P, size, m, n, p, out.ctypes.data_as(C.POINTER(C.c_int64)))
+    if rc:
+        raise ValueError("no partition")
+    return out
 
 
 class Problem:

@@ -1,0 +1,178 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle and the golden fixtures.
+
+Bars: integer artefacts bit-exact; on one rank the element kinematics,
+strains, stresses, residual, assembled matrix and SpMV are bit-exact too (same operation
+order, no FMA contraction); the CG solution differs only through the reduction order of the
+dot products: iteration count within +-1 and |du - du_oracle| / |du| <= 1e-10 at
+-ksp_rtol 1e-12 (the north-star tolerance), <= 50 * rtol at looser rtol.
+Full-size grids are checked through size-independent properties (true residual, symmetry,
+linearity, determinism).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import macroc_amd as M
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+SINGLE = ["g442_r1", "g522_r1", "g444_r1", "g888_r1", "g16_r1"]
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+
+
+def argv_for(NX, NY, NZ, rtol, extra=()):
+    return ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-ksp_rtol", repr(rtol), "-ksp_monitor", *extra]
+
+
+def du_tol(rtol):
+    return 1e-10 if rtol <= 1e-12 else 50 * rtol
+
+
+@pytest.mark.parametrize("name", SINGLE)
+def test_newton_step_single_rank(name):
+    fx = load(name)
+    NX, NY, NZ = (int(v) for v in fx["grid"])
+    rtol = float(fx["rtol"])
+    P = O.Problem(NX, NY, NZ, rtol=rtol)
+    with M.Macroc(argv_for(NX, NY, NZ, rtol)) as m:
+        petsc, nat = m.owned_dofs()
+        assert np.array_equal(petsc, fx["dof_map"][nat])
+        assert np.array_equal(m.dump_dirichlet(), fx["dirichlet"])
+        # time step 0 then 1 (src/main.c:49-54)
+        for ts in (0, 1):
+            U = m.get_displacement(ts)
+            assert U == P.get_displacement(ts)
+            m.apply_bc_on_u(U)
+            P.apply_bc_u(U)
+        assert np.array_equal(m.u(), P.u())
+        m.set_strains()
+        P.set_strains()
+        assert np.array_equal(m.strain(), P.strain())
+        m.homogenize()
+        P.homogenize()
+        assert np.array_equal(m.stress(), P.stress())
+        res = m.assembly_res()
+        P.assembly_res()
+        assert np.array_equal(m.b(), P.b())
+        assert np.array_equal(m.b(), fx["b"])
+        assert abs(res - float(fx["res"])) <= 1e-13 * max(float(fx["res"]), 1.0)
+        m.assembly_jac()
+        P.assembly_jac()
+        rp, ci, v = m.dump_csr()
+        orp, oci = P.csr()
+        assert np.array_equal(rp, orp) and np.array_equal(ci, oci.astype(np.int64))
+        assert np.array_equal(v, P.A_values())
+        x = np.random.default_rng(42).uniform(-1, 1, m.n)
+        assert np.array_equal(m.spmv(x), P.spmv(x))
+        its, rn, reason = m.solve_Ax()
+        P.solve()
+        assert reason == int(fx["reason"]) or (its == 0 and int(fx["its"]) == 0)
+        assert abs(its - int(fx["its"])) <= 1
+        du = m.du()
+        ref = fx["du"]
+        if np.linalg.norm(ref) > 0:
+            assert np.linalg.norm(du - ref) <= du_tol(rtol) * np.linalg.norm(ref)
+            h = m.ksp_history()
+            k = min(len(h), len(fx["history"]), 20)
+            np.testing.assert_allclose(h[:k], fx["history"][:k], rtol=1e-9)
+        else:
+            assert np.linalg.norm(du) == 0
+        m.update_u()
+        assert np.linalg.norm(m.u() - fx["u"]) <= du_tol(rtol) * np.linalg.norm(fx["u"]) + 1e-300
+
+
+def test_time_loop_matches_oracle_log():
+    """mcx_time_step over -ts 2 on the BASELINE config-1 grid (4x4x2) against orc_run."""
+    P = O.Problem(4, 4, 2, ts=2)
+    with M.Macroc(["-da_grid_x", 4, "-da_grid_y", 4, "-da_grid_z", 2, "-ts", 2]) as m:
+        out0 = m.time_step(0)
+        assert out0["newton_its"] == 0 and out0["res"][0] == 0.0
+        out1 = m.time_step(1)
+    P.apply_bc_u(P.get_displacement(0))
+    ref = P.newton_step1()
+    assert out1["newton_its"] == 1
+    assert out1["res"][0] == ref["res"]
+    assert abs(out1["ksp_its"][0] - ref["its"]) <= 1
+    # second Newton residual is below newton_rel_tol * |RES_0| (src/main.c:73)
+    assert out1["res"][1] < 1e-4 * out1["res"][0]
+
+
+def test_bending_bc_parity():
+    NX, NY, NZ = 6, 4, 5
+    P = O.Problem(NX, NY, NZ, bc_type=0, rtol=1e-12)
+    with M.Macroc(argv_for(NX, NY, NZ, 1e-12, ["-bc_type", 0])) as m:
+        assert np.array_equal(m.dump_dirichlet(), P.dirichlet_set())
+        P.apply_bc_u(P.get_displacement(1))
+        m.apply_bc_on_u(m.get_displacement(1))
+        assert np.array_equal(m.u(), P.u())
+        for f in ("set_strains", "homogenize"):
+            getattr(m, f)()
+        P.set_strains()
+        P.homogenize()
+        m.assembly_res()
+        P.assembly_res()
+        assert np.array_equal(m.b(), P.b())
+        m.assembly_jac()
+        P.assembly_jac()
+        assert np.array_equal(m.dump_csr()[2], P.A_values())
+        m.solve_Ax()
+        P.solve()
+        assert np.linalg.norm(m.du() - P.du()) <= 1e-10 * np.linalg.norm(P.du())
+
+
+def test_ksp_edge_cases():
+    """maxits hit -> DIVERGED_ITS with its == maxits; zero rhs -> converged at its 0."""
+    with M.Macroc(argv_for(8, 8, 8, 1e-12, ["-ksp_max_it", 5])) as m:
+        m.apply_bc_on_u(m.get_displacement(1))
+        m.set_strains()
+        m.homogenize()
+        m.assembly_res()
+        m.assembly_jac()
+        its, rn, reason = m.solve_Ax()
+        assert (its, reason) == (5, -3)
+    with M.Macroc(argv_for(5, 2, 2, 1e-5)) as m:
+        m.apply_bc_on_u(m.get_displacement(1))
+        m.set_strains()
+        m.homogenize()
+        assert m.assembly_res() == 0.0
+        m.assembly_jac()
+        its, rn, reason = m.solve_Ax()
+        assert its == 0 and reason in (2, 3)
+
+
+def _solve_big(N, rtol):
+    m = M.Macroc(argv_for(N, N, N, rtol))
+    m.apply_bc_on_u(m.get_displacement(1))
+    m.set_strains()
+    m.homogenize()
+    res = m.assembly_res()
+    m.assembly_jac()
+    its, rn, reason = m.solve_Ax()
+    return m, res, its, reason
+
+
+def test_64cubed_properties():
+    """BASELINE config 2 (64^3, rtol 1e-8): convergence, true residual, symmetry, linearity,
+    determinism of assembly + SpMV."""
+    m, res, its, reason = _solve_big(64, 1e-8)
+    try:
+        assert reason == 2 and 650 <= its <= 800  # scipy restatement: 720
+        b, du = m.b(), m.du()
+        r = m.spmv(du) - b
+        assert np.linalg.norm(r) <= 1e-4 * np.linalg.norm(b)
+        rng = np.random.default_rng(7)
+        x, y = rng.uniform(-1, 1, m.n), rng.uniform(-1, 1, m.n)
+        Ax, Ay = m.spmv(x), m.spmv(y)
+        assert abs(y @ Ax - x @ Ay) <= 1e-12 * np.linalg.norm(Ax) * np.linalg.norm(y)
+        np.testing.assert_allclose(m.spmv(2.0 * x + y), 2.0 * Ax + Ay, rtol=1e-12, atol=1e-6)
+        v1 = m.dump_csr()[2]
+        m.assembly_jac()
+        assert np.array_equal(m.dump_csr()[2], v1)
+        assert np.array_equal(m.spmv(x), Ax)
+    finally:
+        m.finish()

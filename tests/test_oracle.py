@@ -1,0 +1,85 @@
+"""The CPU oracle (test infrastructure) pinned against the reference's known answer and the
+committed golden fixtures (tests/golden/, generated + cross-checked by make_golden.py)."""
+import glob
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+CASES = sorted(os.path.basename(p)[:-4] for p in glob.glob(os.path.join(GOLDEN, "g*.npz")))
+
+
+def load(name):
+    return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def test_known_answer_test_dm_1():
+    # tests/test_dm_1.c:5-19: 5x2 DMDA on 2 ranks, PETSc global ordering
+    order = O.petsc_numbering(5, 2, 1, 2).reshape(2, 5)
+    assert order.tolist() == [[0, 1, 2, 6, 7], [3, 4, 5, 8, 9]]
+    assert O.dmda_decide(5, 2, 1, 2) == (2, 1, 1)
+
+
+def test_decide_cube_8():
+    assert O.dmda_decide(512, 512, 512, 8) == (2, 2, 2)
+    assert O.dmda_decide(256, 256, 256, 1) == (1, 1, 1)
+    assert O.dmda_decide(5, 3, 4, 8, 0, 0, 0)[0] * O.dmda_decide(5, 3, 4, 8)[1] * O.dmda_decide(5, 3, 4, 8)[2] == 8
+
+
+def test_calc_B_fixture():
+    Bo = np.stack([O.calc_B(gp) for gp in range(8)])
+    assert np.array_equal(Bo, load("calc_B")["B"])
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_vs_golden(name):
+    fx = load(name)
+    NX, NY, NZ = (int(v) for v in fx["grid"])
+    m, n, p = (int(v) for v in fx["decomp"])
+    nr = int(fx["nranks"])
+    P = O.Problem(NX, NY, NZ, nranks=nr, m=m, n=n, p=p, rtol=float(fx["rtol"]))
+    # integer artefacts: bit-exact
+    assert P.decomp() == (m, n, p)
+    assert np.array_equal(P.dof_map(), fx["dof_map"])
+    assert np.array_equal(P.dirichlet_set(), fx["dirichlet"])
+    conn = np.concatenate([P.elements(r) for r in range(nr)])
+    assert np.array_equal(conn, fx["conn"])
+    assert np.array_equal(np.array([P.corners(r) for r in range(nr)]), fx["corners"])
+    rp, ci = P.csr()
+    assert sha(rp) == str(fx["csr_rowptr_sha"]) and sha(ci) == str(fx["csr_colidx_sha"])
+    # floating point: the oracle is deterministic, so bit-exact against its own fixture
+    out = P.newton_step1()
+    assert out["its"] == int(fx["its"]) and out["reason"] == int(fx["reason"])
+    assert np.array_equal(P.b(), fx["b"])
+    assert np.array_equal(P.du(), fx["du"])
+    assert np.array_equal(out["history"], fx["history"])
+    if "A" in fx:
+        assert np.array_equal(P.A_values(), fx["A"])
+    # and the direct solve agrees where the solve is tight
+    if float(fx["rtol"]) <= 1e-12:
+        d = fx["du_direct"]
+        assert np.linalg.norm(P.du() - d) <= 1e-9 * np.linalg.norm(d)
+    P.close()
+
+
+def test_ctest_grids_never_solve():
+    # on 5x2x2 no node is inside the load circle -> zero residual, no KSPSolve
+    fx = load("g522_r1")
+    assert float(fx["res"]) == 0.0 and int(fx["its"]) == 0
+
+
+def test_oracle_log_matches_reference_format(tmp_path):
+    P = O.Problem(4, 4, 2, ts=2)
+    log = tmp_path / "log.txt"
+    P.run(str(log))
+    txt = log.read_text()
+    assert "Time Step = 1" in txt and "|RES| = 1.029218e+06" in txt
+    assert "KSP : |Ax - b|/|Ax| = " in txt and "Its = 39" in txt
