@@ -88,6 +88,7 @@ def main():
     ap.add_argument("--rtol", type=float, default=1e-8)
     ap.add_argument("--cpu-sample", type=int, default=40, help="oracle sample grid (0 = skip)")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--same-device", action="store_true", help="testing only: every rank on device 0")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -99,7 +100,8 @@ def main():
     G = args.grid
     NX, NY, NZ = G * px, G * py, G * pz
     argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
-            "-da_processors_z", pz, "-ts", 2, "-ksp_rtol", repr(args.rtol), "-device", local]
+            "-da_processors_z", pz, "-ts", 2, "-ksp_rtol", repr(args.rtol),
+            "-device", 0 if args.same_device else local]
     comm_id = None
     if world > 1:
         obj = [M.comm_unique_id() if rank == 0 else None]

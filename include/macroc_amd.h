@@ -125,6 +125,12 @@ int mcx_plan_halo(const mcx_opts* o, int rank, int nranks, int* nnbr, int* nbr_r
                   int64_t* recv_cnt, int64_t* send_nat, int64_t* recv_nat, int64_t* nsend, int64_t* nrecv);
 
 int mcx_init(const mcx_opts* o, int rank, int nranks, const void* comm_id, void** ctx);
+/* In-process transport: `nranks` contexts on one device, each driven by its own host thread,
+   exchanging halos / partial sums by device copies (multi-rank path without RCCL; every
+   collective entry point must then be called by all members). */
+int mcx_local_group_create(int nranks, int device, void** group);
+int mcx_local_group_destroy(void* group);
+int mcx_init_local(const mcx_opts* o, int rank, void* group, void** ctx);
 int mcx_finalize(void* ctx);
 int mcx_get_info(void* ctx, mcx_info* info);
 

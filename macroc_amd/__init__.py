@@ -31,6 +31,7 @@ KSP_REASONS = {2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL", -3: "DIVERGED_ITS", -4:
 # symbols declared in include/macroc_amd.h (checked by tests/test_abi.py)
 EXPORTS = [
     "mcx_last_error", "mcx_version", "mcx_default_opts", "mcx_parse_args", "mcx_comm_unique_id", "mcx_plan", "mcx_plan_halo", "mcx_init",
+    "mcx_local_group_create", "mcx_local_group_destroy", "mcx_init_local",
     "mcx_finalize", "mcx_get_info", "mcx_material_set", "mcx_get_displacement", "mcx_zero_u", "mcx_apply_bc_u",
     "mcx_set_strains", "mcx_homogenize", "mcx_assembly_res", "mcx_assembly_jac", "mcx_solve", "mcx_update_u",
     "mcx_time_step", "mcx_get_u", "mcx_set_u", "mcx_get_b", "mcx_get_du", "mcx_get_strain", "mcx_get_stress",
@@ -106,6 +107,9 @@ def lib():
     L.mcx_plan.argtypes = [C.POINTER(Opts), C.c_int, C.c_int, C.POINTER(Info)]
     L.mcx_plan_halo.argtypes = [C.POINTER(Opts), C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_int),
                                 i64, i64, i64, i64, i64, i64]
+    L.mcx_local_group_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
+    L.mcx_local_group_destroy.argtypes = [vp]
+    L.mcx_init_local.argtypes = [C.POINTER(Opts), C.c_int, vp, C.POINTER(C.c_void_p)]
     L.mcx_finalize.argtypes = [vp]
     L.mcx_get_info.argtypes = [vp, C.POINTER(Info)]
     L.mcx_material_set.argtypes = [vp, C.c_int, C.c_double, C.c_double, C.c_double, C.c_double, C.c_int]
@@ -187,19 +191,36 @@ def plan_halo(argv, rank=0, nranks=1):
     return out
 
 
+class LocalGroup:
+    """In-process transport for `nranks` contexts on one device (one host thread per rank)."""
+
+    def __init__(self, nranks, device=0):
+        self.nranks = nranks
+        self._g = C.c_void_p()
+        _check(lib().mcx_local_group_create(nranks, device, C.byref(self._g)), "mcx_local_group_create")
+
+    def destroy(self):
+        if self._g:
+            _check(lib().mcx_local_group_destroy(self._g), "mcx_local_group_destroy")
+            self._g = C.c_void_p()
+
+
 class Macroc:
     """One rank (= one GPU subdomain) of the MacroC hot path."""
 
-    def __init__(self, argv=(), rank=0, nranks=1, comm_id=None, opts=None):
+    def __init__(self, argv=(), rank=0, nranks=1, comm_id=None, opts=None, group=None):
         L = lib()
         self.opts = opts if opts is not None else parse_args(argv)
         self._ctx = C.c_void_p()
         cid = None
-        if nranks > 1:
+        if nranks > 1 and group is None:
             if comm_id is None or len(comm_id) != COMM_ID_BYTES:
                 raise MacrocError("nranks > 1 needs the 128-byte id from comm_unique_id() on every rank")
             cid = C.create_string_buffer(comm_id, COMM_ID_BYTES)
-        _check(L.mcx_init(C.byref(self.opts), rank, nranks, cid, C.byref(self._ctx)), "mcx_init")
+        if group is not None:
+            _check(L.mcx_init_local(C.byref(self.opts), rank, group._g, C.byref(self._ctx)), "mcx_init_local")
+        else:
+            _check(L.mcx_init(C.byref(self.opts), rank, nranks, cid, C.byref(self._ctx)), "mcx_init")
         inf = Info()
         _check(L.mcx_get_info(self._ctx, C.byref(inf)), "mcx_get_info")
         self.info = inf.as_dict()

@@ -70,8 +70,9 @@ static int free_ctx(Ctx* c) {
   return 0;
 }
 
-static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void* comm_id) {
+static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void* comm_id, LocalGroup* lg) {
   c.o = *o;
+  c.lg = lg;
   c.rank = rank;
   c.nranks = nranks;
   int ndev = 0;
@@ -80,7 +81,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
     set_error("no HIP device visible");
     return 11;
   }
-  c.device = o->device >= 0 ? o->device : rank % ndev;
+  c.device = lg ? lg->device : (o->device >= 0 ? o->device : rank % ndev);
   MCX_HIP(hipSetDevice(c.device));
   int rc = setup_decomposition(c);
   if (rc) return rc;
@@ -112,6 +113,11 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   c.nnz_local = count_nnz_rows(c, g.xs, g.ys, g.zs, g.nx, g.ny, g.nz);
   c.nnz_global = count_nnz_rows(c, 0, 0, 0, o->NX, o->NY, o->NZ);
   MCX_HIP(hipStreamSynchronize(c.stream));
+  if (lg) {
+    lg->members[rank] = &c;
+    MCX_HIP(hipMemcpy(lg->d_red_ptrs + rank, &c.red_loc, sizeof(double*), hipMemcpyHostToDevice));
+    group_barrier(lg);
+  }
   return 0;
 }
 
@@ -298,7 +304,7 @@ int mcx_init(const mcx_opts* o, int rank, int nranks, const void* comm_id, void*
     return 1;
   }
   Ctx* c = new Ctx();
-  int rc = init_ctx(*c, o, rank, nranks, comm_id);
+  int rc = init_ctx(*c, o, rank, nranks, comm_id, nullptr);
   if (rc) {
     std::string e = g_err;
     free_ctx(c);
@@ -310,7 +316,35 @@ int mcx_init(const mcx_opts* o, int rank, int nranks, const void* comm_id, void*
   return 0;
 }
 
-int mcx_finalize(void* ctx) { return free_ctx(reinterpret_cast<Ctx*>(ctx)); }
+int mcx_init_local(const mcx_opts* o, int rank, void* group, void** ctx) {
+  auto* lg = static_cast<LocalGroup*>(group);
+  if (!o || !ctx || !lg || rank < 0 || rank >= lg->nranks) {
+    set_error("mcx_init_local: bad arguments");
+    return 1;
+  }
+  Ctx* c = new Ctx();
+  int rc = init_ctx(*c, o, rank, lg->nranks, nullptr, lg);
+  if (rc) {
+    std::string e = g_err;
+    free_ctx(c);
+    g_err = e;
+    *ctx = nullptr;
+    return rc;
+  }
+  *ctx = c;
+  return 0;
+}
+
+int mcx_finalize(void* ctx) {
+  Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  if (c && c->lg) {
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    group_barrier(c->lg);  // no member still copies from this context's buffers
+    c->lg->members[c->rank] = nullptr;
+  }
+  return free_ctx(c);
+}
 
 static void fill_info(const Ctx& c, mcx_info* in) {
   const Geo& g = c.g;

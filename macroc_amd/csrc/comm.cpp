@@ -7,7 +7,9 @@
 // loop never returns to the host between iterations.
 #include <rccl/rccl.h>
 
+#include <condition_variable>
 #include <cstring>
+#include <mutex>
 
 #include "mcx_internal.h"
 
@@ -23,7 +25,7 @@ namespace mcx {
   } while (0)
 
 int comm_init(Ctx& c, const void* id) {
-  if (c.nranks <= 1) return 0;
+  if (c.nranks <= 1 || c.lg) return 0;
   if (!id) {
     set_error("nranks > 1 needs a communicator id from mcx_comm_unique_id");
     return 21;
@@ -44,8 +46,49 @@ void comm_destroy(Ctx& c) {
   }
 }
 
+void group_barrier(LocalGroup* g) {
+  auto* m = static_cast<std::mutex*>(g->mtx);
+  auto* cv = static_cast<std::condition_variable*>(g->cv);
+  std::unique_lock<std::mutex> lk(*m);
+  int gen = g->generation;
+  if (++g->count == g->nranks) {
+    g->count = 0;
+    g->generation++;
+    cv->notify_all();
+  } else {
+    cv->wait(lk, [&] { return g->generation != gen; });
+  }
+}
+
+static int halo_exchange_local(Ctx& c, double* xpad) {
+  LocalGroup* g = c.lg;
+  HaloPlan& h = c.halo;
+  // neighbours finished reading my previous send buffer
+  for (int q : h.nbr_rank) MCX_HIP(hipStreamWaitEvent(c.stream, g->ev_halo_done[q], 0));
+  launch_pack(c, xpad);
+  MCX_HIP(hipEventRecord(g->ev_packed[c.rank], c.stream));
+  group_barrier(g);
+  for (size_t t = 0; t < h.nbr_rank.size(); t++) {
+    const Ctx& q = *g->members[h.nbr_rank[t]];
+    size_t idx = 0;
+    while (idx < q.halo.nbr_rank.size() && q.halo.nbr_rank[idx] != c.rank) idx++;
+    if (idx == q.halo.nbr_rank.size() || q.halo.send_cnt[idx] != h.recv_cnt[t]) {
+      set_error("local halo: inconsistent neighbour plans");
+      return 22;
+    }
+    MCX_HIP(hipStreamWaitEvent(c.stream, g->ev_packed[h.nbr_rank[t]], 0));
+    MCX_HIP(hipMemcpyAsync(h.d_recvbuf + 3 * h.recv_off[t], q.halo.d_sendbuf + 3 * q.halo.send_off[idx],
+                           sizeof(double) * 3 * h.recv_cnt[t], hipMemcpyDeviceToDevice, c.stream));
+  }
+  MCX_HIP(hipEventRecord(g->ev_halo_done[c.rank], c.stream));
+  group_barrier(g);
+  launch_unpack(c, xpad);
+  return 0;
+}
+
 int halo_exchange(Ctx& c, double* xpad) {
   if (c.nranks <= 1 || c.halo.nbr_rank.empty()) return 0;
+  if (c.lg) return halo_exchange_local(c, xpad);
   HaloPlan& h = c.halo;
   launch_pack(c, xpad);
   MCX_NCCL(ncclGroupStart());
@@ -65,11 +108,64 @@ int allreduce_sum(Ctx& c, const double* in, double* out, int count) {
     if (in != out) MCX_HIP(hipMemcpyAsync(out, in, sizeof(double) * count, hipMemcpyDeviceToDevice, c.stream));
     return 0;
   }
+  if (c.lg) {
+    LocalGroup* g = c.lg;
+    MCX_HIP(hipEventRecord(g->ev_red[c.rank], c.stream));
+    group_barrier(g);
+    for (int q = 0; q < g->nranks; q++) MCX_HIP(hipStreamWaitEvent(c.stream, g->ev_red[q], 0));
+    launch_group_sum(c, (const double* const*)g->d_red_ptrs, g->nranks, count, out);
+    MCX_HIP(hipEventRecord(g->ev_sum[c.rank], c.stream));
+    group_barrier(g);
+    return 0;
+  }
   MCX_NCCL(ncclAllReduce(in, out, count, ncclDouble, ncclSum, (ncclComm_t)c.comm, c.stream));
   return 0;
 }
 
+// before overwriting red_loc: every member has summed the previous partials
+int allreduce_prepare(Ctx& c) {
+  if (!c.lg) return 0;
+  for (int q = 0; q < c.lg->nranks; q++) MCX_HIP(hipStreamWaitEvent(c.stream, c.lg->ev_sum[q], 0));
+  return 0;
+}
+
 }  // namespace mcx
+
+extern "C" int mcx_local_group_create(int nranks, int device, void** group) {
+  using namespace mcx;
+  if (nranks < 1 || !group) {
+    set_error("mcx_local_group_create: bad arguments");
+    return 1;
+  }
+  MCX_HIP(hipSetDevice(device));
+  auto* g = new LocalGroup();
+  g->nranks = nranks;
+  g->device = device;
+  g->members.assign(nranks, nullptr);
+  g->mtx = new std::mutex();
+  g->cv = new std::condition_variable();
+  for (auto* v : {&g->ev_packed, &g->ev_halo_done, &g->ev_red, &g->ev_sum}) {
+    v->resize(nranks);
+    for (auto& e : *v) MCX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  MCX_HIP(hipMalloc(&g->d_red_ptrs, sizeof(double*) * nranks));
+  *group = g;
+  return 0;
+}
+
+extern "C" int mcx_local_group_destroy(void* group) {
+  using namespace mcx;
+  auto* g = static_cast<LocalGroup*>(group);
+  if (!g) return 0;
+  (void)hipSetDevice(g->device);
+  for (auto* v : {&g->ev_packed, &g->ev_halo_done, &g->ev_red, &g->ev_sum})
+    for (auto& e : *v) (void)hipEventDestroy(e);
+  (void)hipFree(g->d_red_ptrs);
+  delete static_cast<std::mutex*>(g->mtx);
+  delete static_cast<std::condition_variable*>(g->cv);
+  delete g;
+  return 0;
+}
 
 extern "C" int mcx_comm_unique_id(void* id) {
   ncclUniqueId uid;

@@ -618,6 +618,15 @@ __global__ void k_cg_logic(const double* __restrict__ red, int mode, CgState* cg
   else if (mode == RED_NORM) out[0] = sqrt(red[0]);
 }
 
+// in-process all-reduce: out[v] = sum over ranks (rank order) of ptrs[r][v]
+__global__ void k_group_sum(const double* const* __restrict__ ptrs, int nranks, int count, double* __restrict__ out) {
+  int v = threadIdx.x;
+  if (v >= count) return;
+  double s = 0.;
+  for (int r = 0; r < nranks; r++) s += ptrs[r][v];
+  out[v] = s;
+}
+
 // ---------------------------------------------------------------------------- misc vectors
 __global__ void k_update_u(Geo g, double* __restrict__ u, const double* __restrict__ du) {
   int n = blockIdx.x * TPB + threadIdx.x;
@@ -749,12 +758,18 @@ void launch_unpack(Ctx& c, double* xpad) {
 
 // reduce partials into out (and, for RED_NORM, out[0] = sqrt); multi-rank: local sums are
 // all-reduced over RCCL first.
+void launch_group_sum(Ctx& c, const double* const* ptrs, int nranks, int count, double* out) {
+  hipLaunchKernelGGL(k_group_sum, dim3(1), dim3(64), 0, c.stream, ptrs, nranks, count, out);
+}
+
 static int reduce_and_logic(Ctx& c, int nvals, int nparts, int mode, bool gated) {
   if (c.nranks == 1) {
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, c.stream, c.partials, nparts, nvals, c.red, mode, c.cg, c.hist,
                        gated ? 1 : 0);
     return 0;
   }
+  int rc0 = allreduce_prepare(c);
+  if (rc0) return rc0;
   hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, c.stream, c.partials, nparts, nvals, c.red_loc, (int)RED_STORE,
                      c.cg, c.hist, gated ? 1 : 0);
   int rc = allreduce_sum(c, c.red_loc, c.red, nvals);

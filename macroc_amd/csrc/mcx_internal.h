@@ -57,6 +57,24 @@ struct HaloPlan {
   int64_t nsend = 0, nrecv = 0;
 };
 
+struct Ctx;
+
+// In-process transport: several contexts (one host thread each) exchanging halos and partial
+// sums by device copies + events.  Used to run the multi-rank path on one GPU (tests) and for
+// a single process driving several GPUs; the RCCL transport is the multi-process path.
+struct LocalGroup {
+  int nranks = 0;
+  std::vector<Ctx*> members;
+  std::vector<hipEvent_t> ev_packed, ev_halo_done, ev_red, ev_sum;
+  double** d_red_ptrs = nullptr;   // device array: red_loc of every member
+  int device = 0;
+  // host barrier
+  void* mtx = nullptr;
+  void* cv = nullptr;
+  int count = 0, generation = 0;
+};
+void group_barrier(LocalGroup* g);
+
 struct Ctx {
   mcx_opts o;
   int rank = 0, nranks = 1, device = 0;
@@ -67,7 +85,8 @@ struct Ctx {
   double dy = 0;
   Material mat{};
   hipStream_t stream = nullptr;
-  void* comm = nullptr;                         // ncclComm_t when nranks > 1
+  void* comm = nullptr;                         // ncclComm_t when nranks > 1 (RCCL transport)
+  LocalGroup* lg = nullptr;                     // in-process transport
   HaloPlan halo;
 
   // device arrays
@@ -121,6 +140,8 @@ int comm_init(Ctx& c, const void* id);
 void comm_destroy(Ctx& c);
 int halo_exchange(Ctx& c, double* xpad);
 int allreduce_sum(Ctx& c, const double* in, double* out, int count);
+int allreduce_prepare(Ctx& c);
+void launch_group_sum(Ctx& c, const double* const* ptrs, int nranks, int count, double* out);
 
 // ---- kernel launchers (kernels.hip)
 int upload_constants(Ctx& c);

@@ -1,0 +1,116 @@
+"""Multi-rank parity on one GPU: N contexts (one host thread each) over the in-process
+transport run the decomposed path — halo exchanges, owner-computes assembly on subdomains,
+all-reduced CG scalars — and must reproduce the single-rank answer.
+
+Owner-computes makes every row independent of the rank grid: strains, residual, assembled
+matrix and SpMV are bit-identical to the one-rank oracle in natural ordering; only the CG dot
+products change summation order (its +-1, du within the north-star tolerance).  The RCCL
+transport differs from this one only in the two calls that move the bytes.
+"""
+import os
+import threading
+
+import numpy as np
+import pytest
+
+import macroc_amd as M
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def run_group(argv, nranks, fn, timeout=300):
+    g = M.LocalGroup(nranks)
+    results, errors = [None] * nranks, []
+
+    def worker(r):
+        try:
+            m = M.Macroc(argv, rank=r, nranks=nranks, group=g)
+            try:
+                results[r] = fn(m)
+            finally:
+                m.finish()
+        except Exception as e:  # surfaced below
+            errors.append((r, e))
+
+    ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(nranks)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout)
+    assert not any(t.is_alive() for t in ts), f"group hung; errors={errors}"
+    assert not errors, errors
+    g.destroy()
+    return results
+
+
+def newton_step(x_global_nat):
+    def fn(m):
+        petsc, nat = m.owned_dofs()
+        m.apply_bc_on_u(m.get_displacement(0))
+        m.apply_bc_on_u(m.get_displacement(1))
+        m.set_strains()
+        m.homogenize()
+        res = m.assembly_res()
+        m.assembly_jac()
+        rp, ci, v = m.dump_csr()
+        y = m.spmv(x_global_nat[nat])
+        its, rn, reason = m.solve_Ax()
+        m.update_u()
+        return dict(petsc=petsc, nat=nat, b=m.b(), du=m.du(), u=m.u(), res=res, its=its, reason=reason,
+                    rp=rp, ci=ci, v=v, y=y, dir=m.dump_dirichlet(), info=m.info)
+    return fn
+
+
+@pytest.mark.parametrize("name", ["g1088_r2", "g888_r8", "g522_r3", "g534_r8"])
+def test_multirank_newton_step(name):
+    fx = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    NX, NY, NZ = (int(v) for v in fx["grid"])
+    nr = int(fx["nranks"])
+    px, py, pz = (int(v) for v in fx["decomp"])
+    rtol = float(fx["rtol"])
+    argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
+            "-da_processors_z", pz, "-ksp_rtol", repr(rtol)]
+    ref = O.Problem(NX, NY, NZ, rtol=rtol)  # one rank: natural order == PETSc order
+    x = np.random.default_rng(3).uniform(-1, 1, ref.ndofs)
+    out = run_group(argv, nr, newton_step(x))
+    ref.newton_step1()
+    A1 = {}
+    rp1, ci1 = ref.csr()
+    v1 = ref.A_values()
+    y1 = ref.spmv(x)
+    dm = fx["dof_map"]  # natural -> PETSc of the nr-rank decomposition
+    inv = np.empty_like(dm)
+    inv[dm] = np.arange(len(dm))
+    b = np.zeros(ref.ndofs)
+    du = np.zeros(ref.ndofs)
+    dset = []
+    for r, o in enumerate(out):
+        assert np.array_equal(o["petsc"], dm[o["nat"]])  # integer artefact: bit-exact
+        b[o["nat"]] = o["b"]
+        du[o["nat"]] = o["du"]
+        dset.append(o["dir"])
+        assert np.array_equal(o["y"], y1[o["nat"]])  # SpMV bit-exact
+        assert abs(o["its"] - int(fx["its"])) <= 1
+        assert o["res"] == out[0]["res"]
+        # matrix rows: global PETSc columns, values bit-exact vs the one-rank matrix
+        for q in range(len(o["nat"])):
+            row_nat = o["nat"][q]
+            cols_p = o["ci"][o["rp"][q]:o["rp"][q + 1]]
+            vals = o["v"][o["rp"][q]:o["rp"][q + 1]]
+            lo, hi = rp1[row_nat], rp1[row_nat + 1]
+            ref_cols = ci1[lo:hi]
+            ref_vals = v1[lo:hi]
+            order = np.argsort(inv[cols_p])
+            assert np.array_equal(inv[cols_p][order], ref_cols)
+            assert np.array_equal(vals[order], ref_vals)
+    assert np.array_equal(np.sort(np.concatenate(dset)), fx["dirichlet"])
+    assert np.array_equal(b, ref.b())  # residual bit-exact in natural order
+    assert abs(out[0]["res"] - ref.norm_b()) <= 1e-14 * max(ref.norm_b(), 1.0)
+    duref = ref.du()
+    if np.linalg.norm(duref) > 0:
+        tol = 1e-10 if rtol <= 1e-12 else 50 * rtol
+        assert np.linalg.norm(du - duref) <= tol * np.linalg.norm(duref)
+    else:
+        assert not du.any()
