@@ -53,6 +53,11 @@ enum {
   MCX_KSP_DIVERGED_INDEFINITE_MAT = -10
 };
 
+/* matrix storage: -dm_mat_type aij (default, the reference's MATAIJ, src/init.c:92) or
+   sbaij (PETSc MATSBAIJ semantics with -mat_ignore_lower_triangular: upper triangle kept,
+   lower triangle mirrored from it) */
+enum { MCX_MAT_AIJ = 0, MCX_MAT_SBAIJ = 1 };
+
 /* constitutive models behind the Gauss-point callback */
 enum { MCX_MAT_ELASTIC = 0 };
 
@@ -75,6 +80,7 @@ typedef struct {
   double micro_mat_2[4];       /* -micro_mat_2 */
   int device;                  /* HIP device of this rank (-1: rank % device count) */
   int ksp_monitor;             /* -ksp_monitor: keep the residual history */
+  int mat_type;                /* -dm_mat_type aij|sbaij  (MCX_MAT_AIJ) */
 } mcx_opts;
 
 typedef struct {

@@ -51,7 +51,7 @@ class Opts(C.Structure):
         ("ksp_rtol", C.c_double), ("ksp_abstol", C.c_double), ("ksp_dtol", C.c_double),
         ("ksp_max_it", C.c_int), ("micro_n", C.c_int), ("micro_type", C.c_int),
         ("micro_mat_1", C.c_double * 4), ("micro_mat_2", C.c_double * 4),
-        ("device", C.c_int), ("ksp_monitor", C.c_int),
+        ("device", C.c_int), ("ksp_monitor", C.c_int), ("mat_type", C.c_int),
     ]
 
 

@@ -53,7 +53,7 @@ static int free_ctx(Ctx* c) {
   if (!c) return 0;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->V, c->eps, c->sig, c->ctan,
+  void* ptrs[] = {c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->V, c->U, c->eps, c->sig, c->ctan,
                   c->Ke, c->be, c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf};
   for (void* p : ptrs)
@@ -97,7 +97,9 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   if ((rc = dalloc(c, &c.u_pad, npad)) || (rc = dalloc(c, &c.p_pad, npad)) || (rc = dalloc(c, &c.b, nown3)) ||
       (rc = dalloc(c, &c.du, nown3)) || (rc = dalloc(c, &c.r, nown3)) || (rc = dalloc(c, &c.z, nown3)) ||
       (rc = dalloc(c, &c.w, nown3)) || (rc = dalloc(c, &c.dinv, nown3)) || (rc = dalloc(c, &c.tmp, nown3)) ||
-      (rc = dalloc(c, &c.V, c.ngroups * NPAIR * 128)) || (rc = dalloc(c, &c.eps, 6 * 8 * E)) ||
+      (c.o.mat_type == MCX_MAT_SBAIJ ? (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))
+                                     : (rc = dalloc(c, &c.V, c.ngroups * NPAIR * 128))) ||
+      (rc = dalloc(c, &c.eps, 6 * 8 * E)) ||
       (rc = dalloc(c, &c.sig, 6 * 8 * E)) || (rc = dalloc(c, &c.ctan, 36 * 8 * E)) ||
       (rc = dalloc(c, &c.Ke, (int64_t)NKE * E)) || (rc = dalloc(c, &c.be, 24 * E)) ||
       (rc = dalloc(c, &c.partials, 2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64)) ||
@@ -112,6 +114,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   elastic_C(c.mat.E, c.mat.nu, c.mat.C);
   c.nnz_local = count_nnz_rows(c, g.xs, g.ys, g.zs, g.nx, g.ny, g.nz);
   c.nnz_global = count_nnz_rows(c, 0, 0, 0, o->NX, o->NY, o->NZ);
+  c.nupper_local = count_upper_values(c);
   MCX_HIP(hipStreamSynchronize(c.stream));
   if (lg) {
     lg->members[rank] = &c;
@@ -281,6 +284,16 @@ int mcx_parse_args(mcx_opts* o, int argc, const char* const* argv) {
         I("-ksp_max_it", &o->ksp_max_it) || I("-micro_n", &o->micro_n) || I("-micro_type", &o->micro_type) ||
         A4("-micro_mat_1", o->micro_mat_1) || A4("-micro_mat_2", o->micro_mat_2) || I("-device", &o->device))
       continue;
+    if (!std::strcmp(k, "-dm_mat_type")) {
+      if (!v || (std::strcmp(v, "aij") && std::strcmp(v, "sbaij"))) {
+        set_error(std::string("-dm_mat_type: aij or sbaij, got ") + (v ? v : "(none)"));
+        return 2;
+      }
+      o->mat_type = std::strcmp(v, "sbaij") ? MCX_MAT_AIJ : MCX_MAT_SBAIJ;
+      a++;
+      continue;
+    }
+    if (!std::strcmp(k, "-mat_ignore_lower_triangular")) continue;
     if (!std::strcmp(k, "-ksp_monitor")) {
       o->ksp_monitor = 1;
       continue;
@@ -527,7 +540,8 @@ int mcx_assembly_jac(void* ctx) {
   CTX(ctx);
   PhaseTimer t(c, &c.t.jacobian_ms);
   launch_element_ke(c);
-  launch_gather_matrix(c);
+  if (c.U) launch_gather_matrix_sym(c);
+  else launch_gather_matrix(c);
   MCX_HIP(hipGetLastError());
   return 0;
 }
@@ -679,10 +693,11 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
   const Geo& g = c.g;
   std::vector<double> V;
   if (vals) {
-    V.resize(c.ngroups * NPAIR * 128);
-    MCX_HIP(hipMemcpyAsync(V.data(), c.V, sizeof(double) * V.size(), hipMemcpyDeviceToHost, c.stream));
+    V.resize(c.U ? c.npgroups * UPAIR * 128 : c.ngroups * NPAIR * 128);
+    MCX_HIP(hipMemcpyAsync(V.data(), c.U ? c.U : c.V, sizeof(double) * V.size(), hipMemcpyDeviceToHost, c.stream));
     MCX_HIP(hipStreamSynchronize(c.stream));
   }
+  auto uval = [&](int64_t p, int s) { return V[(p >> 6) * (UPAIR * 128) + (int64_t)(s >> 1) * 128 + 2 * (p & 63) + (s & 1)]; };
   int64_t pos = 0;
   if (rowptr) rowptr[0] = 0;
   std::vector<std::pair<int64_t, double>> row;
@@ -697,7 +712,14 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
         int64_t col0 = 3 * petsc_node(c, hi, hj, hk);
         for (int cc = 0; cc < 3; cc++) {
           double v = 0.;
-          if (vals) {
+          if (vals && c.U) {
+            const int64_t pc = (i + 1) + (j + 1) * (int64_t)g.PX + (k + 1) * (int64_t)g.PX * g.PY;
+            const int64_t q = pc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * (int64_t)g.PX + (nb / 9 - 1) * (int64_t)g.PX * g.PY;
+            static const int dsl[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
+            if (nb < 13) v = uval(q, 6 + 9 * (12 - nb) + cc * 3 + r);
+            else if (nb == 13) v = uval(pc, dsl[r][cc]);
+            else v = uval(pc, 6 + 9 * (nb - 14) + r * 3 + cc);
+          } else if (vals) {
             int s = nb * 9 + r * 3 + cc;
             v = V[(n >> 6) * (NPAIR * 128) + (int64_t)(s >> 1) * 128 + 2 * (n & 63) + (s & 1)];
           }
@@ -777,7 +799,7 @@ int mcx_get_timing(void* ctx, mcx_timing* t) {
   *t = c.t;
   // algorithmic bytes of one SpMV in this format: the stencil-block values actually present
   // (AIJ nonzeros of the owned rows x 8 B), x read once, y written once
-  t->spmv_bytes_per_launch = c.nnz_local * 8 + 2 * 3 * (int64_t)c.g.nown * 8;
+  t->spmv_bytes_per_launch = (c.U ? c.nupper_local : c.nnz_local) * 8 + 2 * 3 * (int64_t)c.g.nown * 8;
   return 0;
 }
 

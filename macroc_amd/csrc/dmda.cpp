@@ -138,7 +138,23 @@ int setup_decomposition(Ctx& c) {
   g.wg = g.dx * c.dy * g.dz / NPE;
   g.rad = o.rad;
   c.ngroups = (g.nown + GROUP - 1) / GROUP;
+  c.npgroups = ((int64_t)g.PX * g.PY * g.PZ + GROUP - 1) / GROUP;
   return 0;
+}
+
+// sbaij: values stored for the owned rows = 6 per node + 9 per in-domain upper neighbour
+int64_t count_upper_values(const Ctx& c) {
+  const Geo& g = c.g;
+  auto cnt = [](int s, int w, int N, int d) {
+    int64_t t = 0;
+    for (int i = s; i < s + w; i++) t += (i + d >= 0 && i + d < N);
+    return t;
+  };
+  int64_t tot = 6 * (int64_t)g.nown;
+  for (int nb = 14; nb < 27; nb++)
+    tot += 9 * cnt(g.xs, g.nx, g.NX, nb % 3 - 1) * cnt(g.ys, g.ny, g.NY, (nb / 3) % 3 - 1) *
+           cnt(g.zs, g.nz, g.NZ, nb / 9 - 1);
+  return tot;
 }
 
 int64_t petsc_node(const Ctx& c, int64_t i, int64_t j, int64_t k) {

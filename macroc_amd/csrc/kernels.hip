@@ -309,48 +309,96 @@ __global__ __launch_bounds__(TPB) void k_element_ke(Geo g, const double* __restr
 // src/bcs.c:341-347) as a deterministic gather: thread = (owned node, neighbour block nb);
 // the 9 entries are 0 + Ke_e1 + Ke_e2 + ... over the shared elements in ascending element
 // order (the reference's insertion order on one rank), then Dirichlet rows/columns.
+// one 3x3 block A(node g, node g+d) of the assembled matrix: 0 + Ke_e1 + Ke_e2 + ... over the
+// shared elements in ascending element order, then MatZeroRowsColumns(diag = 1)
+__device__ __forceinline__ void matrix_block(const Geo& g, const double* __restrict__ Ke, int gi, int gj, int gk,
+                                             int dx, int dy, int dz, double (&val)[9]) {
+  const int hi = gi + dx, hj = gj + dy, hk = gk + dz;
+#pragma unroll
+  for (int q = 0; q < 9; q++) val[q] = 0.;
+  if (gi < 0 || gj < 0 || gk < 0 || gi >= g.NX || gj >= g.NY || gk >= g.NZ) return;
+  if (hi < 0 || hj < 0 || hk < 0 || hi >= g.NX || hj >= g.NY || hk >= g.NZ) return;
+  for (int ez = gk - 1 + (dz > 0); ez <= gk + (dz < 0 ? -1 : 0); ez++) {
+    if (ez < 0 || ez > g.NZ - 2) continue;
+    for (int ey = gj - 1 + (dy > 0); ey <= gj + (dy < 0 ? -1 : 0); ey++) {
+      if (ey < 0 || ey > g.NY - 2) continue;
+      for (int ex = gi - 1 + (dx > 0); ex <= gi + (dx < 0 ? -1 : 0); ex++) {
+        if (ex < 0 || ex > g.NX - 2) continue;
+        const int64_t le = (ex - g.ex0) + (int64_t)(ey - g.ey0) * g.nex + (int64_t)(ez - g.ez0) * g.nex * g.ney;
+        const int a = q1_local(gi - ex, gj - ey, gk - ez);
+        const int bn = q1_local(hi - ex, hj - ey, hk - ez);
+        const double* src = Ke + (int64_t)((a * 8 + bn) * 9) * g.nelem + le;
+#pragma unroll
+        for (int q = 0; q < 9; q++) val[q] += src[(int64_t)q * g.nelem];
+      }
+    }
+  }
+  const int rm = dirichlet_mask(g, gi, gj, gk), cm = dirichlet_mask(g, hi, hj, hk);
+  const bool self = !dx && !dy && !dz;
+#pragma unroll
+  for (int r = 0; r < 3; r++)
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      if (rm >> r & 1) val[r * 3 + c] = (self && r == c) ? 1.0 : 0.0;
+      else if (cm >> c & 1) val[r * 3 + c] = 0.0;
+    }
+}
+
+// MatSetValuesLocal(ADD) + MatAssembly + MatZeroRowsColumns(diag=1) (src/assembly.c:106-112,
+// src/bcs.c:341-347) as a deterministic gather: thread = (owned node, neighbour block nb);
+// the 9 entries are 0 + Ke_e1 + Ke_e2 + ... over the shared elements in ascending element
+// order (the reference's insertion order on one rank), then Dirichlet rows/columns.
 __global__ __launch_bounds__(TPB) void k_gather_matrix(Geo g, const double* __restrict__ Ke, double* __restrict__ V) {
   const int n = blockIdx.x * TPB + threadIdx.x;
   const int nb = blockIdx.y;
   if (n >= g.nown) return;
-  const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
   int i, j, k;
   node_ijk(g, n, i, j, k);
-  const int gi = g.xs + i, gj = g.ys + j, gk = g.zs + k;
-  const int hi = gi + dx, hj = gj + dy, hk = gk + dz;
   double val[9];
-#pragma unroll
-  for (int q = 0; q < 9; q++) val[q] = 0.;
-  if (hi >= 0 && hj >= 0 && hk >= 0 && hi < g.NX && hj < g.NY && hk < g.NZ) {
-    for (int ez = gk - 1 + (dz > 0); ez <= gk + (dz < 0 ? -1 : 0); ez++) {
-      if (ez < 0 || ez > g.NZ - 2) continue;
-      for (int ey = gj - 1 + (dy > 0); ey <= gj + (dy < 0 ? -1 : 0); ey++) {
-        if (ey < 0 || ey > g.NY - 2) continue;
-        for (int ex = gi - 1 + (dx > 0); ex <= gi + (dx < 0 ? -1 : 0); ex++) {
-          if (ex < 0 || ex > g.NX - 2) continue;
-          const int64_t le = (ex - g.ex0) + (int64_t)(ey - g.ey0) * g.nex + (int64_t)(ez - g.ez0) * g.nex * g.ney;
-          const int a = q1_local(gi - ex, gj - ey, gk - ez);
-          const int bn = q1_local(hi - ex, hj - ey, hk - ez);
-          const double* src = Ke + (int64_t)((a * 8 + bn) * 9) * g.nelem + le;
-#pragma unroll
-          for (int q = 0; q < 9; q++) val[q] += src[(int64_t)q * g.nelem];
-        }
-      }
-    }
-    const int rm = dirichlet_mask(g, gi, gj, gk), cm = dirichlet_mask(g, hi, hj, hk);
-#pragma unroll
-    for (int r = 0; r < 3; r++)
-#pragma unroll
-      for (int c = 0; c < 3; c++) {
-        if (rm >> r & 1) val[r * 3 + c] = (nb == 13 && r == c) ? 1.0 : 0.0;
-        else if (cm >> c & 1) val[r * 3 + c] = 0.0;
-      }
-  }
+  matrix_block(g, Ke, g.xs + i, g.ys + j, g.zs + k, nb % 3 - 1, (nb / 3) % 3 - 1, nb / 9 - 1, val);
   double* Vg = V + (int64_t)(n >> 6) * (NPAIR * 128) + 2 * (n & 63);
 #pragma unroll
   for (int q = 0; q < 9; q++) {
     const int s = nb * 9 + q;
     Vg[(s >> 1) * 128 + (s & 1)] = val[q];
+  }
+}
+
+// sbaij storage (PETSc MATSBAIJ semantics): for every node of the padded box the upper
+// triangle of its diagonal block (6 values) and its 13 upper neighbour blocks (nb > 13 =
+// larger natural index).  Ghost-layer nodes store only the blocks pointing at owned nodes
+// (the mirrors the owned rows need); owner-computes covers them (every element shared by a
+// ghost and an owned node touches the owned node).  Thread = (padded node, t): t = 0 the
+// diagonal block, t = 1..13 upper block nb = 13 + t.
+__global__ __launch_bounds__(TPB) void k_gather_matrix_sym(Geo g, const double* __restrict__ Ke,
+                                                           double* __restrict__ U, int npad) {
+  const int p = blockIdx.x * TPB + threadIdx.x;
+  const int t = blockIdx.y;
+  if (p >= npad) return;
+  const int pi = p % g.PX, pj = (p / g.PX) % g.PY, pk = p / (g.PX * g.PY);
+  const int nb = 13 + t;
+  const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
+  const bool owned = pi >= 1 && pi <= g.nx && pj >= 1 && pj <= g.ny && pk >= 1 && pk <= g.nz;
+  const int qi = pi + dx, qj = pj + dy, qk = pk + dz;
+  const bool nbr_owned = qi >= 1 && qi <= g.nx && qj >= 1 && qj <= g.ny && qk >= 1 && qk <= g.nz;
+  double val[9];
+  if (owned || (t > 0 && nbr_owned)) {
+    matrix_block(g, Ke, g.xs + pi - 1, g.ys + pj - 1, g.zs + pk - 1, dx, dy, dz, val);
+  } else {
+#pragma unroll
+    for (int q = 0; q < 9; q++) val[q] = 0.;
+  }
+  double* Ug = U + (int64_t)(p >> 6) * (UPAIR * 128) + 2 * (p & 63);
+  if (t == 0) {
+    const double up[6] = {val[0], val[1], val[2], val[4], val[5], val[8]};
+#pragma unroll
+    for (int s = 0; s < 6; s++) Ug[(s >> 1) * 128 + (s & 1)] = up[s];
+  } else {
+#pragma unroll
+    for (int q = 0; q < 9; q++) {
+      const int s = 6 + 9 * (t - 1) + q;
+      Ug[(s >> 1) * 128 + (s & 1)] = val[q];
+    }
   }
 }
 
@@ -363,6 +411,23 @@ __global__ void k_jacobi(Geo g, const double* __restrict__ V, double* __restrict
   for (int r = 0; r < 3; r++) {
     const int s = 13 * 9 + r * 4;
     double d = Vg[(s >> 1) * 128 + (s & 1)];
+    if (d != 0.0) d = 1.0 / d;
+    if (d == 0.0) d = 1.0;
+    dinv[3 * n + r] = d;
+  }
+}
+
+__global__ void k_jacobi_sym(Geo g, const double* __restrict__ U, double* __restrict__ dinv) {
+  int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  const int pc = pad_of(g, i, j, k);
+  const double* Ug = U + (int64_t)(pc >> 6) * (UPAIR * 128) + 2 * (pc & 63);
+  const int sl[3] = {0, 3, 5};
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    double d = Ug[(sl[r] >> 1) * 128 + (sl[r] & 1)];
     if (d != 0.0) d = 1.0 / d;
     if (d == 0.0) d = 1.0;
     dinv[3 * n + r] = d;
@@ -428,6 +493,75 @@ __global__ __launch_bounds__(TPB) void k_spmv(Geo g, const double2* __restrict__
     y[3 * n + 1] = y1;
     y[3 * n + 2] = y2;
     if (DOT) dot = xv[13][0] * y0 + xv[13][1] * y1 + xv[13][2] * y2;
+  }
+  if (DOT) {
+    double s = block_sum<TPB>(dot, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+  }
+}
+
+// sbaij SpMV: y_n = sum_nb A(n,nb) x_nb in ascending (nb, c) order, where A(n,nb) for nb < 13 is
+// the transpose of the upper block 26-nb stored at node n+off(nb), the diagonal block is
+// mirrored from its upper triangle, nb > 13 comes from node n's own storage.
+template <int NB>
+__device__ __forceinline__ double usl(const double* __restrict__ Ug, int s) {
+  return Ug[(s >> 1) * 128 + (s & 1)];
+}
+
+template <bool DOT, bool GATED>
+__global__ __launch_bounds__(TPB) void k_spmv_sym(Geo g, const double* __restrict__ U, const double* __restrict__ x,
+                                                  double* __restrict__ y, double* __restrict__ part,
+                                                  const CgState* __restrict__ cg, int nblk_padded) {
+  __shared__ double sh[TPB / 64];
+  if (GATED && cg->reason) return;
+  const int lb = xcd_remap(blockIdx.x, nblk_padded);
+  const int n = lb * TPB + threadIdx.x;
+  double dot = 0.;
+  if (n < g.nown) {
+    int i, j, k;
+    node_ijk(g, n, i, j, k);
+    const int PX = g.PX, PXY = g.PX * g.PY;
+    const int pc = (i + 1) + (j + 1) * PX + (k + 1) * PXY;
+    double y0 = 0., y1 = 0., y2 = 0.;
+    double xc0 = 0., xc1 = 0., xc2 = 0.;
+#pragma unroll
+    for (int nb = 0; nb < 27; nb++) {
+      const int off = (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
+      const int q = pc + off;
+      const double* xp = x + 3 * (int64_t)q;
+      const double x0 = xp[0], x1 = xp[1], x2 = xp[2];
+      double a[9];
+      if (nb < 13) {
+        const double* Ug = U + (int64_t)(q >> 6) * (UPAIR * 128) + 2 * (q & 63);
+        const int base = 6 + 9 * (12 - nb);
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+          for (int c = 0; c < 3; c++) a[r * 3 + c] = usl<0>(Ug, base + c * 3 + r);
+      } else if (nb == 13) {
+        const double* Ug = U + (int64_t)(pc >> 6) * (UPAIR * 128) + 2 * (pc & 63);
+        const double d00 = usl<0>(Ug, 0), d01 = usl<0>(Ug, 1), d02 = usl<0>(Ug, 2), d11 = usl<0>(Ug, 3),
+                     d12 = usl<0>(Ug, 4), d22 = usl<0>(Ug, 5);
+        a[0] = d00; a[1] = d01; a[2] = d02;
+        a[3] = d01; a[4] = d11; a[5] = d12;
+        a[6] = d02; a[7] = d12; a[8] = d22;
+        xc0 = x0;
+        xc1 = x1;
+        xc2 = x2;
+      } else {
+        const double* Ug = U + (int64_t)(pc >> 6) * (UPAIR * 128) + 2 * (pc & 63);
+        const int base = 6 + 9 * (nb - 14);
+#pragma unroll
+        for (int s = 0; s < 9; s++) a[s] = usl<0>(Ug, base + s);
+      }
+      y0 += a[0] * x0; y0 += a[1] * x1; y0 += a[2] * x2;
+      y1 += a[3] * x0; y1 += a[4] * x1; y1 += a[5] * x2;
+      y2 += a[6] * x0; y2 += a[7] * x1; y2 += a[8] * x2;
+    }
+    y[3 * n + 0] = y0;
+    y[3 * n + 1] = y1;
+    y[3 * n + 2] = y2;
+    if (DOT) dot = xc0 * y0 + xc1 * y1 + xc2 * y2;
   }
   if (DOT) {
     double s = block_sum<TPB>(dot, sh);
@@ -597,8 +731,16 @@ __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ part
   if (gated && cg->reason) return;
   double res[2] = {0., 0.};
   for (int v = 0; v < nvals; v++) {
-    double acc = 0.;
-    for (int q = threadIdx.x; q < nparts; q += 1024) acc += part[(int64_t)v * nparts + q];
+    // 8 independent accumulators per thread keep 8 loads in flight; fixed combination order
+    const double* pv = part + (int64_t)v * nparts;
+    double a[8] = {0., 0., 0., 0., 0., 0., 0., 0.};
+    int q = threadIdx.x;
+    for (; q + 7 * 1024 < nparts; q += 8 * 1024) {
+#pragma unroll
+      for (int u = 0; u < 8; u++) a[u] += pv[q + u * 1024];
+    }
+    for (; q < nparts; q += 1024) a[0] += pv[q];
+    const double acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     res[v] = block_sum<1024>(acc, sh);
   }
   if (threadIdx.x) return;
@@ -717,12 +859,32 @@ void launch_gather_matrix(Ctx& c) {
   hipLaunchKernelGGL(k_gather_matrix, dim3(nblk(c.g.nown), 27), dim3(TPB), 0, c.stream, c.g, c.Ke, c.V);
 }
 
+void launch_gather_matrix_sym(Ctx& c) {
+  const int npad = c.g.PX * c.g.PY * c.g.PZ;
+  hipLaunchKernelGGL(k_gather_matrix_sym, dim3(nblk(npad), 14), dim3(TPB), 0, c.stream, c.g, c.Ke, c.U, npad);
+}
+
 void launch_jacobi(Ctx& c) {
-  hipLaunchKernelGGL(k_jacobi, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.V, c.dinv);
+  if (c.U)
+    hipLaunchKernelGGL(k_jacobi_sym, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.U, c.dinv);
+  else
+    hipLaunchKernelGGL(k_jacobi, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.V, c.dinv);
 }
 
 void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
   int nb = (int)spmv_grid_blocks(c);
+  if (c.U) {
+    if (dot && gated)
+      hipLaunchKernelGGL((k_spmv_sym<true, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, c.U, xpad, y, c.partials,
+                         c.cg, nb);
+    else if (dot)
+      hipLaunchKernelGGL((k_spmv_sym<true, false>), dim3(nb), dim3(TPB), 0, c.stream, c.g, c.U, xpad, y, c.partials,
+                         c.cg, nb);
+    else
+      hipLaunchKernelGGL((k_spmv_sym<false, false>), dim3(nb), dim3(TPB), 0, c.stream, c.g, c.U, xpad, y, c.partials,
+                         c.cg, nb);
+    return;
+  }
   const double2* V = reinterpret_cast<const double2*>(c.V);
   if (dot && gated)
     hipLaunchKernelGGL((k_spmv<true, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials, c.cg, nb);

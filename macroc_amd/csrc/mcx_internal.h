@@ -17,6 +17,8 @@ constexpr int NSLOT = 243;   // 27 neighbour blocks x 3x3
 constexpr int NPAIR = 122;   // slots stored as double2 pairs (slot 243 = zero pad)
 constexpr int GROUP = 64;    // nodes per AoSoA group (= one wavefront)
 constexpr int NKE = 576;     // 24x24 element matrix
+constexpr int USLOT = 123;   // sbaij: 6 upper-triangle diagonal values + 13 upper blocks x 9
+constexpr int UPAIR = 62;
 
 void set_error(const std::string& s);
 
@@ -98,7 +100,10 @@ struct Ctx {
   double* z = nullptr;
   double* w = nullptr;
   double* dinv = nullptr;    // Jacobi inverse diagonal
-  double* V = nullptr;       // stencil-block matrix, AoSoA [ngroups][NPAIR][64] double2
+  double* V = nullptr;       // aij stencil-block matrix, AoSoA [ngroups][NPAIR][64] double2
+  double* U = nullptr;       // sbaij upper stencil blocks over the padded box [npgroups][UPAIR][64] double2
+  int64_t npgroups = 0;
+  int64_t nupper_local = 0;  // sbaij: stored upper values of the owned rows
   double* eps = nullptr;     // [6][8][nelem]
   double* sig = nullptr;     // [6][8][nelem]
   double* ctan = nullptr;    // [36][8][nelem]
@@ -134,6 +139,7 @@ void plan_halo(Ctx& c, std::vector<int>& sidx, std::vector<int>& ridx);
 int64_t pad_to_natural(const Ctx& c, int p);
 int64_t count_nnz_rows(const Ctx& c, int64_t xs, int64_t ys, int64_t zs, int64_t nx, int64_t ny, int64_t nz);
 void compute_B_table(double B[8][6][24]);
+int64_t count_upper_values(const Ctx& c);
 
 // ---- communication (comm.cpp)
 int comm_init(Ctx& c, const void* id);
@@ -151,6 +157,7 @@ void launch_homogenize(Ctx& c);
 void launch_residual(Ctx& c);          // b + partial sums of b.b
 void launch_element_ke(Ctx& c);
 void launch_gather_matrix(Ctx& c);
+void launch_gather_matrix_sym(Ctx& c);
 void launch_jacobi(Ctx& c);
 void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated);
 void launch_update_u(Ctx& c);

@@ -1003,3 +1003,14 @@ int orc_petsc_numbering(int64_t M, int64_t N, int64_t P, int size, int m, int n,
   free(off);
   return 0;
 }
+
+/* -dm_mat_type sbaij -mat_ignore_lower_triangular [ext]: MATSBAIJ keeps the upper triangle
+   (global column >= row) of what assembly_jac inserts and MatMult uses its transpose for the
+   lower triangle (MatMult_SeqSBAIJ_3).  Emulated by mirroring the assembled AIJ values. */
+void orc_sbaij_mirror(orc_problem* P) {
+  for (int64_t row = 0; row < P->ndofs; row++)
+    for (int64_t q = P->rowptr[row]; q < P->rowptr[row + 1]; q++) {
+      int64_t col = P->colidx[q];
+      if (col < row) P->val[q] = P->val[csr_find(P, col, row)];
+    }
+}

@@ -123,6 +123,7 @@ void orc_homogenize(orc_problem* P);
 void orc_assembly_res(orc_problem* P);
 double orc_norm2(const orc_problem* P, const double* v);
 void orc_assembly_jac(orc_problem* P);
+void orc_sbaij_mirror(orc_problem* P);
 void orc_spmv(const orc_problem* P, const double* x, double* y);
 /* KSPSolve(CG, Jacobi) of A du = b; hist (len maxits+1, may be NULL) = residual history */
 int orc_solve(orc_problem* P, int* its, double* rnorm, int* reason, double* hist);

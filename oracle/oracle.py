@@ -71,7 +71,8 @@ def lib():
         L.orc_get_displacement.argtypes = [P, C.c_int]
         L.orc_get_displacement.restype = C.c_double
         L.orc_apply_bc_u.argtypes = [P, C.c_double]
-        for fn in ("orc_set_strains", "orc_homogenize", "orc_assembly_res", "orc_assembly_jac", "orc_update_u"):
+        for fn in ("orc_set_strains", "orc_homogenize", "orc_assembly_res", "orc_assembly_jac", "orc_update_u",
+                   "orc_sbaij_mirror"):
             getattr(L, fn).argtypes = [P]
         L.orc_norm2.argtypes = [P, d]
         L.orc_norm2.restype = C.c_double
@@ -239,6 +240,10 @@ class Problem:
 
     def assembly_jac(self):
         lib().orc_assembly_jac(self._p)
+
+    def sbaij_mirror(self):
+        """-dm_mat_type sbaij semantics: lower triangle := transpose of the upper triangle."""
+        lib().orc_sbaij_mirror(self._p)
 
     def spmv(self, x):
         x = np.ascontiguousarray(x, dtype=np.float64)

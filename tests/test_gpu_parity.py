@@ -176,3 +176,32 @@ def test_64cubed_properties():
         assert np.array_equal(m.spmv(x), Ax)
     finally:
         m.finish()
+
+
+@pytest.mark.parametrize("NX,NY,NZ", [(8, 8, 8), (16, 16, 16), (12, 7, 9)])
+def test_sbaij_single_rank(NX, NY, NZ):
+    """-dm_mat_type sbaij: matrix and SpMV bit-exact vs the oracle's MATSBAIJ emulation; the
+    solution agrees with the reference's AIJ path within the north-star tolerance."""
+    rtol = 1e-12
+    P = O.Problem(NX, NY, NZ, rtol=rtol)
+    ref_aij = O.Problem(NX, NY, NZ, rtol=rtol)
+    ref_aij.newton_step1()
+    with M.Macroc(argv_for(NX, NY, NZ, rtol, ["-dm_mat_type", "sbaij", "-mat_ignore_lower_triangular"])) as m:
+        for ts in (0, 1):
+            m.apply_bc_on_u(m.get_displacement(ts))
+            P.apply_bc_u(P.get_displacement(ts))
+        m.set_strains(); m.homogenize(); m.assembly_res()
+        P.set_strains(); P.homogenize(); P.assembly_res()
+        m.assembly_jac()
+        P.assembly_jac()
+        P.sbaij_mirror()
+        rp, ci, v = m.dump_csr()
+        assert np.array_equal(v, P.A_values())
+        x = np.random.default_rng(5).uniform(-1, 1, m.n)
+        assert np.array_equal(m.spmv(x), P.spmv(x))
+        its, rn, reason = m.solve_Ax()
+        P.solve()
+        assert abs(its - P.solve()["its"]) <= 1
+        du = m.du()
+        assert np.linalg.norm(du - P.du()) <= 1e-10 * np.linalg.norm(P.du())
+        assert np.linalg.norm(du - ref_aij.du()) <= 1e-10 * np.linalg.norm(ref_aij.du())
