@@ -38,14 +38,17 @@ def rank_grid(n):
     return {1: (1, 1, 1), 2: (2, 1, 1), 4: (2, 2, 1), 8: (2, 2, 2), 16: (4, 2, 2)}.get(n) or (n, 1, 1)
 
 
-def cpu_baseline(N, gpu_its, rtol, ndofs_target, nelem_target, nnz_target):
-    """Oracle (scalar C restatement, 1 thread) on an N^3 sample of the same workload; its
+def cpu_baseline(N, threads, gpu_its, rtol, ndofs_target, nelem_target, nnz_target, cg_cap=200):
+    """The oracle — the C restatement of the reference path, its MPI ranks run as OpenMP threads
+    (one emulated rank per thread, PETSc stash / per-rank dot semantics) — on an N^3 sample of
+    the same workload: full assembly + homogenize + residual, then `cg_cap` CG iterations.  Its
     per-element assembly time and per-(CG iteration x nonzero) time are scaled to the target
     grid with the GPU run's CG iteration count."""
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from oracle import oracle as O
 
-    P = O.Problem(N, N, N, rtol=rtol)
+    used = O.set_threads(threads)
+    P = O.Problem(N, N, N, nranks=used, rtol=rtol, maxits=cg_cap)
     P.apply_bc_u(P.get_displacement(0))
     P.apply_bc_u(P.get_displacement(1))
     t0 = time.perf_counter()
@@ -61,7 +64,7 @@ def cpu_baseline(N, gpu_its, rtol, ndofs_target, nelem_target, nnz_target):
     P.update_u()
     t4 = time.perf_counter()
     nelem = (N - 1) ** 3
-    t_elem = ((t1 - t0) + (t2 - t1)) / nelem
+    t_elem = (t2 - t0) / nelem
     t_it_nnz = (t3 - t2) / max(out["its"], 1) / P.nnz
     t_vec = (t4 - t3) / P.ndofs
     t_target = t_elem * nelem_target + t_it_nnz * gpu_its * nnz_target + t_vec * ndofs_target
@@ -69,11 +72,12 @@ def cpu_baseline(N, gpu_its, rtol, ndofs_target, nelem_target, nnz_target):
     return {
         "value": ndofs_target / t_target,
         "unit": "DOF/s",
-        "cores": 1,
+        "cores": used,
         "kind": "port",
-        "sample": (f"oracle/ (scalar C restatement, gcc -O2, 1 thread) full Newton iteration on {N}^3 "
-                   f"({out['its']} CG its, {t3 - t0:.1f} s); per-element assembly time and per-(CG-iteration x "
-                   f"nonzero) time scaled to the GPU workload with its {gpu_its} CG iterations"),
+        "sample": (f"oracle/ (C restatement of the reference path, gcc -O2, {used} OpenMP threads = {used} emulated "
+                   f"MPI ranks) on {N}^3: assembly {t2 - t0:.1f} s, {out['its']} CG its {t3 - t2:.1f} s; "
+                   f"per-element and per-(CG-iteration x nonzero) times scaled to the GPU workload with its "
+                   f"{gpu_its} CG iterations"),
         "sample_seconds": t4 - t0,
         "extrapolated_step_seconds": t_target,
     }
@@ -86,9 +90,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--grid", type=int, default=256, help="nodes per direction per GPU")
     ap.add_argument("--rtol", type=float, default=1e-8)
-    ap.add_argument("--cpu-sample", type=int, default=40, help="oracle sample grid (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=96, help="oracle sample grid (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16)
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--same-device", action="store_true", help="testing only: every rank on device 0")
+    ap.add_argument("--mat-type", default="aij", choices=["aij", "sbaij"], help="-dm_mat_type")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -101,7 +107,7 @@ def main():
     NX, NY, NZ = G * px, G * py, G * pz
     argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
             "-da_processors_z", pz, "-ts", 2, "-ksp_rtol", repr(args.rtol),
-            "-device", 0 if args.same_device else local]
+            "-device", 0 if args.same_device else local, "-dm_mat_type", args.mat_type]
     comm_id = None
     if world > 1:
         obj = [M.comm_unique_id() if rank == 0 else None]
@@ -171,8 +177,8 @@ def main():
         cpu = None
         if world == 1 and args.cpu_sample > 0:
             try:
-                cpu = cpu_baseline(args.cpu_sample, its, args.rtol, ndofs, (NX - 1) * (NY - 1) * (NZ - 1),
-                                   info["nnz_global"])
+                cpu = cpu_baseline(args.cpu_sample, args.cpu_threads, its, args.rtol, ndofs,
+                                   (NX - 1) * (NY - 1) * (NZ - 1), info["nnz_global"])
             except Exception as e:  # the baseline is reported, never the product path
                 cpu = {"error": repr(e)}
         line = {
@@ -190,7 +196,7 @@ def main():
             "data": "synthetic (reference defaults: lx=50 ly=1 lz=50, BC_CIRCLE, E=1e7 nu=0.25, time step 1)",
             "config": {"workload": f"MacroC Newton iteration, time step 1, CG/Jacobi rtol {args.rtol:g}",
                        "grid": [NX, NY, NZ], "grid_per_gpu": [G, G, G], "processors": [px, py, pz],
-                       "dofs": ndofs, "nnz": info["nnz_global"], "parallelism": f"dmda{px}x{py}x{pz}"},
+                       "dofs": ndofs, "nnz": info["nnz_global"], "parallelism": f"dmda{px}x{py}x{pz}", "mat_type": args.mat_type},
             "cg_its": its,
             "ms_per_cg_iter": tm["solve_ms"] / max(its, 1),
             "phases_ms": {k: tm[k] for k in ("strains_ms", "homogenize_ms", "residual_ms", "jacobian_ms",

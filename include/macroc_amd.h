@@ -180,6 +180,10 @@ int mcx_get_ksp_history(void* ctx, double* hist, int64_t* n);
 int mcx_set_timing(void* ctx, int on);
 int mcx_get_timing(void* ctx, mcx_timing* t);
 int mcx_synchronize(void* ctx);
+/* tuning knobs ("spmv_subl": lines per sub-slab of the SpMV sweep, 0 = whole XCD slab) and a
+   device-only SpMV timer (iters launches on the current search direction, HIP events) */
+int mcx_set_option(void* ctx, const char* name, double value);
+int mcx_time_spmv(void* ctx, int iters, double* avg_ms);
 
 #ifdef __cplusplus
 }

@@ -36,7 +36,7 @@ EXPORTS = [
     "mcx_set_strains", "mcx_homogenize", "mcx_assembly_res", "mcx_assembly_jac", "mcx_solve", "mcx_update_u",
     "mcx_time_step", "mcx_get_u", "mcx_set_u", "mcx_get_b", "mcx_get_du", "mcx_get_strain", "mcx_get_stress",
     "mcx_owned_dofs", "mcx_dump_csr", "mcx_dump_dirichlet", "mcx_spmv", "mcx_get_ksp_history",
-    "mcx_set_timing", "mcx_get_timing", "mcx_synchronize",
+    "mcx_set_timing", "mcx_get_timing", "mcx_synchronize", "mcx_set_option", "mcx_time_spmv",
 ]
 
 
@@ -130,6 +130,8 @@ def lib():
     L.mcx_get_ksp_history.argtypes = [vp, d, i64]
     L.mcx_set_timing.argtypes = [vp, C.c_int]
     L.mcx_get_timing.argtypes = [vp, C.POINTER(Timing)]
+    L.mcx_set_option.argtypes = [vp, C.c_char_p, C.c_double]
+    L.mcx_time_spmv.argtypes = [vp, C.c_int, d]
     _LIB = L
     return L
 
@@ -356,6 +358,14 @@ class Macroc:
 
     def set_timing(self, on=True):
         _check(lib().mcx_set_timing(self._ctx, 1 if on else 0), "mcx_set_timing")
+
+    def set_option(self, name, value):
+        _check(lib().mcx_set_option(self._ctx, name.encode(), float(value)), "mcx_set_option")
+
+    def time_spmv(self, iters=20):
+        ms = C.c_double()
+        _check(lib().mcx_time_spmv(self._ctx, int(iters), C.byref(ms)), "mcx_time_spmv")
+        return ms.value
 
     def timing(self):
         t = Timing()

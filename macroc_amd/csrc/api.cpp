@@ -102,7 +102,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
       (rc = dalloc(c, &c.eps, 6 * 8 * E)) ||
       (rc = dalloc(c, &c.sig, 6 * 8 * E)) || (rc = dalloc(c, &c.ctan, 36 * 8 * E)) ||
       (rc = dalloc(c, &c.Ke, (int64_t)NKE * E)) || (rc = dalloc(c, &c.be, 24 * E)) ||
-      (rc = dalloc(c, &c.partials, 2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64)) ||
+      (rc = dalloc(c, &c.partials, c.partials_cap = 4 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64)) ||
       (rc = dalloc(c, &c.red, 16)) || (rc = dalloc(c, &c.red_loc, 16)) || (rc = dalloc(c, &c.cg, 1)) ||
       (rc = dalloc(c, &c.hist, (int64_t)o->ksp_max_it + 2)))
     return rc;
@@ -800,6 +800,35 @@ int mcx_get_timing(void* ctx, mcx_timing* t) {
   // algorithmic bytes of one SpMV in this format: the stencil-block values actually present
   // (AIJ nonzeros of the owned rows x 8 B), x read once, y written once
   t->spmv_bytes_per_launch = (c.U ? c.nupper_local : c.nnz_local) * 8 + 2 * 3 * (int64_t)c.g.nown * 8;
+  return 0;
+}
+
+int mcx_set_option(void* ctx, const char* name, double value) {
+  GUARD(ctx);
+  CTX(ctx);
+  if (!std::strcmp(name, "spmv_subl")) {
+    c.spmv_subl = (int)value;
+    if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
+      set_error("spmv_subl: partials buffer too small");
+      return 2;
+    }
+    return 0;
+  }
+  set_error(std::string("unknown option ") + name);
+  return 2;
+}
+
+int mcx_time_spmv(void* ctx, int iters, double* avg_ms) {
+  GUARD(ctx);
+  CTX(ctx);
+  launch_spmv(c, c.p_pad, c.w, true, false);  // warm
+  MCX_HIP(hipEventRecord(c.ev_a, c.stream));
+  for (int q = 0; q < iters; q++) launch_spmv(c, c.p_pad, c.w, true, false);
+  MCX_HIP(hipEventRecord(c.ev_b, c.stream));
+  MCX_HIP(hipEventSynchronize(c.ev_b));
+  float ms = 0.f;
+  MCX_HIP(hipEventElapsedTime(&ms, c.ev_a, c.ev_b));
+  *avg_ms = ms / std::max(iters, 1);
   return 0;
 }
 

@@ -12,6 +12,7 @@
 // Compiled with -ffp-contract=off: each product / sum is rounded as the reference writes it,
 // so element kinematics, strains, stresses, element matrices, the assembled matrix, the
 // residual and the SpMV are bit-identical to the CPU restatement on one rank.
+#include <algorithm>
 #include <cmath>
 
 #include "mcx_internal.h"
@@ -86,6 +87,67 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk_padded) {
 }
 
 static inline int64_t pad8(int64_t n) { return (n + 7) / 8 * 8; }
+
+// SpMV block tiling, XCD-slab order.  A block = TX nodes along x (TX = 64*ceil(nx/64), <= 256)
+// x LPB = 256/TX consecutive y-lines, at one z-plane.  The y-line groups are cut into 8
+// contiguous slabs, one per XCD (blocks b and b+8 share an XCD under the observed round-robin
+// placement — speed only), and each XCD sweeps its slab plane by plane, so the stencil's
+// previous-plane neighbours (x values, sbaij mirror blocks) of a plane are still in that XCD's
+// L2 when the next plane is processed.
+struct SpmvTiling {
+  int TX, LPB, nxc, jgroups, per_xcd;  // per_xcd = max blocks on one XCD
+  int subl;                            // lines per sub-slab (0 = whole slab per plane)
+};
+
+static SpmvTiling spmv_tiling(const Geo& g, int subl) {
+  SpmvTiling t;
+  t.subl = subl;
+  t.TX = (int)std::min<int64_t>(256, (g.nx + 63) / 64 * 64);
+  t.LPB = 256 / t.TX;
+  t.nxc = (g.nx + t.TX - 1) / t.TX;
+  t.jgroups = (g.ny + t.LPB - 1) / t.LPB;
+  const int slab = (t.jgroups + 7) / 8;
+  t.per_xcd = slab * g.nz * t.nxc;
+  return t;
+}
+
+// returns the owned node of this thread or -1.  Within an XCD's slab the lines are swept in
+// sub-slabs of SUBL lines over all planes (sub-slab, k, line group, x chunk), so one plane of
+// a sub-slab (SUBL x nx nodes, ~2 MB of sbaij blocks at nx = 256) stays in the XCD's 4 MB L2
+// until the next plane reads its mirror blocks; only sub-slab edge lines miss.
+__device__ __forceinline__ int spmv_node(const Geo& g, int TX, int LPB, int nxc, int jgroups, int subl, int& ii,
+                                         int& jj, int& kk) {
+  const int b = blockIdx.x;
+  const int x = b & 7;
+  int t = b >> 3;
+  const int slab = (jgroups + 7) >> 3;
+  const int g0 = x * slab;
+  const int gcount = min(slab, jgroups - g0);
+  if (gcount <= 0) return -1;
+  const int SG = subl > 0 ? max(1, subl / LPB) : gcount;  // line groups per sub-slab
+  const int full = gcount / SG;
+  const int per_sub = SG * g.nz * nxc;
+  int sub, sgn;
+  if (t < full * per_sub) {
+    sub = t / per_sub;
+    t -= sub * per_sub;
+    sgn = SG;
+  } else {
+    t -= full * per_sub;
+    sub = full;
+    sgn = gcount - full * SG;
+    if (sgn <= 0 || t >= sgn * g.nz * nxc) return -1;
+  }
+  const int k = t / (sgn * nxc);
+  const int rem = t - k * (sgn * nxc);
+  const int gg = g0 + sub * SG + rem / nxc, c = rem % nxc;
+  const int i = c * TX + (int)(threadIdx.x % TX), j = gg * LPB + (int)(threadIdx.x / TX);
+  if (i >= g.nx || j >= g.ny) return -1;
+  ii = i;
+  jj = j;
+  kk = k;
+  return i + j * g.nx + k * g.nx * g.ny;
+}
 
 // ---------------------------------------------------------------------------- BC on u
 // apply_bc_on_u -> bc_apply_on_u_circle / _bending (src/bcs.c:29-146)
@@ -466,15 +528,13 @@ struct PairLoop<0> {
 template <bool DOT, bool GATED>
 __global__ __launch_bounds__(TPB) void k_spmv(Geo g, const double2* __restrict__ V, const double* __restrict__ x,
                                               double* __restrict__ y, double* __restrict__ part,
-                                              const CgState* __restrict__ cg, int nblk_padded) {
+                                              const CgState* __restrict__ cg, SpmvTiling tl) {
   __shared__ double sh[TPB / 64];
   if (GATED && cg->reason) return;
-  const int lb = xcd_remap(blockIdx.x, nblk_padded);
-  const int n = lb * TPB + threadIdx.x;
+  int i = 0, j = 0, k = 0;
+  const int n = spmv_node(g, tl.TX, tl.LPB, tl.nxc, tl.jgroups, tl.subl, i, j, k);
   double dot = 0.;
-  if (n < g.nown) {
-    int i, j, k;
-    node_ijk(g, n, i, j, k);
+  if (n >= 0) {
     const int PX = g.PX, PXY = g.PX * g.PY;
     const int pc = (i + 1) + (j + 1) * PX + (k + 1) * PXY;
     double xv[27][3];
@@ -511,15 +571,13 @@ __device__ __forceinline__ double usl(const double* __restrict__ Ug, int s) {
 template <bool DOT, bool GATED>
 __global__ __launch_bounds__(TPB) void k_spmv_sym(Geo g, const double* __restrict__ U, const double* __restrict__ x,
                                                   double* __restrict__ y, double* __restrict__ part,
-                                                  const CgState* __restrict__ cg, int nblk_padded) {
+                                                  const CgState* __restrict__ cg, SpmvTiling tl) {
   __shared__ double sh[TPB / 64];
   if (GATED && cg->reason) return;
-  const int lb = xcd_remap(blockIdx.x, nblk_padded);
-  const int n = lb * TPB + threadIdx.x;
+  int i = 0, j = 0, k = 0;
+  const int n = spmv_node(g, tl.TX, tl.LPB, tl.nxc, tl.jgroups, tl.subl, i, j, k);
   double dot = 0.;
-  if (n < g.nown) {
-    int i, j, k;
-    node_ijk(g, n, i, j, k);
+  if (n >= 0) {
     const int PX = g.PX, PXY = g.PX * g.PY;
     const int pc = (i + 1) + (j + 1) * PX + (k + 1) * PXY;
     double y0 = 0., y1 = 0., y2 = 0.;
@@ -822,7 +880,7 @@ static inline unsigned nblk(int64_t n) { return (unsigned)((n + TPB - 1) / TPB);
 int dirichlet_mask_host(const Geo& g, int gi, int gj, int gk) { return dirichlet_mask(g, gi, gj, gk); }
 
 int64_t node_blocks(const Ctx& c) { return nblk(c.g.nown); }
-int64_t spmv_grid_blocks(const Ctx& c) { return pad8(nblk(c.g.nown)); }
+int64_t spmv_grid_blocks(const Ctx& c) { return 8 * (int64_t)spmv_tiling(c.g, c.spmv_subl).per_xcd; }
 
 int upload_constants(Ctx& c) {
   double B[8][6][24];
@@ -872,26 +930,27 @@ void launch_jacobi(Ctx& c) {
 }
 
 void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
-  int nb = (int)spmv_grid_blocks(c);
+  const int nb = (int)spmv_grid_blocks(c);
+  const SpmvTiling tl = spmv_tiling(c.g, c.spmv_subl);
   if (c.U) {
     if (dot && gated)
       hipLaunchKernelGGL((k_spmv_sym<true, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, c.U, xpad, y, c.partials,
-                         c.cg, nb);
+                         c.cg, tl);
     else if (dot)
       hipLaunchKernelGGL((k_spmv_sym<true, false>), dim3(nb), dim3(TPB), 0, c.stream, c.g, c.U, xpad, y, c.partials,
-                         c.cg, nb);
+                         c.cg, tl);
     else
       hipLaunchKernelGGL((k_spmv_sym<false, false>), dim3(nb), dim3(TPB), 0, c.stream, c.g, c.U, xpad, y, c.partials,
-                         c.cg, nb);
+                         c.cg, tl);
     return;
   }
   const double2* V = reinterpret_cast<const double2*>(c.V);
   if (dot && gated)
-    hipLaunchKernelGGL((k_spmv<true, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials, c.cg, nb);
+    hipLaunchKernelGGL((k_spmv<true, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials, c.cg, tl);
   else if (dot)
-    hipLaunchKernelGGL((k_spmv<true, false>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials, c.cg, nb);
+    hipLaunchKernelGGL((k_spmv<true, false>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials, c.cg, tl);
   else
-    hipLaunchKernelGGL((k_spmv<false, false>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials, c.cg, nb);
+    hipLaunchKernelGGL((k_spmv<false, false>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials, c.cg, tl);
 }
 
 void launch_update_u(Ctx& c) {

@@ -104,6 +104,8 @@ struct Ctx {
   double* U = nullptr;       // sbaij upper stencil blocks over the padded box [npgroups][UPAIR][64] double2
   int64_t npgroups = 0;
   int64_t nupper_local = 0;  // sbaij: stored upper values of the owned rows
+  int spmv_subl = 0;
+  int64_t partials_cap = 0;         // SpMV sweep: lines per sub-slab of an XCD's slab (0 = whole slab)
   double* eps = nullptr;     // [6][8][nelem]
   double* sig = nullptr;     // [6][8][nelem]
   double* ctan = nullptr;    // [36][8][nelem]

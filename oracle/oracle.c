@@ -643,6 +643,7 @@ void orc_apply_bc_u(orc_problem* P, double U) {
 
 /* set_strains src/assembly.c:25-66 (per rank, elements in DMDAGetElements order) */
 void orc_set_strains(orc_problem* P) {
+#pragma omp parallel for schedule(dynamic, 1)
   for (int r = 0; r < P->nranks; r++) {
     int64_t c[12];
     orc_rank_corners(P, r, c);
@@ -670,6 +671,7 @@ void orc_set_strains(orc_problem* P) {
 
 /* MicroPP surrogate (micropp_C_homogenize, src/main.c:62): sigma = C eps */
 void orc_homogenize(orc_problem* P) {
+#pragma omp parallel for schedule(static)
   for (int64_t g = 0; g < P->ngp; g++) {
     const double* e = P->eps + g * NVOI;
     double* s = P->sig + g * NVOI;
@@ -686,6 +688,7 @@ void orc_homogenize(orc_problem* P) {
 void orc_assembly_res(orc_problem* P) {
   memset(P->b, 0, P->ndofs * sizeof(double));
   double** bloc = malloc(P->nranks * sizeof(double*));
+#pragma omp parallel for schedule(dynamic, 1)
   for (int r = 0; r < P->nranks; r++) {
     int64_t c[12];
     orc_rank_corners(P, r, c);
@@ -708,6 +711,7 @@ void orc_assembly_res(orc_problem* P) {
     free(conn);
   }
   /* owned entries */
+#pragma omp parallel for schedule(dynamic, 1)
   for (int r = 0; r < P->nranks; r++) {
     int64_t c[12];
     orc_rank_corners(P, r, c);
@@ -719,6 +723,7 @@ void orc_assembly_res(orc_problem* P) {
     }
   }
   /* ghost entries, by destination then source rank */
+#pragma omp parallel for schedule(dynamic, 1)
   for (int dst = 0; dst < P->nranks; dst++)
     for (int r = 0; r < P->nranks; r++) {
       if (r == dst) continue;
@@ -735,27 +740,36 @@ void orc_assembly_res(orc_problem* P) {
   free(bloc);
   /* apply_bc_on_res src/bcs.c:350-362, then VecScale(b,-1) src/assembly.c:173 */
   for (int64_t q = 0; q < P->ndir; q++) P->b[P->dir[q]] = 0.;
+#pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < P->ndofs; i++) P->b[i] = P->b[i] * -1.;
 }
 
 /* VecNorm(NORM_2) — per-rank partial sums, summed in rank order [ext] */
 double orc_norm2(const orc_problem* P, const double* v) {
-  double tot = 0.;
+  double* part = malloc(P->nranks * sizeof(double));
+#pragma omp parallel for schedule(static)
   for (int r = 0; r < P->nranks; r++) {
     double s = 0.;
     for (int64_t i = 3 * P->node_off[r]; i < 3 * P->node_off[r + 1]; i++) s += v[i] * v[i];
-    tot += s;
+    part[r] = s;
   }
+  double tot = 0.;
+  for (int r = 0; r < P->nranks; r++) tot += part[r];
+  free(part);
   return sqrt(tot);
 }
 
 static double dot(const orc_problem* P, const double* x, const double* y) {
-  double tot = 0.;
+  double* part = malloc(P->nranks * sizeof(double));
+#pragma omp parallel for schedule(static)
   for (int r = 0; r < P->nranks; r++) {
     double s = 0.;
     for (int64_t i = 3 * P->node_off[r]; i < 3 * P->node_off[r + 1]; i++) s += x[i] * y[i];
-    tot += s;
+    part[r] = s;
   }
+  double tot = 0.;
+  for (int r = 0; r < P->nranks; r++) tot += part[r];
+  free(part);
   return tot;
 }
 
@@ -767,8 +781,9 @@ void orc_assembly_jac(orc_problem* P) {
   int64_t* ns = calloc(P->nranks * P->nranks, sizeof(int64_t));
   int64_t* cap = calloc(P->nranks * P->nranks, sizeof(int64_t));
   stash_entry** st = calloc(P->nranks * P->nranks, sizeof(stash_entry*));
-  double Ae[NPE * DIM * NPE * DIM];
+#pragma omp parallel for schedule(dynamic, 1)
   for (int r = 0; r < P->nranks; r++) {
+    double Ae[NPE * DIM * NPE * DIM];
     int64_t c[12];
     orc_rank_corners(P, r, c);
     int64_t ne = P->ne[r];
@@ -805,6 +820,7 @@ void orc_assembly_jac(orc_problem* P) {
     }
     free(conn);
   }
+#pragma omp parallel for schedule(dynamic, 1)
   for (int dst = 0; dst < P->nranks; dst++)
     for (int src = 0; src < P->nranks; src++) {
       int q = dst * P->nranks + src;
@@ -813,6 +829,7 @@ void orc_assembly_jac(orc_problem* P) {
     }
   free(st); free(ns); free(cap);
   /* MatZeroRowsColumns(A, n, rows, 1.0, NULL, NULL) over the union of rank lists */
+#pragma omp parallel for schedule(static)
   for (int64_t row = 0; row < P->ndofs; row++) {
     int rowD = is_dirichlet(P, row);
     for (int64_t q = P->rowptr[row]; q < P->rowptr[row + 1]; q++) {
@@ -826,6 +843,7 @@ void orc_assembly_jac(orc_problem* P) {
 /* MatMult: rows summed in ascending column order (MatMult_SeqAIJ); with several ranks the
    MPIAIJ split is emulated: owned-column block first, then off-rank columns [ext] */
 void orc_spmv(const orc_problem* P, const double* x, double* y) {
+#pragma omp parallel for schedule(static)
   for (int r = 0; r < P->nranks; r++) {
     int64_t c0 = 3 * P->node_off[r], c1 = 3 * P->node_off[r + 1];
     for (int64_t row = c0; row < c1; row++) {
@@ -857,6 +875,7 @@ int orc_solve(orc_problem* P, int* its_out, double* rnorm_out, int* reason_out, 
   int64_t N = P->ndofs;
   double *X = P->du, *R = P->r, *Z = P->z, *Pv = P->pp, *W = P->w;
   /* PCSetUp_Jacobi: diag, VecReciprocal (zeros untouched), then zeros -> 1 */
+  #pragma omp parallel for schedule(static)
   for (int64_t row = 0; row < N; row++) {
     double d = P->val[csr_find(P, row, row)];
     if (d != 0.0) d = 1.0 / d;
@@ -867,6 +886,7 @@ int orc_solve(orc_problem* P, int* its_out, double* rnorm_out, int* reason_out, 
   int reason = 0, its = 0, i;
   memset(X, 0, N * sizeof(double));                       /* guess zero */
   memcpy(R, P->b, N * sizeof(double));                    /* r <- b */
+  #pragma omp parallel for schedule(static)
   for (int64_t q = 0; q < N; q++) Z[q] = R[q] * P->dinv[q]; /* z <- Br */
   dp = orc_norm2(P, Z);
   if (hist) hist[0] = dp;
@@ -890,6 +910,7 @@ int orc_solve(orc_problem* P, int* its_out, double* rnorm_out, int* reason_out, 
       b = 0.0;
     } else {
       b = beta / betaold;
+      #pragma omp parallel for schedule(static)
       for (int64_t q = 0; q < N; q++) Pv[q] = Z[q] + b * Pv[q]; /* VecAYPX */
     }
     dpiold = dpi;
@@ -901,8 +922,11 @@ int orc_solve(orc_problem* P, int* its_out, double* rnorm_out, int* reason_out, 
       break;
     }
     a = beta / dpi;
+    #pragma omp parallel for schedule(static)
     for (int64_t q = 0; q < N; q++) X[q] = X[q] + a * Pv[q];
+    #pragma omp parallel for schedule(static)
     for (int64_t q = 0; q < N; q++) R[q] = R[q] + (-a) * W[q];
+    #pragma omp parallel for schedule(static)
     for (int64_t q = 0; q < N; q++) Z[q] = R[q] * P->dinv[q];
     dp = orc_norm2(P, Z);
     rnorm = dp;
@@ -1013,4 +1037,18 @@ void orc_sbaij_mirror(orc_problem* P) {
       int64_t col = P->colidx[q];
       if (col < row) P->val[q] = P->val[csr_find(P, col, row)];
     }
+}
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+/* threads used by the emulated ranks (bench cpu_baseline); returns the count in effect */
+int orc_set_threads(int n) {
+#ifdef _OPENMP
+  if (n > 0) omp_set_num_threads(n);
+  return omp_get_max_threads();
+#else
+  (void)n;
+  return 1;
+#endif
 }

@@ -132,6 +132,7 @@ void orc_update_u(orc_problem* P);
 /* full run of src/main.c:49-109; writes log lines to `log` (may be NULL).
    newton_out: per (time step, newton it) records: |RES|, ksp its, ksp rnorm (cap entries) */
 int orc_run(orc_problem* P, const char* log_path, double* t_newton_solve_s);
+int orc_set_threads(int n);
 
 #ifdef __cplusplus
 }

@@ -81,6 +81,8 @@ def lib():
         L.orc_dmda_decide.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int,
                                       C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.orc_run.argtypes = [P, C.c_char_p, d]
+        L.orc_set_threads.argtypes = [C.c_int]
+        L.orc_set_threads.restype = C.c_int
         L.orc_petsc_numbering.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int,
                                           C.POINTER(C.c_int64)]
         _LIB = L
@@ -103,6 +105,11 @@ def dmda_decide(M, N, P, size, m=0, n=0, p=0):
     if rc:
         raise ValueError(f"no DMDA partition (code {rc})")
     return mm.value, nn.value, pp.value
+
+
+def set_threads(n):
+    """OpenMP threads for the emulated ranks; returns the thread count in effect."""
+    return lib().orc_set_threads(int(n))
 
 
 def petsc_numbering(M, N, P, size, m=0, n=0, p=0):

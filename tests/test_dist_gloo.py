@@ -31,6 +31,7 @@ def _worker(rank, world, port, grid, procs, q):
     import macroc_amd as M
     from oracle import oracle as O
 
+    O.set_threads(1)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
