@@ -58,8 +58,8 @@ enum {
    lower triangle mirrored from it) */
 enum { MCX_MAT_AIJ = 0, MCX_MAT_SBAIJ = 1 };
 
-/* constitutive models behind the Gauss-point callback */
-enum { MCX_MAT_ELASTIC = 0 };
+/* constitutive laws behind the Gauss-point callback (-mat_law elastic|plastic) */
+enum { MCX_LAW_ELASTIC = 0, MCX_LAW_PLASTIC = 1 };
 
 typedef struct {
   int64_t NX, NY, NZ;          /* -da_grid_x/y/z          (default 40 3 40, include/macroc.h:44-46) */
@@ -81,6 +81,8 @@ typedef struct {
   int device;                  /* HIP device of this rank (-1: rank % device count) */
   int ksp_monitor;             /* -ksp_monitor: keep the residual history */
   int mat_type;                /* -dm_mat_type aij|sbaij  (MCX_MAT_AIJ) */
+  int mat_law;                 /* -mat_law elastic|plastic (MCX_LAW_ELASTIC; plastic = J2 with
+                                  micro_mat_1's Sy, Ka: MicroPP material type 1) */
 } mcx_opts;
 
 typedef struct {
@@ -152,6 +154,11 @@ int mcx_assembly_res(void* ctx, double* norm2);
 int mcx_assembly_jac(void* ctx);
 int mcx_solve(void* ctx, int* its, double* rnorm, int* reason);
 int mcx_update_u(void* ctx);
+/* micropp_C_update_vars (src/main.c:83): commit the Gauss-point history of the time step */
+int mcx_update_vars(void* ctx);
+/* get_non_linear_gps / get_f_trial_max (src/util.c:69-102) over this rank's PETSc-owned
+   elements: GPs with f_trial > 0 in the last homogenize, and the max f_trial */
+int mcx_get_nonlinear_stats(void* ctx, int64_t* n_nonlinear, double* f_trial_max);
 
 /* src/main.c:57-82 for one time step; returns Newton iterations done, per-iteration
    |RES|, KSP its and KSP rnorm in caller arrays of length >= newton_max_its (may be NULL) */

@@ -33,7 +33,8 @@ EXPORTS = [
     "mcx_last_error", "mcx_version", "mcx_default_opts", "mcx_parse_args", "mcx_comm_unique_id", "mcx_plan", "mcx_plan_halo", "mcx_init",
     "mcx_local_group_create", "mcx_local_group_destroy", "mcx_init_local",
     "mcx_finalize", "mcx_get_info", "mcx_material_set", "mcx_get_displacement", "mcx_zero_u", "mcx_apply_bc_u",
-    "mcx_set_strains", "mcx_homogenize", "mcx_assembly_res", "mcx_assembly_jac", "mcx_solve", "mcx_update_u",
+    "mcx_set_strains", "mcx_homogenize", "mcx_assembly_res", "mcx_assembly_jac", "mcx_solve", "mcx_update_u", "mcx_update_vars",
+    "mcx_get_nonlinear_stats",
     "mcx_time_step", "mcx_get_u", "mcx_set_u", "mcx_get_b", "mcx_get_du", "mcx_get_strain", "mcx_get_stress",
     "mcx_owned_dofs", "mcx_dump_csr", "mcx_dump_dirichlet", "mcx_spmv", "mcx_get_ksp_history",
     "mcx_set_timing", "mcx_get_timing", "mcx_synchronize", "mcx_set_option", "mcx_time_spmv",
@@ -51,7 +52,7 @@ class Opts(C.Structure):
         ("ksp_rtol", C.c_double), ("ksp_abstol", C.c_double), ("ksp_dtol", C.c_double),
         ("ksp_max_it", C.c_int), ("micro_n", C.c_int), ("micro_type", C.c_int),
         ("micro_mat_1", C.c_double * 4), ("micro_mat_2", C.c_double * 4),
-        ("device", C.c_int), ("ksp_monitor", C.c_int), ("mat_type", C.c_int),
+        ("device", C.c_int), ("ksp_monitor", C.c_int), ("mat_type", C.c_int), ("mat_law", C.c_int),
     ]
 
 
@@ -116,7 +117,8 @@ def lib():
     L.mcx_get_displacement.argtypes = [vp, C.c_int]
     L.mcx_get_displacement.restype = C.c_double
     L.mcx_apply_bc_u.argtypes = [vp, C.c_double]
-    for fn in ("mcx_zero_u", "mcx_set_strains", "mcx_homogenize", "mcx_assembly_jac", "mcx_update_u", "mcx_synchronize"):
+    for fn in ("mcx_zero_u", "mcx_set_strains", "mcx_homogenize", "mcx_assembly_jac", "mcx_update_u",
+               "mcx_synchronize", "mcx_update_vars"):
         getattr(L, fn).argtypes = [vp]
     L.mcx_assembly_res.argtypes = [vp, d]
     L.mcx_solve.argtypes = [vp, C.POINTER(C.c_int), d, C.POINTER(C.c_int)]
@@ -124,6 +126,7 @@ def lib():
     for fn in ("mcx_get_u", "mcx_set_u", "mcx_get_b", "mcx_get_du", "mcx_get_strain", "mcx_get_stress"):
         getattr(L, fn).argtypes = [vp, d]
     L.mcx_owned_dofs.argtypes = [vp, i64, i64]
+    L.mcx_get_nonlinear_stats.argtypes = [vp, i64, d]
     L.mcx_dump_csr.argtypes = [vp, i64, i64, d]
     L.mcx_dump_dirichlet.argtypes = [vp, i64, i64]
     L.mcx_spmv.argtypes = [vp, d, d]
@@ -282,6 +285,14 @@ class Macroc:
 
     def update_u(self):
         _check(lib().mcx_update_u(self._ctx), "VecAXPY(u,1,du)")
+
+    def update_vars(self):
+        _check(lib().mcx_update_vars(self._ctx), "micropp_C_update_vars")
+
+    def nonlinear_stats(self):
+        n, f = C.c_int64(), C.c_double()
+        _check(lib().mcx_get_nonlinear_stats(self._ctx, C.byref(n), C.byref(f)), "nonlinear_stats")
+        return n.value, f.value
 
     def time_step(self, time_s):
         k = max(self.opts.newton_max_its, 1)

@@ -53,7 +53,7 @@ static int free_ctx(Ctx* c) {
   if (!c) return 0;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->V, c->U, c->eps, c->sig, c->ctan,
+  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->V, c->U, c->eps, c->sig, c->ctan,
                   c->Ke, c->be, c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf};
   for (void* p : ptrs)
@@ -106,11 +106,17 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
       (rc = dalloc(c, &c.red, 16)) || (rc = dalloc(c, &c.red_loc, 16)) || (rc = dalloc(c, &c.cg, 1)) ||
       (rc = dalloc(c, &c.hist, (int64_t)o->ksp_max_it + 2)))
     return rc;
+  if (o->mat_law == MCX_LAW_PLASTIC &&
+      ((rc = dalloc(c, &c.hist_old, 7 * 8 * E)) || (rc = dalloc(c, &c.hist_new, 7 * 8 * E)) ||
+       (rc = dalloc(c, &c.ftrial, 8 * E))))
+    return rc;
   MCX_HIP(hipHostMalloc((void**)&c.h_cg, sizeof(CgState) * 2, hipHostMallocDefault));
   std::memset(c.h_cg, 0, sizeof(CgState) * 2);
-  c.mat.kind = MCX_MAT_ELASTIC;
+  c.mat.law = o->mat_law;
   c.mat.E = o->micro_mat_1[0];
   c.mat.nu = o->micro_mat_1[1];
+  c.mat.Sy = o->micro_mat_1[2];
+  c.mat.Ka = o->micro_mat_1[3];
   elastic_C(c.mat.E, c.mat.nu, c.mat.C);
   c.nnz_local = count_nnz_rows(c, g.xs, g.ys, g.zs, g.nx, g.ny, g.nz);
   c.nnz_global = count_nnz_rows(c, 0, 0, 0, o->NX, o->NY, o->NZ);
@@ -294,6 +300,15 @@ int mcx_parse_args(mcx_opts* o, int argc, const char* const* argv) {
       continue;
     }
     if (!std::strcmp(k, "-mat_ignore_lower_triangular")) continue;
+    if (!std::strcmp(k, "-mat_law")) {
+      if (!v || (std::strcmp(v, "elastic") && std::strcmp(v, "plastic"))) {
+        set_error(std::string("-mat_law: elastic or plastic, got ") + (v ? v : "(none)"));
+        return 2;
+      }
+      o->mat_law = std::strcmp(v, "plastic") ? MCX_LAW_ELASTIC : MCX_LAW_PLASTIC;
+      a++;
+      continue;
+    }
     if (!std::strcmp(k, "-ksp_monitor")) {
       o->ksp_monitor = 1;
       continue;
@@ -468,8 +483,10 @@ int mcx_material_set(void* ctx, int id, double E, double nu, double Sy, double K
   if (id == 0) {
     c.mat.E = E;
     c.mat.nu = nu;
+    c.mat.Sy = Sy;
+    c.mat.Ka = Ka;
     elastic_C(E, nu, c.mat.C);
-  } else if (id == 1 && (E != c.mat.E || nu != c.mat.nu)) {
+  } else if (id == 1 && (E != c.mat.E || nu != c.mat.nu || Sy != c.mat.Sy || Ka != c.mat.Ka)) {
     set_error("two distinct materials need the MicroPP micro-structure (out of scope); use equal materials");
     return 3;
   }
@@ -573,6 +590,45 @@ int mcx_update_u(void* ctx) {
   return 0;
 }
 
+int mcx_update_vars(void* ctx) {
+  GUARD(ctx);
+  CTX(ctx);
+  if (c.hist_old) std::swap(c.hist_old, c.hist_new);
+  return 0;
+}
+
+int mcx_get_nonlinear_stats(void* ctx, int64_t* n_nonlinear, double* f_trial_max) {
+  GUARD(ctx);
+  CTX(ctx);
+  int64_t n = 0;
+  double fm = 0.;
+  if (c.ftrial) {
+    const Geo& g = c.g;
+    std::vector<double> ft(8 * g.nelem);
+    MCX_HIP(hipMemcpyAsync(ft.data(), c.ftrial, sizeof(double) * ft.size(), hipMemcpyDeviceToHost, c.stream));
+    MCX_HIP(hipStreamSynchronize(c.stream));
+    int lo[3], hi[3], s[3] = {g.xs, g.ys, g.zs}, w[3] = {g.nx, g.ny, g.nz};
+    for (int d = 0; d < 3; d++) {
+      lo[d] = s[d] > 0 ? s[d] - 1 : s[d];
+      hi[d] = s[d] + w[d] - 2;
+    }
+    fm = -1e300;
+    for (int ez = lo[2]; ez <= hi[2]; ez++)
+      for (int ey = lo[1]; ey <= hi[1]; ey++)
+        for (int ex = lo[0]; ex <= hi[0]; ex++) {
+          int64_t le = (ex - g.ex0) + (int64_t)(ey - g.ey0) * g.nex + (int64_t)(ez - g.ez0) * g.nex * g.ney;
+          for (int gp = 0; gp < 8; gp++) {
+            double f = ft[gp * g.nelem + le];
+            if (f > 0.) n++;
+            if (f > fm) fm = f;
+          }
+        }
+  }
+  if (n_nonlinear) *n_nonlinear = n;
+  if (f_trial_max) *f_trial_max = fm;
+  return 0;
+}
+
 int mcx_time_step(void* ctx, int time_s, int* newton_its, double* res, int* ksp_its, double* ksp_rnorm) {
   GUARD(ctx);
   CTX(ctx);
@@ -595,6 +651,7 @@ int mcx_time_step(void* ctx, int time_s, int* newton_its, double* res, int* ksp_
     it++;
   }
   if (newton_its) *newton_its = it;
+  if ((rc = mcx_update_vars(ctx))) return rc;  // src/main.c:83
   MCX_HIP(hipStreamSynchronize(c.stream));
   return 0;
 }

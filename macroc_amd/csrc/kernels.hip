@@ -223,6 +223,84 @@ __global__ void k_homogenize_elastic(int64_t ngp, Material mat, const double* __
   for (int kl = 0; kl < 36; kl++) ctan[kl * ngp + q] = mat.C[kl];
 }
 
+// small-strain J2 plasticity with linear isotropic hardening (MicroPP material type 1: E, nu,
+// Sy, Ka), radial return + consistent tangent; same operation order as orc_j2_point (oracle).
+__global__ void k_homogenize_plastic(int64_t ngp, Material mat, const double* __restrict__ eps,
+                                     const double* __restrict__ hold, double* __restrict__ sig,
+                                     double* __restrict__ ctan, double* __restrict__ hnew,
+                                     double* __restrict__ ftrial) {
+  int64_t q = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (q >= ngp) return;
+  const double E = mat.E, nu = mat.nu, Sy = mat.Sy, Ka = mat.Ka;
+  const double G = E / (2. * (1. + nu));
+  const double K = E / (3. * (1. - 2. * nu));
+  double e[6], h[7];
+#pragma unroll
+  for (int l = 0; l < 6; l++) e[l] = eps[l * ngp + q];
+#pragma unroll
+  for (int l = 0; l < 7; l++) h[l] = hold[l * ngp + q];
+  const double tr = e[0] + e[1] + e[2];
+  double dev[6], st[6];
+#pragma unroll
+  for (int i = 0; i < 3; i++) dev[i] = e[i] - tr / 3.;
+#pragma unroll
+  for (int i = 3; i < 6; i++) dev[i] = e[i] / 2.;
+#pragma unroll
+  for (int i = 0; i < 6; i++) st[i] = 2. * G * (dev[i] - h[i]);
+  double nrm2 = st[0] * st[0] + st[1] * st[1] + st[2] * st[2];
+  nrm2 = nrm2 + 2. * (st[3] * st[3] + st[4] * st[4] + st[5] * st[5]);
+  const double snorm = sqrt(nrm2);
+  const double alpha = h[6];
+  const double f = snorm - sqrt(2. / 3.) * (Sy + Ka * alpha);
+  ftrial[q] = f;
+  double C[36], s[6];
+  const double lam = K - 2. * G / 3.;
+#pragma unroll
+  for (int k2 = 0; k2 < 36; k2++) C[k2] = 0.;
+#pragma unroll
+  for (int a = 0; a < 3; a++)
+#pragma unroll
+    for (int b = 0; b < 3; b++) C[a * 6 + b] = lam + (a == b ? 2. * G : 0.);
+#pragma unroll
+  for (int a = 3; a < 6; a++) C[a * 6 + a] = G;
+  if (f <= 0.) {
+#pragma unroll
+    for (int i = 0; i < 3; i++) s[i] = K * tr + st[i];
+#pragma unroll
+    for (int i = 3; i < 6; i++) s[i] = st[i];
+#pragma unroll
+    for (int i = 0; i < 7; i++) hnew[i * ngp + q] = h[i];
+  } else {
+    const double dg = f / (2. * G + 2. / 3. * Ka);
+    double n[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) n[i] = st[i] / snorm;
+#pragma unroll
+    for (int i = 0; i < 3; i++) s[i] = K * tr + (st[i] - 2. * G * dg * n[i]);
+#pragma unroll
+    for (int i = 3; i < 6; i++) s[i] = st[i] - 2. * G * dg * n[i];
+#pragma unroll
+    for (int i = 0; i < 6; i++) hnew[i * ngp + q] = h[i] + dg * n[i];
+    hnew[6 * ngp + q] = alpha + sqrt(2. / 3.) * dg;
+    const double theta = 1. - 2. * G * dg / snorm;
+    const double thetab = 1. / (1. + Ka / (3. * G)) - (1. - theta);
+#pragma unroll
+    for (int a = 0; a < 3; a++)
+#pragma unroll
+      for (int b = 0; b < 3; b++) C[a * 6 + b] = K + 2. * G * theta * ((a == b ? 1. : 0.) - 1. / 3.);
+#pragma unroll
+    for (int a = 3; a < 6; a++) C[a * 6 + a] = G * theta;
+#pragma unroll
+    for (int a = 0; a < 6; a++)
+#pragma unroll
+      for (int b = 0; b < 6; b++) C[a * 6 + b] = C[a * 6 + b] - 2. * G * thetab * n[a] * n[b];
+  }
+#pragma unroll
+  for (int k2 = 0; k2 < 6; k2++) sig[k2 * ngp + q] = s[k2];
+#pragma unroll
+  for (int kl = 0; kl < 36; kl++) ctan[kl * ngp + q] = C[kl];
+}
+
 // ---------------------------------------------------------------------------- residual
 // assembly_res (src/assembly.c:142-154): be[i] += B[j][i] * sigma[j] * wg, gp outer, j inner
 __global__ void k_element_res(Geo g, const double* __restrict__ sig, double* __restrict__ be) {
@@ -899,7 +977,12 @@ void launch_strains(Ctx& c) {
 
 void launch_homogenize(Ctx& c) {
   int64_t ngp = 8 * c.g.nelem;
-  hipLaunchKernelGGL(k_homogenize_elastic, dim3(nblk(ngp)), dim3(TPB), 0, c.stream, ngp, c.mat, c.eps, c.sig, c.ctan);
+  if (c.mat.law == MCX_LAW_PLASTIC)
+    hipLaunchKernelGGL(k_homogenize_plastic, dim3(nblk(ngp)), dim3(TPB), 0, c.stream, ngp, c.mat, c.eps, c.hist_old,
+                       c.sig, c.ctan, c.hist_new, c.ftrial);
+  else
+    hipLaunchKernelGGL(k_homogenize_elastic, dim3(nblk(ngp)), dim3(TPB), 0, c.stream, ngp, c.mat, c.eps, c.sig,
+                       c.ctan);
 }
 
 void launch_residual(Ctx& c) {

@@ -44,8 +44,8 @@ struct CgState {
 };
 
 struct Material {
-  int kind;
-  double E, nu;
+  int law;                 // MCX_LAW_ELASTIC | MCX_LAW_PLASTIC
+  double E, nu, Sy, Ka;
   double C[36];            // isotropic elastic tangent (Voigt, engineering shear)
 };
 
@@ -109,6 +109,9 @@ struct Ctx {
   double* eps = nullptr;     // [6][8][nelem]
   double* sig = nullptr;     // [6][8][nelem]
   double* ctan = nullptr;    // [36][8][nelem]
+  double* hist_old = nullptr; // plastic law: [7][8][nelem] plastic strain (tensor comps) + alpha
+  double* hist_new = nullptr;
+  double* ftrial = nullptr;  // [8][nelem]
   double* Ke = nullptr;      // [576][nelem] element matrices (assembly scratch)
   double* be = nullptr;      // [24][nelem] element residuals
   double* partials = nullptr;

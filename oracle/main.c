@@ -23,6 +23,7 @@ int main(int argc, char** argv) {
     DBL("-newton_min_tol", newton_min_tol) DBL("-newton_rel_tol", newton_rel_tol)
     DBL("-ksp_rtol", rtol) DBL("-ksp_atol", abstol) DBL("-ksp_divtol", dtol) INT("-ksp_max_it", maxits)
     if (!strcmp(k, "-log")) { log = v; a++; continue; }
+    INT("-mat_law", law)
     fprintf(stderr, "warning: unknown option %s ignored\n", k);
   }
   orc_problem* P = orc_create(&o);

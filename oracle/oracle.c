@@ -45,7 +45,9 @@ struct orc_problem {
   double *val;
   int64_t nnz;
   double *u, *b, *du;
-  double *eps, *sig;
+  double *eps, *sig, *ctan;
+  double *hist_old, *hist_new;  /* [ngp][7]: plastic strain (tensor components) + alpha */
+  double *ftrial;
   double C[36];
   double Btab[NGP][NVOI][NPE * DIM];
   int64_t *dir;
@@ -123,6 +125,9 @@ void orc_default_opts(orc_opts* o) {
   o->maxits = 10000;
   o->E = 1.0e7;
   o->nu = 0.25;
+  o->Sy = 1.0e4;
+  o->Ka = 1.0e7;
+  o->law = 0;
 }
 
 /* ------------------------------------------------------------------------------------
@@ -594,6 +599,10 @@ orc_problem* orc_create(const orc_opts* o) {
   P->dinv = calloc(N, sizeof(double));
   P->eps = calloc(P->ngp * NVOI, sizeof(double));
   P->sig = calloc(P->ngp * NVOI, sizeof(double));
+  P->ctan = calloc(P->ngp * 36, sizeof(double));
+  P->hist_old = calloc(P->ngp * 7, sizeof(double));
+  P->hist_new = calloc(P->ngp * 7, sizeof(double));
+  P->ftrial = calloc(P->ngp, sizeof(double));
   return P;
 }
 
@@ -606,6 +615,7 @@ void orc_destroy(orc_problem* P) {
   free(P->rowptr); free(P->colidx); free(P->val);
   free(P->u); free(P->b); free(P->du); free(P->r); free(P->z); free(P->pp); free(P->w);
   free(P->dinv); free(P->eps); free(P->sig); free(P->dir);
+  free(P->ctan); free(P->hist_old); free(P->hist_new); free(P->ftrial);
   free(P);
 }
 
@@ -669,19 +679,92 @@ void orc_set_strains(orc_problem* P) {
   }
 }
 
-/* MicroPP surrogate (micropp_C_homogenize, src/main.c:62): sigma = C eps */
+/* Gauss-point constitutive law behind micropp_C_homogenize (src/main.c:62).
+   law 0: isotropic elastic, sigma = C eps, ctan = C.
+   law 1: small-strain J2 plasticity with linear isotropic hardening (MicroPP material type 1
+   with parameters E, nu, Sy, Ka; src/init.c:196-201), radial return + consistent tangent.
+   Voigt xx,yy,zz,xy,xz,yz; strains engineering shear; history = plastic strain (tensor
+   components) + accumulated plastic strain alpha.  Shared by the GPU kernel (same order of
+   operations) — MicroPP itself is not available: parity vs MicroPP is unpinned. */
+void orc_j2_point(double E, double nu, double Sy, double Ka, const double* e, const double* hold,
+                  double* s, double* C, double* hnew, double* ftrial) {
+  const double G = E / (2. * (1. + nu));
+  const double K = E / (3. * (1. - 2. * nu));
+  const double tr = e[0] + e[1] + e[2];
+  double dev[6];
+  for (int i = 0; i < 3; i++) dev[i] = e[i] - tr / 3.;
+  for (int i = 3; i < 6; i++) dev[i] = e[i] / 2.;
+  double st[6];
+  for (int i = 0; i < 6; i++) st[i] = 2. * G * (dev[i] - hold[i]);
+  double nrm2 = st[0] * st[0] + st[1] * st[1] + st[2] * st[2];
+  nrm2 = nrm2 + 2. * (st[3] * st[3] + st[4] * st[4] + st[5] * st[5]);
+  const double snorm = sqrt(nrm2);
+  const double alpha = hold[6];
+  const double f = snorm - sqrt(2. / 3.) * (Sy + Ka * alpha);
+  *ftrial = f;
+  const double lam = K - 2. * G / 3.;
+  for (int k = 0; k < 36; k++) C[k] = 0.;
+  for (int a = 0; a < 3; a++)
+    for (int b = 0; b < 3; b++) C[a * 6 + b] = lam + (a == b ? 2. * G : 0.);
+  for (int a = 3; a < 6; a++) C[a * 6 + a] = G;
+  if (f <= 0.) {
+    for (int i = 0; i < 3; i++) s[i] = K * tr + st[i];
+    for (int i = 3; i < 6; i++) s[i] = st[i];
+    for (int i = 0; i < 7; i++) hnew[i] = hold[i];
+    return;
+  }
+  const double dg = f / (2. * G + 2. / 3. * Ka);
+  double n[6];
+  for (int i = 0; i < 6; i++) n[i] = st[i] / snorm;
+  for (int i = 0; i < 3; i++) s[i] = K * tr + (st[i] - 2. * G * dg * n[i]);
+  for (int i = 3; i < 6; i++) s[i] = st[i] - 2. * G * dg * n[i];
+  for (int i = 0; i < 6; i++) hnew[i] = hold[i] + dg * n[i];
+  hnew[6] = alpha + sqrt(2. / 3.) * dg;
+  const double theta = 1. - 2. * G * dg / snorm;
+  const double thetab = 1. / (1. + Ka / (3. * G)) - (1. - theta);
+  for (int a = 0; a < 3; a++)
+    for (int b = 0; b < 3; b++) C[a * 6 + b] = K + 2. * G * theta * ((a == b ? 1. : 0.) - 1. / 3.);
+  for (int a = 3; a < 6; a++) C[a * 6 + a] = G * theta;
+  for (int a = 0; a < 6; a++)
+    for (int b = 0; b < 6; b++) C[a * 6 + b] = C[a * 6 + b] - 2. * G * thetab * n[a] * n[b];
+}
+
 void orc_homogenize(orc_problem* P) {
 #pragma omp parallel for schedule(static)
   for (int64_t g = 0; g < P->ngp; g++) {
     const double* e = P->eps + g * NVOI;
     double* s = P->sig + g * NVOI;
+    if (P->o.law == 1) {
+      orc_j2_point(P->o.E, P->o.nu, P->o.Sy, P->o.Ka, e, P->hist_old + 7 * g, s, P->ctan + 36 * g,
+                   P->hist_new + 7 * g, P->ftrial + g);
+      continue;
+    }
     for (int k = 0; k < NVOI; k++) {
       double acc = 0.;
       for (int l = 0; l < NVOI; l++) acc += P->C[k * NVOI + l] * e[l];
       s[k] = acc;
     }
+    memcpy(P->ctan + 36 * g, P->C, 36 * sizeof(double));
+    P->ftrial[g] = 0.;
   }
 }
+
+void orc_update_vars(orc_problem* P) {
+  memcpy(P->hist_old, P->hist_new, P->ngp * 7 * sizeof(double));
+}
+
+int64_t orc_nonlinear_gps(const orc_problem* P, double* fmax) {
+  int64_t n = 0;
+  double m = -1e300;
+  for (int64_t g = 0; g < P->ngp; g++) {
+    if (P->ftrial[g] > 0.) n++;
+    if (P->ftrial[g] > m) m = P->ftrial[g];
+  }
+  if (fmax) *fmax = m;
+  return n;
+}
+
+double* orc_ctan(orc_problem* P) { return P->ctan; }
 
 /* assembly_res src/assembly.c:120-176 with DMLocalToGlobal(ADD) emulated as
    owned part first, then remote ghost contributions by source rank */
@@ -792,7 +875,7 @@ void orc_assembly_jac(orc_problem* P) {
     for (int64_t ie = 0; ie < ne; ++ie) {
       memset(Ae, 0, sizeof(Ae));
       for (int gp = 0; gp < NGP; ++gp) {
-        const double* ctan = P->C; /* micropp_C_get_ctan3 (uniform elastic surrogate) */
+        const double* ctan = P->ctan + 36 * (P->gp_off[r] + ie * NGP + gp); /* micropp_C_get_ctan3 */
         double(*B)[NPE * DIM] = P->Btab[gp];
         for (int i = 0; i < NPE * DIM; ++i)
           for (int j = 0; j < NPE * DIM; ++j)
@@ -984,6 +1067,7 @@ int orc_run(orc_problem* P, const char* log_path, double* t_newton_solve_s) {
       if (t_first < 0) t_first = now_s() - t0;
       newton_it++;
     }
+    orc_update_vars(P);
   }
   if (f) fclose(f);
   if (t_newton_solve_s) *t_newton_solve_s = t_first;

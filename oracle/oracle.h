@@ -70,6 +70,8 @@ typedef struct {
   double rtol, abstol, dtol; /* -ksp_rtol ... (src/init.c:147-156) */
   int maxits;              /* -ksp_max_it */
   double E, nu;            /* material (src/init.c:31-32) */
+  double Sy, Ka;           /* yield stress, hardening modulus (micro_mat_1[2..3]) */
+  int law;                 /* 0 = isotropic elastic, 1 = J2 plasticity (MicroPP material type 1) */
 } orc_opts;
 
 typedef struct orc_problem orc_problem;
@@ -128,6 +130,11 @@ void orc_spmv(const orc_problem* P, const double* x, double* y);
 /* KSPSolve(CG, Jacobi) of A du = b; hist (len maxits+1, may be NULL) = residual history */
 int orc_solve(orc_problem* P, int* its, double* rnorm, int* reason, double* hist);
 void orc_update_u(orc_problem* P);
+/* micropp_C_update_vars (src/main.c:83): commit the Gauss-point history */
+void orc_update_vars(orc_problem* P);
+/* non-linear Gauss points of the last homogenize and max f_trial (src/util.c:69-102) */
+int64_t orc_nonlinear_gps(const orc_problem* P, double* f_trial_max);
+double* orc_ctan(orc_problem* P);  /* [ngp][36] */
 
 /* full run of src/main.c:49-109; writes log lines to `log` (may be NULL).
    newton_out: per (time step, newton it) records: |RES|, ksp its, ksp rnorm (cap entries) */

@@ -25,7 +25,7 @@ class Opts(C.Structure):
         ("ts", C.c_int), ("bc_type", C.c_int), ("rad", C.c_double),
         ("newton_max_its", C.c_int), ("newton_min_tol", C.c_double), ("newton_rel_tol", C.c_double),
         ("rtol", C.c_double), ("abstol", C.c_double), ("dtol", C.c_double), ("maxits", C.c_int),
-        ("E", C.c_double), ("nu", C.c_double),
+        ("E", C.c_double), ("nu", C.c_double), ("Sy", C.c_double), ("Ka", C.c_double), ("law", C.c_int),
     ]
 
 
@@ -72,7 +72,7 @@ def lib():
         L.orc_get_displacement.restype = C.c_double
         L.orc_apply_bc_u.argtypes = [P, C.c_double]
         for fn in ("orc_set_strains", "orc_homogenize", "orc_assembly_res", "orc_assembly_jac", "orc_update_u",
-                   "orc_sbaij_mirror"):
+                   "orc_sbaij_mirror", "orc_update_vars"):
             getattr(L, fn).argtypes = [P]
         L.orc_norm2.argtypes = [P, d]
         L.orc_norm2.restype = C.c_double
@@ -81,6 +81,10 @@ def lib():
         L.orc_dmda_decide.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int,
                                       C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.orc_run.argtypes = [P, C.c_char_p, d]
+        L.orc_nonlinear_gps.argtypes = [P, d]
+        L.orc_nonlinear_gps.restype = C.c_int64
+        L.orc_ctan.argtypes = [P]
+        L.orc_ctan.restype = d
         L.orc_set_threads.argtypes = [C.c_int]
         L.orc_set_threads.restype = C.c_int
         L.orc_petsc_numbering.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int,
@@ -247,6 +251,17 @@ class Problem:
 
     def assembly_jac(self):
         lib().orc_assembly_jac(self._p)
+
+    def update_vars(self):
+        lib().orc_update_vars(self._p)
+
+    def nonlinear_gps(self):
+        fm = np.zeros(1)
+        n = lib().orc_nonlinear_gps(self._p, _dp(fm))
+        return n, float(fm[0])
+
+    def ctan(self):
+        return self._vec("orc_ctan", self.ngp * 36).reshape(self.ngp, 36)
 
     def sbaij_mirror(self):
         """-dm_mat_type sbaij semantics: lower triangle := transpose of the upper triangle."""
