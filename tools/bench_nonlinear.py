@@ -1,0 +1,43 @@
+"""BASELINE config 5 path: 128^3 grid, non-linear Newton with the J2-plastic Gauss-point law behind
+the callback (MicroPP material type 1 parameters E, nu, Sy, Ka from -micro_mat_1), time steps
+1..T of src/main.c:49-109 (apply BC, Newton to newton_rel_tol, update_vars).  Prints one JSON
+line: Newton iterations, CG iterations, wall time per Newton iteration (solve-bearing), DOF/s.
+MicroPP's FE2 micro solve (-micro_n 10) is not available; the callback runs the material-point
+law, which is MicroPP's homogenised response for identical phase materials."""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import macroc_amd as M  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--grid", type=int, default=128)
+ap.add_argument("--ts", type=int, default=3, help="time steps (step 0 has zero load)")
+ap.add_argument("--mat-type", default="aij")
+ap.add_argument("--rtol", type=float, default=1e-8)
+ap.add_argument("--dt", type=float, default=0.01, help="load step (U = -ts*dt); 0.01 drives the circle plastic")
+a = ap.parse_args()
+N = a.grid
+m = M.Macroc(["-da_grid_x", N, "-da_grid_y", N, "-da_grid_z", N, "-mat_law", "plastic", "-ksp_rtol", repr(a.rtol),
+              "-dm_mat_type", a.mat_type, "-ts", a.ts, "-dt", a.dt])
+m.set_timing(True)
+steps = []
+t_all = time.perf_counter()
+for ts in range(a.ts):
+    t0 = time.perf_counter()
+    out = m.time_step(ts)
+    dt = time.perf_counter() - t0
+    nl, fmax = m.nonlinear_stats()
+    steps.append(dict(ts=ts, newton_its=out["newton_its"], ksp_its=out["ksp_its"], res=out["res"], seconds=dt,
+                      nonlinear_gps=nl, f_trial_max=fmax))
+    print(json.dumps(steps[-1]), file=sys.stderr, flush=True)
+tot = time.perf_counter() - t_all
+nits = sum(s["newton_its"] for s in steps)
+print(json.dumps({"workload": f"config 5 path: {N}^3 non-linear Newton (J2 callback), {a.ts} time steps, dt {a.dt}",
+                  "mat_type": a.mat_type, "newton_its": nits, "cg_its": sum(sum(s["ksp_its"]) for s in steps),
+                  "seconds": tot, "ms_per_newton_iter": tot / max(nits, 1) * 1e3,
+                  "dof_per_s": 3 * N ** 3 * nits / tot, "steps": steps}))
+m.finish()
