@@ -38,6 +38,20 @@ def rank_grid(n):
     return {1: (1, 1, 1), 2: (2, 1, 1), 4: (2, 2, 1), 8: (2, 2, 2), 16: (4, 2, 2)}.get(n) or (n, 1, 1)
 
 
+def pmc_traffic(mat_type, NX, NY, NZ):
+    """HBM bytes per SpMV launch from the committed rocprofv3 PMC passes (profiles/pmc_spmv.json:
+    (FETCH_SIZE*2 [gfx950 wide-read correction] + WRITE_SIZE) * 1024 per launch, same kernel and
+    grid), or None when no matching measurement exists."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_spmv.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(f"{mat_type}:{NX}x{NY}x{NZ}")
+        return e["hbm_bytes_per_launch"] if e else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def cpu_baseline(N, threads, gpu_its, rtol, ndofs_target, nelem_target, nnz_target, cg_cap=200):
     """The oracle — the C restatement of the reference path, its MPI ranks run as OpenMP threads
     (one emulated rank per thread, PETSc stash / per-rank dot semantics) — on an N^3 sample of
@@ -83,42 +97,14 @@ def cpu_baseline(N, threads, gpu_its, rtol, ndofs_target, nelem_target, nnz_targ
     }
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=2)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--grid", type=int, default=256, help="nodes per direction per GPU")
-    ap.add_argument("--rtol", type=float, default=1e-8)
-    ap.add_argument("--cpu-sample", type=int, default=96, help="oracle sample grid (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16)
-    ap.add_argument("--no-check", action="store_true")
-    ap.add_argument("--same-device", action="store_true", help="testing only: every rank on device 0")
-    ap.add_argument("--mat-type", default="aij", choices=["aij", "sbaij"], help="-dm_mat_type")
-    args = ap.parse_args()
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    px, py, pz = rank_grid(world)
-    G = args.grid
-    NX, NY, NZ = G * px, G * py, G * pz
-    argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
-            "-da_processors_z", pz, "-ts", 2, "-ksp_rtol", repr(args.rtol),
-            "-device", 0 if args.same_device else local, "-dm_mat_type", args.mat_type]
-    comm_id = None
-    if world > 1:
-        obj = [M.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        comm_id = obj[0]
+def measure(argv, rank, world, comm_id, args):
+    """Setup + warmup + timed steps of one configuration; returns the timings of this rank."""
     t_setup = time.perf_counter()
     m = M.Macroc(argv, rank=rank, nranks=world, comm_id=comm_id)
     m.set_timing(True)
     info = m.info
-    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s, device GB {info['device_bytes'] / 1e9:.1f}, "
-        f"local {info['nx']}x{info['ny']}x{info['nz']}")
+    log(f"[rank {rank}] {argv[-1]}: setup {time.perf_counter() - t_setup:.1f}s, device GB "
+        f"{info['device_bytes'] / 1e9:.1f}, local {info['nx']}x{info['ny']}x{info['nz']}")
     U = m.get_displacement(1)
 
     def step():
@@ -157,8 +143,6 @@ def main():
     tm = m.timing()
     spmv_avg_ms = tm["spmv_ms_total"] / max(tm["spmv_launches"], 1)
     spmv_bytes = tm["spmv_bytes_per_launch"]
-    achieved = spmv_bytes / (spmv_avg_ms * 1e-3) / 1e9
-
     check = None
     if not args.no_check:
         # size-independent property: true residual of the solve, |A du - b| / |b| (collective)
@@ -170,9 +154,62 @@ def main():
             dist.all_reduce(tt)
             loc = tt.numpy()
         check = {"true_rel_residual": float(np.sqrt(loc[0] / loc[1])), "ksp_reason": int(reason)}
+    m.finish()
+    return {"its": its, "tm": tm, "info": info, "check": check, "spmv_avg_ms": spmv_avg_ms, "spmv_bytes": spmv_bytes,
+            "achieved": spmv_bytes / (spmv_avg_ms * 1e-3) / 1e9, "ms_step": dt / args.steps * 1e3}
 
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--grid", type=int, default=256, help="nodes per direction per GPU")
+    ap.add_argument("--rtol", type=float, default=1e-8)
+    ap.add_argument("--cpu-sample", type=int, default=96, help="oracle sample grid (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16)
+    ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--same-device", action="store_true", help="testing only: every rank on device 0")
+    ap.add_argument("--mat-type", default="aij", choices=["aij", "sbaij"], help="-dm_mat_type of the headline")
+    ap.add_argument("--variants", default="sbaij", help="other -dm_mat_type runs reported beside it ('' = none)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    px, py, pz = rank_grid(world)
+    G = args.grid
+    NX, NY, NZ = G * px, G * py, G * pz
+    argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
+            "-da_processors_z", pz, "-ts", 2, "-ksp_rtol", repr(args.rtol),
+            "-device", 0 if args.same_device else local]
+    comm_id = None
+    if world > 1:
+        obj = [M.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm_id = obj[0]
+    def run(mat_type):
+        return measure(argv + ["-dm_mat_type", mat_type], rank, world, comm_id, args)
+
+    r = run(args.mat_type)
+    variants = {}
+    if args.variants:
+        for v in args.variants.split(","):
+            if v and v != args.mat_type:
+                if world > 1:
+                    obj = [M.comm_unique_id() if rank == 0 else None]
+                    dist.broadcast_object_list(obj, src=0)
+                    comm_id = obj[0]
+                vr = run(v)
+                variants[v] = {"value": 3 * NX * NY * NZ / (vr["ms_step"] * 1e-3), "ms_per_step": vr["ms_step"],
+                               "cg_its": vr["its"], "ms_per_cg_iter": vr["tm"]["solve_ms"] / max(vr["its"], 1),
+                               "spmv_avg_ms": vr["spmv_avg_ms"], "spmv_bytes_per_launch": vr["spmv_bytes"],
+                               "spmv_achieved_GBs": vr["achieved"], "check": vr["check"]}
+    its, tm, info, check = r["its"], r["tm"], r["info"], r["check"]
+    spmv_avg_ms, spmv_bytes, achieved, ms_step = r["spmv_avg_ms"], r["spmv_bytes"], r["achieved"], r["ms_step"]
     ndofs = 3 * NX * NY * NZ
-    ms_step = dt / args.steps * 1e3
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_sample > 0:
@@ -202,14 +239,14 @@ def main():
             "phases_ms": {k: tm[k] for k in ("strains_ms", "homogenize_ms", "residual_ms", "jacobian_ms",
                                              "solve_ms", "update_ms")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS, "traffic": None,
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": pmc_traffic(args.mat_type, NX, NY, NZ),
                          "kernel": "k_spmv (stencil-block SpMV inside CG)", "bytes_per_launch": spmv_bytes,
                          "avg_launch_ms": spmv_avg_ms, "launches_timed": tm["spmv_launches"]},
             "cpu_baseline": cpu,
             "check": check,
+            "variants": variants,
         }
         print(json.dumps(line), flush=True)
-    m.finish()
     if world > 1:
         dist.destroy_process_group()
 

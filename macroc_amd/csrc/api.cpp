@@ -871,6 +871,18 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     }
     return 0;
   }
+  if (!std::strcmp(name, "spmv_nt")) {
+    c.spmv_nt = (int)value;
+    return 0;
+  }
+  if (!std::strcmp(name, "spmv_kernel")) {
+    c.spmv_kernel = (int)value;
+    if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
+      set_error("spmv_kernel: partials buffer too small");
+      return 2;
+    }
+    return 0;
+  }
   set_error(std::string("unknown option ") + name);
   return 2;
 }

@@ -587,23 +587,35 @@ __device__ __forceinline__ void slot_acc(double v, const double (&xv)[27][3], do
   else y2 += v * xv[nb][c];
 }
 
-template <int Q>
+template <bool NT>
+__device__ __forceinline__ double2 ldv(const double2* p) {
+  if constexpr (NT) {
+    double2 r;
+    r.x = __builtin_nontemporal_load(&p->x);
+    r.y = __builtin_nontemporal_load(&p->y);
+    return r;
+  } else {
+    return *p;
+  }
+}
+
+template <int Q, bool NT = false>
 struct PairLoop {
   static __device__ __forceinline__ void run(const double2* __restrict__ v, const double (&xv)[27][3], double& y0,
                                              double& y1, double& y2) {
-    PairLoop<Q - 1>::run(v, xv, y0, y1, y2);
-    const double2 a = v[(Q - 1) * 64];
+    PairLoop<Q - 1, NT>::run(v, xv, y0, y1, y2);
+    const double2 a = ldv<NT>(v + (Q - 1) * 64);
     slot_acc<2 * (Q - 1)>(a.x, xv, y0, y1, y2);
     if constexpr (2 * (Q - 1) + 1 < NSLOT) slot_acc<2 * (Q - 1) + 1>(a.y, xv, y0, y1, y2);
   }
 };
-template <>
-struct PairLoop<0> {
+template <bool NT>
+struct PairLoop<0, NT> {
   static __device__ __forceinline__ void run(const double2* __restrict__, const double (&)[27][3], double&, double&,
                                              double&) {}
 };
 
-template <bool DOT, bool GATED>
+template <bool DOT, bool GATED, bool NT = false>
 __global__ __launch_bounds__(TPB) void k_spmv(Geo g, const double2* __restrict__ V, const double* __restrict__ x,
                                               double* __restrict__ y, double* __restrict__ part,
                                               const CgState* __restrict__ cg, SpmvTiling tl) {
@@ -626,7 +638,7 @@ __global__ __launch_bounds__(TPB) void k_spmv(Geo g, const double2* __restrict__
     }
     const double2* v = V + (int64_t)(n >> 6) * (NPAIR * 64) + (n & 63);
     double y0 = 0., y1 = 0., y2 = 0.;
-    PairLoop<NPAIR>::run(v, xv, y0, y1, y2);
+    PairLoop<NPAIR, NT>::run(v, xv, y0, y1, y2);
     y[3 * n + 0] = y0;
     y[3 * n + 1] = y1;
     y[3 * n + 2] = y2;
@@ -701,6 +713,213 @@ __global__ __launch_bounds__(TPB) void k_spmv_sym(Geo g, const double* __restric
   }
   if (DOT) {
     double s = block_sum<TPB>(dot, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+  }
+}
+
+
+// ---------------------------------------------------------------------------- sbaij SpMV, z-marching
+// A block owns a TX x TY (64 x 4) tile of (x,y) columns and marches up a z-chunk.  Each node's
+// upper blocks are read once: the node's own rows use them directly, and the transposed
+// products c = U(m,nb')^T x_m go to the targets inside the tile through LDS slots (9 slots
+// for the next plane, 4 for the current one); targets at the tile edge or at the first plane
+// of the chunk pull the few source blocks they need from HBM/L2 instead.  Every row is the sum
+// of its 27 block products (each a 3-term partial sum) in ascending nb order, however the
+// products were routed, so the result is independent of tiling and rank grid.
+constexpr int ZTX = 64, ZTY = 4;
+
+struct ZTiling {
+  int ntx, nty, nzc, kc;  // tiles in x, y; z chunks and planes per chunk
+};
+
+static ZTiling z_tiling(const Geo& g) {
+  ZTiling t;
+  t.ntx = (g.nx + ZTX - 1) / ZTX;
+  t.nty = (g.ny + ZTY - 1) / ZTY;
+  const int tiles = t.ntx * t.nty;
+  const int want = 1024;  // ~2 resident blocks per CU (80 KB LDS each) x 256 CUs x 2 rounds
+  t.nzc = std::max(1, std::min(g.nz, (want + tiles - 1) / tiles));
+  t.kc = (g.nz + t.nzc - 1) / t.nzc;
+  t.nzc = (g.nz + t.kc - 1) / t.kc;
+  return t;
+}
+
+__device__ __forceinline__ double uval(const double* __restrict__ U, int p, int s) {
+  return U[(int64_t)(p >> 6) * (UPAIR * 128) + 2 * (p & 63) + (s >> 1) * 128 + (s & 1)];
+}
+
+// c = U(p, nb')^T x_p for upper block nb' (14..26) of padded node p
+__device__ __forceinline__ void ut_x(const double* __restrict__ U, const double* __restrict__ x, int p, int nbp,
+                                     double& c0, double& c1, double& c2) {
+  const int base = 6 + 9 * (nbp - 14);
+  const double x0 = x[3 * (int64_t)p], x1 = x[3 * (int64_t)p + 1], x2 = x[3 * (int64_t)p + 2];
+  c0 = uval(U, p, base + 0) * x0;
+  c0 += uval(U, p, base + 3) * x1;
+  c0 += uval(U, p, base + 6) * x2;
+  c1 = uval(U, p, base + 1) * x0;
+  c1 += uval(U, p, base + 4) * x1;
+  c1 += uval(U, p, base + 7) * x2;
+  c2 = uval(U, p, base + 2) * x0;
+  c2 += uval(U, p, base + 5) * x1;
+  c2 += uval(U, p, base + 8) * x2;
+}
+
+template <bool DOT, bool GATED>
+__global__ __launch_bounds__(256) void k_spmv_symz(Geo g, const double* __restrict__ U, const double* __restrict__ x,
+                                                   double* __restrict__ y, double* __restrict__ part,
+                                                   const CgState* __restrict__ cg, ZTiling zt) {
+  __shared__ double accN[9][3][ZTY * ZTX];  // next-plane contributions, by the target's lower nb (0..8)
+  __shared__ double accC[4][3][ZTY * ZTX];  // current-plane contributions, lower nb 9..12
+  __shared__ double sh[4];
+  if (GATED && cg->reason) return;
+  // block -> (tile x, tile y, z chunk); tiles of one XCD form a y-slab (blocks b, b+8 share an XCD)
+  const int b = blockIdx.x;
+  const int xcd = b & 7, t8 = b >> 3;
+  const int slab = (zt.nty + 7) >> 3;
+  const int ty0 = xcd * slab;
+  const int nty_here = min(slab, zt.nty - ty0);
+  const int per = max(nty_here, 0) * zt.ntx * zt.nzc;
+  double dot = 0.;
+  const bool blk_ok = t8 < per;
+  int tyi = 0, txi = 0, zc = 0;
+  if (blk_ok) {
+    zc = t8 % zt.nzc;
+    const int r = t8 / zt.nzc;
+    txi = r % zt.ntx;
+    tyi = ty0 + r / zt.ntx;
+  }
+  const int lx = threadIdx.x % ZTX, ly = threadIdx.x / ZTX, me = threadIdx.x;
+  const int i = txi * ZTX + lx, j = tyi * ZTY + ly;
+  const bool active = blk_ok && i < g.nx && j < g.ny;
+  const int k0 = zc * zt.kc, k1 = min(g.nz, k0 + zt.kc);
+  const int PX = g.PX, PXY = g.PX * g.PY;
+  // a source at tile-relative (lx+dx, ly+dy) is pushed by a thread of this block iff active
+  auto in_tile = [&](int dx, int dy) {
+    const int sx = lx + dx, sy = ly + dy;
+    if (sx < 0 || sx >= ZTX || sy < 0 || sy >= ZTY) return false;
+    const int si = i + dx, sj = j + dy;
+    return si < g.nx && sj < g.ny;
+  };
+  for (int k = k0; blk_ok && k < k1; k++) {
+    const int pc = (i + 1) + (j + 1) * PX + (k + 1) * PXY;
+    double y0 = 0., y1 = 0., y2 = 0.;
+    // 1. lower blocks nb 0..8 (dz = -1), ascending nb
+    if (active) {
+#pragma unroll
+      for (int nb = 0; nb < 9; nb++) {
+        const int dx = nb % 3 - 1, dy = nb / 3 - 1;
+        double c0, c1, c2;
+        if (k > k0 && in_tile(dx, dy)) {
+          c0 = accN[nb][0][me];
+          c1 = accN[nb][1][me];
+          c2 = accN[nb][2][me];
+        } else {
+          ut_x(U, x, pc + dx + dy * PX - PXY, 26 - nb, c0, c1, c2);
+        }
+        y0 += c0;
+        y1 += c1;
+        y2 += c2;
+      }
+    }
+    __syncthreads();
+    // 2. push: this node's transposed upper products to in-tile targets
+    if (active) {
+      const double x0 = x[3 * (int64_t)pc], x1 = x[3 * (int64_t)pc + 1], x2 = x[3 * (int64_t)pc + 2];
+#pragma unroll
+      for (int nbp = 14; nbp < 27; nbp++) {
+        const int dx = nbp % 3 - 1, dy = (nbp / 3) % 3 - 1, dz = nbp / 9 - 1;
+        // target = this node + (dx,dy,dz); its lower nb = 26 - nbp; target is in-tile iff this
+        // node is in-tile seen from the target, i.e. in_tile at (lx+dx, ly+dy) for the target
+        const int tx = lx + dx, ty = ly + dy;
+        if (tx < 0 || tx >= ZTX || ty < 0 || ty >= ZTY) continue;
+        if (i + dx >= g.nx || j + dy >= g.ny) continue;
+        if (dz == 1 && k + 1 >= k1) continue;
+        const int base = 6 + 9 * (nbp - 14);
+        double c0 = uval(U, pc, base + 0) * x0;
+        c0 += uval(U, pc, base + 3) * x1;
+        c0 += uval(U, pc, base + 6) * x2;
+        double c1 = uval(U, pc, base + 1) * x0;
+        c1 += uval(U, pc, base + 4) * x1;
+        c1 += uval(U, pc, base + 7) * x2;
+        double c2 = uval(U, pc, base + 2) * x0;
+        c2 += uval(U, pc, base + 5) * x1;
+        c2 += uval(U, pc, base + 8) * x2;
+        const int tgt = ty * ZTX + tx;
+        if (dz == 1) {
+          accN[26 - nbp][0][tgt] = c0;
+          accN[26 - nbp][1][tgt] = c1;
+          accN[26 - nbp][2][tgt] = c2;
+        } else {
+          accC[26 - nbp - 9][0][tgt] = c0;
+          accC[26 - nbp - 9][1][tgt] = c1;
+          accC[26 - nbp - 9][2][tgt] = c2;
+        }
+      }
+    }
+    __syncthreads();
+    if (active) {
+      // 3. lower blocks nb 9..12 (dz = 0)
+#pragma unroll
+      for (int nb = 9; nb < 13; nb++) {
+        const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1;
+        double c0, c1, c2;
+        if (in_tile(dx, dy)) {
+          c0 = accC[nb - 9][0][me];
+          c1 = accC[nb - 9][1][me];
+          c2 = accC[nb - 9][2][me];
+        } else {
+          ut_x(U, x, pc + dx + dy * PX, 26 - nb, c0, c1, c2);
+        }
+        y0 += c0;
+        y1 += c1;
+        y2 += c2;
+      }
+      // 4. diagonal block (upper triangle mirrored) and upper blocks 14..26
+      const double x0 = x[3 * (int64_t)pc], x1 = x[3 * (int64_t)pc + 1], x2 = x[3 * (int64_t)pc + 2];
+      {
+        const double d00 = uval(U, pc, 0), d01 = uval(U, pc, 1), d02 = uval(U, pc, 2), d11 = uval(U, pc, 3),
+                     d12 = uval(U, pc, 4), d22 = uval(U, pc, 5);
+        double c0 = d00 * x0;
+        c0 += d01 * x1;
+        c0 += d02 * x2;
+        double c1 = d01 * x0;
+        c1 += d11 * x1;
+        c1 += d12 * x2;
+        double c2 = d02 * x0;
+        c2 += d12 * x1;
+        c2 += d22 * x2;
+        y0 += c0;
+        y1 += c1;
+        y2 += c2;
+      }
+#pragma unroll
+      for (int nb = 14; nb < 27; nb++) {
+        const int off = (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
+        const int q = pc + off;
+        const double z0 = x[3 * (int64_t)q], z1 = x[3 * (int64_t)q + 1], z2 = x[3 * (int64_t)q + 2];
+        const int base = 6 + 9 * (nb - 14);
+        double c0 = uval(U, pc, base + 0) * z0;
+        c0 += uval(U, pc, base + 1) * z1;
+        c0 += uval(U, pc, base + 2) * z2;
+        double c1 = uval(U, pc, base + 3) * z0;
+        c1 += uval(U, pc, base + 4) * z1;
+        c1 += uval(U, pc, base + 5) * z2;
+        double c2 = uval(U, pc, base + 6) * z0;
+        c2 += uval(U, pc, base + 7) * z1;
+        c2 += uval(U, pc, base + 8) * z2;
+        y0 += c0;
+        y1 += c1;
+        y2 += c2;
+      }
+      const int n = i + j * g.nx + k * g.nx * g.ny;
+      y[3 * (int64_t)n + 0] = y0;
+      y[3 * (int64_t)n + 1] = y1;
+      y[3 * (int64_t)n + 2] = y2;
+      if (DOT) dot += x0 * y0 + x1 * y1 + x2 * y2;
+    }
+  }
+  if (DOT) {
+    double s = block_sum<256>(dot, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = s;
   }
 }
@@ -958,7 +1177,13 @@ static inline unsigned nblk(int64_t n) { return (unsigned)((n + TPB - 1) / TPB);
 int dirichlet_mask_host(const Geo& g, int gi, int gj, int gk) { return dirichlet_mask(g, gi, gj, gk); }
 
 int64_t node_blocks(const Ctx& c) { return nblk(c.g.nown); }
-int64_t spmv_grid_blocks(const Ctx& c) { return 8 * (int64_t)spmv_tiling(c.g, c.spmv_subl).per_xcd; }
+int64_t spmv_grid_blocks(const Ctx& c) {
+  if (c.U && c.spmv_kernel == 1) {
+    const ZTiling zt = z_tiling(c.g);
+    return 8 * (int64_t)(((zt.nty + 7) / 8) * zt.ntx * zt.nzc);
+  }
+  return 8 * (int64_t)spmv_tiling(c.g, c.spmv_subl).per_xcd;
+}
 
 int upload_constants(Ctx& c) {
   double B[8][6][24];
@@ -1015,6 +1240,19 @@ void launch_jacobi(Ctx& c) {
 void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
   const int nb = (int)spmv_grid_blocks(c);
   const SpmvTiling tl = spmv_tiling(c.g, c.spmv_subl);
+  if (c.U && c.spmv_kernel == 1) {
+    const ZTiling zt = z_tiling(c.g);
+    if (dot && gated)
+      hipLaunchKernelGGL((k_spmv_symz<true, true>), dim3(nb), dim3(256), 0, c.stream, c.g, c.U, xpad, y, c.partials,
+                         c.cg, zt);
+    else if (dot)
+      hipLaunchKernelGGL((k_spmv_symz<true, false>), dim3(nb), dim3(256), 0, c.stream, c.g, c.U, xpad, y, c.partials,
+                         c.cg, zt);
+    else
+      hipLaunchKernelGGL((k_spmv_symz<false, false>), dim3(nb), dim3(256), 0, c.stream, c.g, c.U, xpad, y, c.partials,
+                         c.cg, zt);
+    return;
+  }
   if (c.U) {
     if (dot && gated)
       hipLaunchKernelGGL((k_spmv_sym<true, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, c.U, xpad, y, c.partials,
@@ -1028,6 +1266,15 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
     return;
   }
   const double2* V = reinterpret_cast<const double2*>(c.V);
+  if (c.spmv_nt) {
+    if (dot && gated)
+      hipLaunchKernelGGL((k_spmv<true, true, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials, c.cg,
+                         tl);
+    else
+      hipLaunchKernelGGL((k_spmv<true, false, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials,
+                         c.cg, tl);
+    return;
+  }
   if (dot && gated)
     hipLaunchKernelGGL((k_spmv<true, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials, c.cg, tl);
   else if (dot)

@@ -104,8 +104,10 @@ struct Ctx {
   double* U = nullptr;       // sbaij upper stencil blocks over the padded box [npgroups][UPAIR][64] double2
   int64_t npgroups = 0;
   int64_t nupper_local = 0;  // sbaij: stored upper values of the owned rows
-  int spmv_subl = 0;
-  int64_t partials_cap = 0;         // SpMV sweep: lines per sub-slab of an XCD's slab (0 = whole slab)
+  int spmv_subl = 0;         // SpMV sweep: lines per sub-slab of an XCD's slab (0 = whole slab)
+  int spmv_kernel = 0;       // sbaij: 0 = pull, 1 = z-marching push/pull tiles (experimental)
+  int spmv_nt = 1;           // aij: non-temporal matrix loads (streamed once; +1.4% measured)
+  int64_t partials_cap = 0;
   double* eps = nullptr;     // [6][8][nelem]
   double* sig = nullptr;     // [6][8][nelem]
   double* ctan = nullptr;    // [36][8][nelem]

@@ -11,7 +11,9 @@ import macroc_amd as M  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--grid", type=int, default=256)
 ap.add_argument("--mat", default="aij")
-ap.add_argument("--subl", default="0,8")
+ap.add_argument("--subl", default="0")
+ap.add_argument("--kernels", default="0", help="sbaij kernels to compare: 0 pull, 1 z-marching")
+ap.add_argument("--nt", default="0", help="aij non-temporal matrix loads: 0,1")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--iters", type=int, default=20)
 a = ap.parse_args()
@@ -22,15 +24,29 @@ m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
 m.spmv(m.b())  # p := b (padded), a realistic operand
 t = m.timing()
 nbytes = None
-variants = [int(v) for v in a.subl.split(",")]
+import numpy as np  # noqa: E402
+
+variants = [(int(s), int(kk), int(nt)) for s in a.subl.split(",") for kk in a.kernels.split(",")
+            for nt in a.nt.split(",")]
 res = {v: [] for v in variants}
+x = np.random.default_rng(1).uniform(-1, 1, m.n)
+ys = {}
+for v in variants:
+    m.set_option("spmv_subl", v[0])
+    m.set_option("spmv_kernel", v[1])
+    m.set_option("spmv_nt", v[2])
+    ys[v] = m.spmv(x)
+y0 = ys[variants[0]]
 for r in range(a.rounds):
     for v in variants:
-        m.set_option("spmv_subl", v)
+        m.set_option("spmv_subl", v[0])
+        m.set_option("spmv_kernel", v[1])
+        m.set_option("spmv_nt", v[2])
         res[v].append(m.time_spmv(a.iters))
 tb = m.timing()["spmv_bytes_per_launch"]
 for v in variants:
     med = statistics.median(res[v])
-    print(f"{a.mat} grid {N}^3 subl={v:3d}: median {med:.4f} ms  min {min(res[v]):.4f}  -> {tb / med / 1e6:.0f} GB/s "
-          f"(algorithmic {tb / 1e9:.2f} GB)")
+    rel = np.linalg.norm(ys[v] - y0) / np.linalg.norm(y0)
+    print(f"{a.mat} grid {N}^3 subl={v[0]:3d} kernel={v[1]} nt={v[2]}: median {med:.4f} ms  min {min(res[v]):.4f}  -> "
+          f"{tb / med / 1e6:.0f} GB/s (algorithmic {tb / 1e9:.2f} GB)  |y-y0|/|y0|={rel:.2e}")
 m.finish()
