@@ -70,6 +70,18 @@ static int free_ctx(Ctx* c) {
   return 0;
 }
 
+// largest SpMV grid over the selectable kernels (mcx_set_option may switch between them)
+static int64_t max_spmv_blocks(Ctx& c) {
+  const int keep = c.spmv_kernel;
+  int64_t m = 0;
+  for (int k = 0; k <= 6; k++) {
+    c.spmv_kernel = k;
+    m = std::max(m, spmv_grid_blocks(c));
+  }
+  c.spmv_kernel = keep;
+  return m;
+}
+
 static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void* comm_id, LocalGroup* lg) {
   c.o = *o;
   c.lg = lg;
@@ -85,6 +97,14 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   MCX_HIP(hipSetDevice(c.device));
   int rc = setup_decomposition(c);
   if (rc) return rc;
+  int ncu = 0;
+  MCX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c.device));
+  if (o->mat_type == MCX_MAT_SBAIJ) {
+    // z-marching tiles: 128x2 where the subdomain is wide enough, one resident round of
+    // blocks (two 80 KB-LDS blocks per CU) — tools/spmv_ab.py sweep, DESIGN.md §6
+    c.spmv_kernel = c.g.nx >= 128 ? 4 : 1;
+    c.spmv_zblocks = 2 * std::max(ncu, 1);
+  }
   MCX_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
   MCX_HIP(hipEventCreate(&c.ev_a));
   MCX_HIP(hipEventCreate(&c.ev_b));
@@ -102,7 +122,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
       (rc = dalloc(c, &c.eps, 6 * 8 * E)) ||
       (rc = dalloc(c, &c.sig, 6 * 8 * E)) || (rc = dalloc(c, &c.ctan, 36 * 8 * E)) ||
       (rc = dalloc(c, &c.Ke, (int64_t)NKE * E)) || (rc = dalloc(c, &c.be, 24 * E)) ||
-      (rc = dalloc(c, &c.partials, c.partials_cap = 4 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64)) ||
+      (rc = dalloc(c, &c.partials, c.partials_cap = 4 * std::max(max_spmv_blocks(c), node_blocks(c)) + 64)) ||
       (rc = dalloc(c, &c.red, 16)) || (rc = dalloc(c, &c.red_loc, 16)) || (rc = dalloc(c, &c.cg, 1)) ||
       (rc = dalloc(c, &c.hist, (int64_t)o->ksp_max_it + 2)))
     return rc;
@@ -867,6 +887,14 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.spmv_subl = (int)value;
     if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
       set_error("spmv_subl: partials buffer too small");
+      return 2;
+    }
+    return 0;
+  }
+  if (!std::strcmp(name, "spmv_zblocks")) {
+    c.spmv_zblocks = (int)value;
+    if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
+      set_error("spmv_zblocks: partials buffer too small");
       return 2;
     }
     return 0;

@@ -726,18 +726,15 @@ __global__ __launch_bounds__(TPB) void k_spmv_sym(Geo g, const double* __restric
 // of the chunk pull the few source blocks they need from HBM/L2 instead.  Every row is the sum
 // of its 27 block products (each a 3-term partial sum) in ascending nb order, however the
 // products were routed, so the result is independent of tiling and rank grid.
-constexpr int ZTX = 64, ZTY = 4;
-
 struct ZTiling {
   int ntx, nty, nzc, kc;  // tiles in x, y; z chunks and planes per chunk
 };
 
-static ZTiling z_tiling(const Geo& g) {
+static ZTiling z_tiling(const Geo& g, int ztx, int zty, int want) {
   ZTiling t;
-  t.ntx = (g.nx + ZTX - 1) / ZTX;
-  t.nty = (g.ny + ZTY - 1) / ZTY;
+  t.ntx = (g.nx + ztx - 1) / ztx;
+  t.nty = (g.ny + zty - 1) / zty;
   const int tiles = t.ntx * t.nty;
-  const int want = 1024;  // ~2 resident blocks per CU (80 KB LDS each) x 256 CUs x 2 rounds
   t.nzc = std::max(1, std::min(g.nz, (want + tiles - 1) / tiles));
   t.kc = (g.nz + t.nzc - 1) / t.nzc;
   t.nzc = (g.nz + t.kc - 1) / t.kc;
@@ -764,13 +761,14 @@ __device__ __forceinline__ void ut_x(const double* __restrict__ U, const double*
   c2 += uval(U, p, base + 8) * x2;
 }
 
-template <bool DOT, bool GATED>
-__global__ __launch_bounds__(256) void k_spmv_symz(Geo g, const double* __restrict__ U, const double* __restrict__ x,
-                                                   double* __restrict__ y, double* __restrict__ part,
-                                                   const CgState* __restrict__ cg, ZTiling zt) {
+template <bool DOT, bool GATED, int ZTX, int ZTY>
+__global__ __launch_bounds__(ZTX * ZTY, (ZTX * ZTY >= 512 ? 1 : 2)) void k_spmv_symz(Geo g, const double* __restrict__ U,
+                                                         const double* __restrict__ x, double* __restrict__ y,
+                                                         double* __restrict__ part, const CgState* __restrict__ cg,
+                                                         ZTiling zt) {
   __shared__ double accN[9][3][ZTY * ZTX];  // next-plane contributions, by the target's lower nb (0..8)
   __shared__ double accC[4][3][ZTY * ZTX];  // current-plane contributions, lower nb 9..12
-  __shared__ double sh[4];
+  __shared__ double sh[(ZTX * ZTY) / 64];
   if (GATED && cg->reason) return;
   // block -> (tile x, tile y, z chunk); tiles of one XCD form a y-slab (blocks b, b+8 share an XCD)
   const int b = blockIdx.x;
@@ -822,28 +820,65 @@ __global__ __launch_bounds__(256) void k_spmv_symz(Geo g, const double* __restri
       }
     }
     __syncthreads();
-    // 2. push: this node's transposed upper products to in-tile targets
+    // 2. one pass over this node's upper storage: its own rows' upper sum (diagonal block, then
+    //    nb 14..26 ascending) and the transposed products pushed to in-tile targets
+    double s0 = 0., s1 = 0., s2 = 0.;
+    double x0 = 0., x1 = 0., x2 = 0.;
     if (active) {
-      const double x0 = x[3 * (int64_t)pc], x1 = x[3 * (int64_t)pc + 1], x2 = x[3 * (int64_t)pc + 2];
-#pragma unroll
+      x0 = x[3 * (int64_t)pc];
+      x1 = x[3 * (int64_t)pc + 1];
+      x2 = x[3 * (int64_t)pc + 2];
+      const double* Ug = U + (int64_t)(pc >> 6) * (UPAIR * 128) + 2 * (pc & 63);
+      {
+        const double d00 = Ug[0], d01 = Ug[1], d02 = Ug[128], d11 = Ug[129], d12 = Ug[256], d22 = Ug[257];
+        s0 = d00 * x0;
+        s0 += d01 * x1;
+        s0 += d02 * x2;
+        s1 = d01 * x0;
+        s1 += d11 * x1;
+        s1 += d12 * x2;
+        s2 = d02 * x0;
+        s2 += d12 * x1;
+        s2 += d22 * x2;
+      }
+#pragma unroll 2
       for (int nbp = 14; nbp < 27; nbp++) {
         const int dx = nbp % 3 - 1, dy = (nbp / 3) % 3 - 1, dz = nbp / 9 - 1;
-        // target = this node + (dx,dy,dz); its lower nb = 26 - nbp; target is in-tile iff this
-        // node is in-tile seen from the target, i.e. in_tile at (lx+dx, ly+dy) for the target
+        double a[9];
+#pragma unroll
+        for (int t = 0; t < 9; t++) {
+          const int s = 6 + 9 * (nbp - 14) + t;
+          a[t] = Ug[(s >> 1) * 128 + (s & 1)];
+        }
+        // own rows: U(m, nbp) x_{m + off}
+        const int q = pc + dx + dy * PX + dz * PXY;
+        const double z0 = x[3 * (int64_t)q], z1 = x[3 * (int64_t)q + 1], z2 = x[3 * (int64_t)q + 2];
+        double u0 = a[0] * z0;
+        u0 += a[1] * z1;
+        u0 += a[2] * z2;
+        double u1 = a[3] * z0;
+        u1 += a[4] * z1;
+        u1 += a[5] * z2;
+        double u2 = a[6] * z0;
+        u2 += a[7] * z1;
+        u2 += a[8] * z2;
+        s0 += u0;
+        s1 += u1;
+        s2 += u2;
+        // push U(m, nbp)^T x_m to the target m + (dx,dy,dz) when it is inside this tile
         const int tx = lx + dx, ty = ly + dy;
         if (tx < 0 || tx >= ZTX || ty < 0 || ty >= ZTY) continue;
         if (i + dx >= g.nx || j + dy >= g.ny) continue;
         if (dz == 1 && k + 1 >= k1) continue;
-        const int base = 6 + 9 * (nbp - 14);
-        double c0 = uval(U, pc, base + 0) * x0;
-        c0 += uval(U, pc, base + 3) * x1;
-        c0 += uval(U, pc, base + 6) * x2;
-        double c1 = uval(U, pc, base + 1) * x0;
-        c1 += uval(U, pc, base + 4) * x1;
-        c1 += uval(U, pc, base + 7) * x2;
-        double c2 = uval(U, pc, base + 2) * x0;
-        c2 += uval(U, pc, base + 5) * x1;
-        c2 += uval(U, pc, base + 8) * x2;
+        double c0 = a[0] * x0;
+        c0 += a[3] * x1;
+        c0 += a[6] * x2;
+        double c1 = a[1] * x0;
+        c1 += a[4] * x1;
+        c1 += a[7] * x2;
+        double c2 = a[2] * x0;
+        c2 += a[5] * x1;
+        c2 += a[8] * x2;
         const int tgt = ty * ZTX + tx;
         if (dz == 1) {
           accN[26 - nbp][0][tgt] = c0;
@@ -858,7 +893,7 @@ __global__ __launch_bounds__(256) void k_spmv_symz(Geo g, const double* __restri
     }
     __syncthreads();
     if (active) {
-      // 3. lower blocks nb 9..12 (dz = 0)
+      // 3. lower blocks nb 9..12 (dz = 0), then the upper sum: y = (lower, ascending nb) + upper
 #pragma unroll
       for (int nb = 9; nb < 13; nb++) {
         const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1;
@@ -874,43 +909,9 @@ __global__ __launch_bounds__(256) void k_spmv_symz(Geo g, const double* __restri
         y1 += c1;
         y2 += c2;
       }
-      // 4. diagonal block (upper triangle mirrored) and upper blocks 14..26
-      const double x0 = x[3 * (int64_t)pc], x1 = x[3 * (int64_t)pc + 1], x2 = x[3 * (int64_t)pc + 2];
-      {
-        const double d00 = uval(U, pc, 0), d01 = uval(U, pc, 1), d02 = uval(U, pc, 2), d11 = uval(U, pc, 3),
-                     d12 = uval(U, pc, 4), d22 = uval(U, pc, 5);
-        double c0 = d00 * x0;
-        c0 += d01 * x1;
-        c0 += d02 * x2;
-        double c1 = d01 * x0;
-        c1 += d11 * x1;
-        c1 += d12 * x2;
-        double c2 = d02 * x0;
-        c2 += d12 * x1;
-        c2 += d22 * x2;
-        y0 += c0;
-        y1 += c1;
-        y2 += c2;
-      }
-#pragma unroll
-      for (int nb = 14; nb < 27; nb++) {
-        const int off = (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
-        const int q = pc + off;
-        const double z0 = x[3 * (int64_t)q], z1 = x[3 * (int64_t)q + 1], z2 = x[3 * (int64_t)q + 2];
-        const int base = 6 + 9 * (nb - 14);
-        double c0 = uval(U, pc, base + 0) * z0;
-        c0 += uval(U, pc, base + 1) * z1;
-        c0 += uval(U, pc, base + 2) * z2;
-        double c1 = uval(U, pc, base + 3) * z0;
-        c1 += uval(U, pc, base + 4) * z1;
-        c1 += uval(U, pc, base + 5) * z2;
-        double c2 = uval(U, pc, base + 6) * z0;
-        c2 += uval(U, pc, base + 7) * z1;
-        c2 += uval(U, pc, base + 8) * z2;
-        y0 += c0;
-        y1 += c1;
-        y2 += c2;
-      }
+      y0 += s0;
+      y1 += s1;
+      y2 += s2;
       const int n = i + j * g.nx + k * g.nx * g.ny;
       y[3 * (int64_t)n + 0] = y0;
       y[3 * (int64_t)n + 1] = y1;
@@ -919,9 +920,33 @@ __global__ __launch_bounds__(256) void k_spmv_symz(Geo g, const double* __restri
     }
   }
   if (DOT) {
-    double s = block_sum<256>(dot, sh);
+    double s = block_sum<ZTX * ZTY>(dot, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = s;
   }
+}
+
+static void z_shape(int kern, int& ztx, int& zty) {
+  switch (kern) {
+    case 2: ztx = 32; zty = 4; break;
+    case 3: ztx = 64; zty = 2; break;
+    case 4: ztx = 128; zty = 2; break;
+    case 5: ztx = 128; zty = 4; break;
+    case 6: ztx = 256; zty = 2; break;
+    default: ztx = 64; zty = 4; break;
+  }
+}
+
+template <int ZTX, int ZTY>
+static void launch_symz(Ctx& c, const double* xpad, double* y, bool dot, bool gated, const ZTiling& zt, int nb) {
+  if (dot && gated)
+    hipLaunchKernelGGL((k_spmv_symz<true, true, ZTX, ZTY>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g, c.U, xpad, y,
+                       c.partials, c.cg, zt);
+  else if (dot)
+    hipLaunchKernelGGL((k_spmv_symz<true, false, ZTX, ZTY>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g, c.U, xpad, y,
+                       c.partials, c.cg, zt);
+  else
+    hipLaunchKernelGGL((k_spmv_symz<false, false, ZTX, ZTY>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g, c.U, xpad,
+                       y, c.partials, c.cg, zt);
 }
 
 // ---------------------------------------------------------------------------- CG vectors
@@ -1178,8 +1203,10 @@ int dirichlet_mask_host(const Geo& g, int gi, int gj, int gk) { return dirichlet
 
 int64_t node_blocks(const Ctx& c) { return nblk(c.g.nown); }
 int64_t spmv_grid_blocks(const Ctx& c) {
-  if (c.U && c.spmv_kernel == 1) {
-    const ZTiling zt = z_tiling(c.g);
+  if (c.U && c.spmv_kernel >= 1) {
+    int ztx, zty;
+    z_shape(c.spmv_kernel, ztx, zty);
+    const ZTiling zt = z_tiling(c.g, ztx, zty, c.spmv_zblocks);
     return 8 * (int64_t)(((zt.nty + 7) / 8) * zt.ntx * zt.nzc);
   }
   return 8 * (int64_t)spmv_tiling(c.g, c.spmv_subl).per_xcd;
@@ -1240,17 +1267,18 @@ void launch_jacobi(Ctx& c) {
 void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
   const int nb = (int)spmv_grid_blocks(c);
   const SpmvTiling tl = spmv_tiling(c.g, c.spmv_subl);
-  if (c.U && c.spmv_kernel == 1) {
-    const ZTiling zt = z_tiling(c.g);
-    if (dot && gated)
-      hipLaunchKernelGGL((k_spmv_symz<true, true>), dim3(nb), dim3(256), 0, c.stream, c.g, c.U, xpad, y, c.partials,
-                         c.cg, zt);
-    else if (dot)
-      hipLaunchKernelGGL((k_spmv_symz<true, false>), dim3(nb), dim3(256), 0, c.stream, c.g, c.U, xpad, y, c.partials,
-                         c.cg, zt);
-    else
-      hipLaunchKernelGGL((k_spmv_symz<false, false>), dim3(nb), dim3(256), 0, c.stream, c.g, c.U, xpad, y, c.partials,
-                         c.cg, zt);
+  if (c.U && c.spmv_kernel >= 1) {
+    int ztx, zty;
+    z_shape(c.spmv_kernel, ztx, zty);
+    const ZTiling zt = z_tiling(c.g, ztx, zty, c.spmv_zblocks);
+    switch (c.spmv_kernel) {
+      case 2: launch_symz<32, 4>(c, xpad, y, dot, gated, zt, nb); break;
+      case 3: launch_symz<64, 2>(c, xpad, y, dot, gated, zt, nb); break;
+      case 4: launch_symz<128, 2>(c, xpad, y, dot, gated, zt, nb); break;
+      case 5: launch_symz<128, 4>(c, xpad, y, dot, gated, zt, nb); break;
+      case 6: launch_symz<256, 2>(c, xpad, y, dot, gated, zt, nb); break;
+      default: launch_symz<64, 4>(c, xpad, y, dot, gated, zt, nb); break;
+    }
     return;
   }
   if (c.U) {

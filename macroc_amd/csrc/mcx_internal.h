@@ -105,7 +105,8 @@ struct Ctx {
   int64_t npgroups = 0;
   int64_t nupper_local = 0;  // sbaij: stored upper values of the owned rows
   int spmv_subl = 0;         // SpMV sweep: lines per sub-slab of an XCD's slab (0 = whole slab)
-  int spmv_kernel = 0;       // sbaij: 0 = pull, 1 = z-marching push/pull tiles (experimental)
+  int spmv_kernel = 0;       // sbaij: 0 = pull, 1..4 = z-marching push/pull tiles (shapes, see z_shape)
+  int spmv_zblocks = 1024;   // z-marching: target block count (sets the z-chunk length)
   int spmv_nt = 1;           // aij: non-temporal matrix loads (streamed once; +1.4% measured)
   int64_t partials_cap = 0;
   double* eps = nullptr;     // [6][8][nelem]
