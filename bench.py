@@ -171,7 +171,8 @@ def main():
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--same-device", action="store_true", help="testing only: every rank on device 0")
     ap.add_argument("--mat-type", default="aij", choices=["aij", "sbaij"], help="-dm_mat_type of the headline")
-    ap.add_argument("--variants", default="sbaij", help="other -dm_mat_type runs reported beside it ('' = none)")
+    ap.add_argument("--variants", default=None,
+                    help="other -dm_mat_type runs reported beside it ('' = none; default sbaij on one GPU only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -194,6 +195,8 @@ def main():
         return measure(argv + ["-dm_mat_type", mat_type], rank, world, comm_id, args)
 
     r = run(args.mat_type)
+    if args.variants is None:
+        args.variants = "sbaij" if world == 1 else ""
     variants = {}
     if args.variants:
         for v in args.variants.split(","):
@@ -205,8 +208,10 @@ def main():
                 vr = run(v)
                 variants[v] = {"value": 3 * NX * NY * NZ / (vr["ms_step"] * 1e-3), "ms_per_step": vr["ms_step"],
                                "cg_its": vr["its"], "ms_per_cg_iter": vr["tm"]["solve_ms"] / max(vr["its"], 1),
+                               "dof_cg_iters_per_s": 3 * NX * NY * NZ * vr["its"] / (vr["tm"]["solve_ms"] * 1e-3),
                                "spmv_avg_ms": vr["spmv_avg_ms"], "spmv_bytes_per_launch": vr["spmv_bytes"],
-                               "spmv_achieved_GBs": vr["achieved"], "check": vr["check"]}
+                               "spmv_achieved_GBs": vr["achieved"], "spmv_traffic": pmc_traffic(v, NX, NY, NZ),
+                               "check": vr["check"]}
     its, tm, info, check = r["its"], r["tm"], r["info"], r["check"]
     spmv_avg_ms, spmv_bytes, achieved, ms_step = r["spmv_avg_ms"], r["spmv_bytes"], r["achieved"], r["ms_step"]
     ndofs = 3 * NX * NY * NZ
@@ -236,6 +241,9 @@ def main():
                        "dofs": ndofs, "nnz": info["nnz_global"], "parallelism": f"dmda{px}x{py}x{pz}", "mat_type": args.mat_type},
             "cg_its": its,
             "ms_per_cg_iter": tm["solve_ms"] / max(its, 1),
+            # CG iterations grow ~linearly with the global grid edge (720 at 64^3, 2814 at 256^3),
+            # so Newton-iter DOF/s cannot weak-scale; DOF x CG iterations / solve second can
+            "dof_cg_iters_per_s": ndofs * its / (tm["solve_ms"] * 1e-3),
             "phases_ms": {k: tm[k] for k in ("strains_ms", "homogenize_ms", "residual_ms", "jacobian_ms",
                                              "solve_ms", "update_ms")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",

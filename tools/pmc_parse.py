@@ -1,0 +1,63 @@
+"""Parse the two rocprofv3 PMC passes of tools/pmc_spmv.sh into per-launch HBM bytes and merge
+them into profiles/pmc_spmv.json (read by bench.py's roofline.traffic).  gfx950 correction:
+FETCH_SIZE counts half the bytes of 16-B-per-lane streaming reads (MI355X_MICROARCH.md, HBM /
+rocprofv3 section), so reads = 2 * FETCH_SIZE; WRITE_SIZE is exact.  Both are in KB."""
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+mat, grid, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
+
+
+def per_dispatch(counter):
+    files = glob.glob(os.path.join(out, counter, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv for {counter} under {out}")
+    vals = {}
+    names = {}
+    for fn in files:
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                if row.get("Counter_Name") != counter:
+                    continue
+                d = row["Dispatch_Id"]
+                vals[d] = vals.get(d, 0.0) + float(row["Counter_Value"])
+                names[d] = row["Kernel_Name"]
+    return vals, names
+
+
+fetch, names = per_dispatch("FETCH_SIZE")
+write, _ = per_dispatch("WRITE_SIZE")
+# gated launches of a converged chunk do no work: keep launches that read > 1 % of the median max
+big = max(fetch.values())
+f_real = [v for v in fetch.values() if v > 0.01 * big]
+bigw = max(write.values())
+w_real = [v for v in write.values() if v > 0.01 * bigw]
+fk, wk = statistics.median(f_real), statistics.median(w_real)
+hbm = (2 * fk + wk) * 1024
+kern = sorted(set(n.split("(")[0] for n in names.values()))
+summary = (f"{mat} {grid}^3 kernels {kern}: FETCH_SIZE dispatches={len(fetch)} real={len(f_real)} "
+           f"median={fk:.1f} KB; WRITE_SIZE dispatches={len(write)} real={len(w_real)} median={wk:.1f} KB; "
+           f"HBM bytes per launch = (2*FETCH + WRITE)*1024 = {hbm / 1e9:.3f} GB")
+print(summary)
+# accumulate in gpurun_out/pmc/pmc_spmv.json (merged back from the GPU box), seeded from the
+# committed profiles/pmc_spmv.json; copy it into profiles/ after review
+root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+path = os.path.join(out, "..", "pmc_spmv.json")
+seed = path if os.path.exists(path) else os.path.join(root, "profiles", "pmc_spmv.json")
+try:
+    with open(seed) as f:
+        d = json.load(f)
+except (OSError, ValueError):
+    d = {}
+d[f"{mat}:{grid}x{grid}x{grid}"] = {"hbm_bytes_per_launch": hbm, "fetch_kb_median": fk, "write_kb_median": wk,
+                                     "launches": len(f_real), "kernels": kern,
+                                     "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes, "
+                                               "--kernel-include-regex, bench.py --steps 1 --warmup 0"}
+with open(path, "w") as f:
+    json.dump(d, f, indent=1, sort_keys=True)
+with open(os.path.join(out, "summary.txt"), "w") as f:
+    f.write(summary + "\n")
