@@ -118,6 +118,16 @@ static SpmvTiling spmv_tiling(const Geo& g, int subl) {
 __device__ __forceinline__ int spmv_node(const Geo& g, int TX, int LPB, int nxc, int jgroups, int subl, int& ii,
                                          int& jj, int& kk) {
   const int b = blockIdx.x;
+  if (subl < 0) {  // linear order: consecutive blocks = consecutive lines (k, line group, x chunk)
+    const int k = b / (jgroups * nxc);
+    const int rem = b - k * (jgroups * nxc);
+    const int i = (rem % nxc) * TX + (int)(threadIdx.x % TX), j = (rem / nxc) * LPB + (int)(threadIdx.x / TX);
+    if (k >= g.nz || i >= g.nx || j >= g.ny) return -1;
+    ii = i;
+    jj = j;
+    kk = k;
+    return i + g.nx * (j + g.ny * k);
+  }
   const int x = b & 7;
   int t = b >> 3;
   const int slab = (jgroups + 7) >> 3;
@@ -615,7 +625,7 @@ struct PairLoop<0, NT> {
                                              double&) {}
 };
 
-template <bool DOT, bool GATED, bool NT = false>
+template <bool DOT, bool GATED, int NT = 0>
 __global__ __launch_bounds__(TPB) void k_spmv(Geo g, const double2* __restrict__ V, const double* __restrict__ x,
                                               double* __restrict__ y, double* __restrict__ part,
                                               const CgState* __restrict__ cg, SpmvTiling tl) {
@@ -638,10 +648,16 @@ __global__ __launch_bounds__(TPB) void k_spmv(Geo g, const double2* __restrict__
     }
     const double2* v = V + (int64_t)(n >> 6) * (NPAIR * 64) + (n & 63);
     double y0 = 0., y1 = 0., y2 = 0.;
-    PairLoop<NPAIR, NT>::run(v, xv, y0, y1, y2);
-    y[3 * n + 0] = y0;
-    y[3 * n + 1] = y1;
-    y[3 * n + 2] = y2;
+    PairLoop<NPAIR, (NT > 0)>::run(v, xv, y0, y1, y2);
+    if constexpr (NT == 2) {
+      __builtin_nontemporal_store(y0, &y[3 * n + 0]);
+      __builtin_nontemporal_store(y1, &y[3 * n + 1]);
+      __builtin_nontemporal_store(y2, &y[3 * n + 2]);
+    } else {
+      y[3 * n + 0] = y0;
+      y[3 * n + 1] = y1;
+      y[3 * n + 2] = y2;
+    }
     if (DOT) dot = xv[13][0] * y0 + xv[13][1] * y1 + xv[13][2] * y2;
   }
   if (DOT) {
@@ -1209,7 +1225,9 @@ int64_t spmv_grid_blocks(const Ctx& c) {
     const ZTiling zt = z_tiling(c.g, ztx, zty, c.spmv_zblocks);
     return 8 * (int64_t)(((zt.nty + 7) / 8) * zt.ntx * zt.nzc);
   }
-  return 8 * (int64_t)spmv_tiling(c.g, c.spmv_subl).per_xcd;
+  const SpmvTiling t = spmv_tiling(c.g, c.spmv_subl);
+  if (c.spmv_subl < 0) return (int64_t)c.g.nz * t.jgroups * t.nxc;
+  return 8 * (int64_t)t.per_xcd;
 }
 
 int upload_constants(Ctx& c) {
@@ -1294,12 +1312,21 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
     return;
   }
   const double2* V = reinterpret_cast<const double2*>(c.V);
-  if (c.spmv_nt) {
+  if (c.spmv_nt == 2) {
     if (dot && gated)
-      hipLaunchKernelGGL((k_spmv<true, true, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials, c.cg,
+      hipLaunchKernelGGL((k_spmv<true, true, 2>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials, c.cg,
                          tl);
     else
-      hipLaunchKernelGGL((k_spmv<true, false, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials,
+      hipLaunchKernelGGL((k_spmv<true, false, 2>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials,
+                         c.cg, tl);
+    return;
+  }
+  if (c.spmv_nt) {
+    if (dot && gated)
+      hipLaunchKernelGGL((k_spmv<true, true, 1>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials, c.cg,
+                         tl);
+    else
+      hipLaunchKernelGGL((k_spmv<true, false, 1>), dim3(nb), dim3(TPB), 0, c.stream, c.g, V, xpad, y, c.partials,
                          c.cg, tl);
     return;
   }

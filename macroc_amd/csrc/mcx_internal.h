@@ -104,10 +104,10 @@ struct Ctx {
   double* U = nullptr;       // sbaij upper stencil blocks over the padded box [npgroups][UPAIR][64] double2
   int64_t npgroups = 0;
   int64_t nupper_local = 0;  // sbaij: stored upper values of the owned rows
-  int spmv_subl = 0;         // SpMV sweep: lines per sub-slab of an XCD's slab (0 = whole slab)
+  int spmv_subl = 0;         // SpMV sweep: lines per sub-slab of an XCD's slab (0 = whole slab, -1 = linear order)
   int spmv_kernel = 0;       // sbaij: 0 = pull, 1..4 = z-marching push/pull tiles (shapes, see z_shape)
   int spmv_zblocks = 1024;   // z-marching: target block count (sets the z-chunk length)
-  int spmv_nt = 1;           // aij: non-temporal matrix loads (streamed once; +1.4% measured)
+  int spmv_nt = 2;           // aij: 1 = non-temporal matrix loads, 2 = + non-temporal y stores (-3 %, spmv_ab)
   int64_t partials_cap = 0;
   double* eps = nullptr;     // [6][8][nelem]
   double* sig = nullptr;     // [6][8][nelem]
