@@ -160,6 +160,18 @@ int mcx_update_vars(void* ctx);
    elements: GPs with f_trial > 0 in the last homogenize, and the max f_trial */
 int mcx_get_nonlinear_stats(void* ctx, int64_t* n_nonlinear, double* f_trial_max);
 
+/* get_non_linear_gps + get_f_trial_max (src/util.c:69-102, called at src/main.c:88,93):
+ * collective.  n_local = this rank's count (its gauss_evolution.dat column), n_total = the sum
+ * over ranks (MPI_Gather + sum), f_trial_max = the max over ranks (MPI_Reduce MAX). */
+int mcx_reduce_nonlinear(void* ctx, int64_t* n_local, int64_t* n_total, double* f_trial_max);
+
+/* calc_force (src/forces.c:25-166, called at src/main.c:91): reaction force of the load case
+ * from the Gauss-point stresses of the last homogenize — BC_CIRCLE: sum over the top element
+ * layer inside the load circle of (sum over 8 GPs of sigma_yy) * dx * dz; BC_BENDING: last x
+ * layer, sigma_xy * dy * dz; per rank in the reference's loop order and element set, then
+ * summed over ranks.  Collective; every rank receives the total. */
+int mcx_calc_force(void* ctx, double* force);
+
 /* src/main.c:57-82 for one time step; returns Newton iterations done, per-iteration
    |RES|, KSP its and KSP rnorm in caller arrays of length >= newton_max_its (may be NULL) */
 int mcx_time_step(void* ctx, int time_s, int* newton_its, double* res, int* ksp_its, double* ksp_rnorm);

@@ -74,7 +74,7 @@ static int free_ctx(Ctx* c) {
 static int64_t max_spmv_blocks(Ctx& c) {
   const int keep = c.spmv_kernel;
   int64_t m = 0;
-  for (int k = 0; k <= 6; k++) {
+  for (int k = 0; k <= 10; k++) {
     c.spmv_kernel = k;
     m = std::max(m, spmv_grid_blocks(c));
   }
@@ -649,6 +649,89 @@ int mcx_get_nonlinear_stats(void* ctx, int64_t* n_nonlinear, double* f_trial_max
   return 0;
 }
 
+}  // extern "C"
+
+// all-reduce of a few host doubles through red_loc / red (collective; op 0 sum, 1 max)
+static int host_allreduce(Ctx& c, double* v, int n, int op) {
+  if (c.nranks <= 1) return 0;
+  int rc;
+  if ((rc = allreduce_prepare(c))) return rc;
+  MCX_HIP(hipMemcpyAsync(c.red_loc, v, sizeof(double) * n, hipMemcpyHostToDevice, c.stream));
+  rc = op ? allreduce_max(c, c.red_loc, c.red, n) : allreduce_sum(c, c.red_loc, c.red, n);
+  if (rc) return rc;
+  MCX_HIP(hipMemcpyAsync(v, c.red, sizeof(double) * n, hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  return 0;
+}
+
+extern "C" {
+
+int mcx_reduce_nonlinear(void* ctx, int64_t* n_local, int64_t* n_total, double* f_trial_max) {
+  GUARD(ctx);
+  CTX(ctx);
+  int64_t n = 0;
+  double fm = 0.;
+  int rc = mcx_get_nonlinear_stats(ctx, &n, &fm);
+  if (rc) return rc;
+  double s = (double)n;  // exact: at most 8 x elements GPs
+  if ((rc = host_allreduce(c, &s, 1, 0)) || (rc = host_allreduce(c, &fm, 1, 1))) return rc;
+  if (n_local) *n_local = n;
+  if (n_total) *n_total = (int64_t)s;
+  if (f_trial_max) *f_trial_max = fm;
+  return 0;
+}
+
+int mcx_calc_force(void* ctx, double* force) {
+  GUARD(ctx);
+  CTX(ctx);
+  const Geo& g = c.g;
+  // the rank's own elements as PETSc lists them (DMDAGetElements): [s - (s > 0), s + w - 1)
+  int lo[3], cnt[3];
+  const int s[3] = {g.xs, g.ys, g.zs}, w[3] = {g.nx, g.ny, g.nz};
+  for (int d = 0; d < 3; d++) {
+    lo[d] = s[d] > 0 ? s[d] - 1 : s[d];
+    cnt[d] = std::max(0, s[d] + w[d] - 1 - lo[d]);
+  }
+  double mpi_force = 0.0;
+  std::vector<double> ave;
+  auto layer = [&](int comp, int fa, int fixed, int a0, int na, int b0, int nb) -> int {
+    ave.assign((size_t)na * nb, 0.);
+    if (ave.empty()) return 0;
+    launch_force_layer(c, comp, fa, fixed, a0, na, b0, nb, c.tmp);
+    MCX_HIP(hipMemcpyAsync(ave.data(), c.tmp, sizeof(double) * ave.size(), hipMemcpyDeviceToHost, c.stream));
+    MCX_HIP(hipStreamSynchronize(c.stream));
+    return 0;
+  };
+  int rc;
+  if (g.bc_type == MCX_BC_BENDING) {
+    // calc_force_bending src/forces.c:58-106: ranks owning x = NX-1 (owned corner, :75),
+    // their last x layer of elements, ey outer / ez inner, stress_ave[3] * dy * dz
+    if (g.xs + g.nx == g.NX && cnt[0] > 0) {
+      if ((rc = layer(3, 0, lo[0] + cnt[0] - 1, lo[1], cnt[1], lo[2], cnt[2]))) return rc;
+      for (int ey = 0; ey < cnt[1]; ++ey)
+        for (int ez = 0; ez < cnt[2]; ++ez) mpi_force += ave[(size_t)ey * cnt[2] + ez] * c.dy * g.dz;
+    }
+  } else {
+    // calc_force_circle src/forces.c:115-166: ghost corners si, sj, sk with the owned ny
+    // (:130-133), top element layer, ex outer / ez inner, elements whose centre is inside
+    // the radius, stress_ave[1] * dx * dz
+    const int si = lo[0], sj = lo[1], sk = lo[2];
+    if (sj + g.ny == g.NY && cnt[1] > 0) {
+      if ((rc = layer(1, 1, lo[1] + cnt[1] - 1, lo[0], cnt[0], lo[2], cnt[2]))) return rc;
+      for (int ex = 0; ex < cnt[0]; ++ex)
+        for (int ez = 0; ez < cnt[2]; ++ez) {
+          const double x = g.lx / 2. - ((si + ex) * g.dx + g.dx / 2.);
+          const double z = g.lz / 2. - ((sk + ez) * g.dz + g.dz / 2.);
+          if ((x * x + z * z) < 1 * (g.rad * g.rad)) mpi_force += ave[(size_t)ex * cnt[2] + ez] * g.dx * g.dz;
+        }
+    }
+  }
+  // MPI_Reduce(SUM) src/forces.c:47 (here every rank receives the total)
+  if ((rc = host_allreduce(c, &mpi_force, 1, 0))) return rc;
+  if (force) *force = mpi_force;
+  return 0;
+}
+
 int mcx_time_step(void* ctx, int time_s, int* newton_its, double* res, int* ksp_its, double* ksp_rnorm) {
   GUARD(ctx);
   CTX(ctx);
@@ -790,8 +873,9 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
         for (int cc = 0; cc < 3; cc++) {
           double v = 0.;
           if (vals && c.U) {
-            const int64_t pc = (i + 1) + (j + 1) * (int64_t)g.PX + (k + 1) * (int64_t)g.PX * g.PY;
-            const int64_t q = pc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * (int64_t)g.PX + (nb / 9 - 1) * (int64_t)g.PX * g.PY;
+            // storage index u_of (kernels.hip): 64-aligned rows of UX nodes
+            const int64_t pc = 64 + i + (j + 1) * (int64_t)g.UX + (k + 1) * (int64_t)g.UXY;
+            const int64_t q = pc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * (int64_t)g.UX + (nb / 9 - 1) * (int64_t)g.UXY;
             static const int dsl[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
             if (nb < 13) v = uval(q, 6 + 9 * (12 - nb) + cc * 3 + r);
             else if (nb == 13) v = uval(pc, dsl[r][cc]);
@@ -897,6 +981,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
       set_error("spmv_zblocks: partials buffer too small");
       return 2;
     }
+    return 0;
+  }
+  if (!std::strcmp(name, "cg_nt")) {
+    c.cg_nt = (int)value;
     return 0;
   }
   if (!std::strcmp(name, "spmv_nt")) {

@@ -103,7 +103,7 @@ int halo_exchange(Ctx& c, double* xpad) {
   return 0;
 }
 
-int allreduce_sum(Ctx& c, const double* in, double* out, int count) {
+static int allreduce_op(Ctx& c, const double* in, double* out, int count, int op) {
   if (c.nranks <= 1) {
     if (in != out) MCX_HIP(hipMemcpyAsync(out, in, sizeof(double) * count, hipMemcpyDeviceToDevice, c.stream));
     return 0;
@@ -113,14 +113,18 @@ int allreduce_sum(Ctx& c, const double* in, double* out, int count) {
     MCX_HIP(hipEventRecord(g->ev_red[c.rank], c.stream));
     group_barrier(g);
     for (int q = 0; q < g->nranks; q++) MCX_HIP(hipStreamWaitEvent(c.stream, g->ev_red[q], 0));
-    launch_group_sum(c, (const double* const*)g->d_red_ptrs, g->nranks, count, out);
+    launch_group_sum(c, (const double* const*)g->d_red_ptrs, g->nranks, count, out, op);
     MCX_HIP(hipEventRecord(g->ev_sum[c.rank], c.stream));
     group_barrier(g);
     return 0;
   }
-  MCX_NCCL(ncclAllReduce(in, out, count, ncclDouble, ncclSum, (ncclComm_t)c.comm, c.stream));
+  MCX_NCCL(ncclAllReduce(in, out, count, ncclDouble, op ? ncclMax : ncclSum, (ncclComm_t)c.comm, c.stream));
   return 0;
 }
+
+// in must be red_loc (the in-process transport sums every member's red_loc)
+int allreduce_sum(Ctx& c, const double* in, double* out, int count) { return allreduce_op(c, in, out, count, 0); }
+int allreduce_max(Ctx& c, const double* in, double* out, int count) { return allreduce_op(c, in, out, count, 1); }
 
 // before overwriting red_loc: every member has summed the previous partials
 int allreduce_prepare(Ctx& c) {

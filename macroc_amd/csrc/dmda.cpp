@@ -138,7 +138,12 @@ int setup_decomposition(Ctx& c) {
   g.wg = g.dx * c.dy * g.dz / NPE;
   g.rad = o.rad;
   c.ngroups = (g.nown + GROUP - 1) / GROUP;
-  c.npgroups = ((int64_t)g.PX * g.PY * g.PZ + GROUP - 1) / GROUP;
+  // sbaij storage: padded box with 64-aligned rows so every x-line of owned nodes starts a
+  // 64-node group (a wave's loads never straddle two groups); node (i, j, k), i in -1..nx, at
+  // 64 + i + (j+1)*UX + (k+1)*UXY (i = -1 lands in the unused last column of the row before)
+  g.UX = (g.nx + 2 + GROUP - 1) / GROUP * GROUP;
+  g.UXY = g.UX * g.PY;
+  c.npgroups = (GROUP + (int64_t)g.UXY * g.PZ + GROUP - 1) / GROUP;
   return 0;
 }
 

@@ -35,6 +35,12 @@ __device__ __forceinline__ int pad_of(const Geo& g, int i, int j, int k) {
   return (i + 1) + (j + 1) * g.PX + (k + 1) * g.PX * g.PY;
 }
 
+// sbaij storage index of node (i, j, k), i, j, k in -1..n (DMDA padded box, 64-aligned rows);
+// neighbour (dx, dy, dz) is u_of + dx + dy*UX + dz*UXY
+__device__ __forceinline__ int u_of(const Geo& g, int i, int j, int k) {
+  return 64 + i + (j + 1) * g.UX + (k + 1) * g.UXY;
+}
+
 // Dirichlet DOFs of a global node as a bit mask (bit d = DOF d).  The union over ranks of
 // bc_init_circle's ghost-corner lists (src/bcs.c:254-338) is exactly: the four y=0 edges,
 // all DOFs; dof 1 of the y=LY nodes inside the load circle (cell-centre offset dx/2, :324-327).
@@ -538,7 +544,8 @@ __global__ __launch_bounds__(TPB) void k_gather_matrix_sym(Geo g, const double* 
 #pragma unroll
     for (int q = 0; q < 9; q++) val[q] = 0.;
   }
-  double* Ug = U + (int64_t)(p >> 6) * (UPAIR * 128) + 2 * (p & 63);
+  const int pu = u_of(g, pi - 1, pj - 1, pk - 1);
+  double* Ug = U + (int64_t)(pu >> 6) * (UPAIR * 128) + 2 * (pu & 63);
   if (t == 0) {
     const double up[6] = {val[0], val[1], val[2], val[4], val[5], val[8]};
 #pragma unroll
@@ -572,8 +579,8 @@ __global__ void k_jacobi_sym(Geo g, const double* __restrict__ U, double* __rest
   if (n >= g.nown) return;
   int i, j, k;
   node_ijk(g, n, i, j, k);
-  const int pc = pad_of(g, i, j, k);
-  const double* Ug = U + (int64_t)(pc >> 6) * (UPAIR * 128) + 2 * (pc & 63);
+  const int pu = u_of(g, i, j, k);
+  const double* Ug = U + (int64_t)(pu >> 6) * (UPAIR * 128) + 2 * (pu & 63);
   const int sl[3] = {0, 3, 5};
 #pragma unroll
   for (int r = 0; r < 3; r++) {
@@ -686,24 +693,26 @@ __global__ __launch_bounds__(TPB) void k_spmv_sym(Geo g, const double* __restric
   if (n >= 0) {
     const int PX = g.PX, PXY = g.PX * g.PY;
     const int pc = (i + 1) + (j + 1) * PX + (k + 1) * PXY;
+    const int uc = u_of(g, i, j, k);
     double y0 = 0., y1 = 0., y2 = 0.;
     double xc0 = 0., xc1 = 0., xc2 = 0.;
 #pragma unroll
     for (int nb = 0; nb < 27; nb++) {
       const int off = (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
       const int q = pc + off;
+      const int uq = uc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * g.UX + (nb / 9 - 1) * g.UXY;
       const double* xp = x + 3 * (int64_t)q;
       const double x0 = xp[0], x1 = xp[1], x2 = xp[2];
       double a[9];
       if (nb < 13) {
-        const double* Ug = U + (int64_t)(q >> 6) * (UPAIR * 128) + 2 * (q & 63);
+        const double* Ug = U + (int64_t)(uq >> 6) * (UPAIR * 128) + 2 * (uq & 63);
         const int base = 6 + 9 * (12 - nb);
 #pragma unroll
         for (int r = 0; r < 3; r++)
 #pragma unroll
           for (int c = 0; c < 3; c++) a[r * 3 + c] = usl<0>(Ug, base + c * 3 + r);
       } else if (nb == 13) {
-        const double* Ug = U + (int64_t)(pc >> 6) * (UPAIR * 128) + 2 * (pc & 63);
+        const double* Ug = U + (int64_t)(uc >> 6) * (UPAIR * 128) + 2 * (uc & 63);
         const double d00 = usl<0>(Ug, 0), d01 = usl<0>(Ug, 1), d02 = usl<0>(Ug, 2), d11 = usl<0>(Ug, 3),
                      d12 = usl<0>(Ug, 4), d22 = usl<0>(Ug, 5);
         a[0] = d00; a[1] = d01; a[2] = d02;
@@ -713,7 +722,7 @@ __global__ __launch_bounds__(TPB) void k_spmv_sym(Geo g, const double* __restric
         xc1 = x1;
         xc2 = x2;
       } else {
-        const double* Ug = U + (int64_t)(pc >> 6) * (UPAIR * 128) + 2 * (pc & 63);
+        const double* Ug = U + (int64_t)(uc >> 6) * (UPAIR * 128) + 2 * (uc & 63);
         const int base = 6 + 9 * (nb - 14);
 #pragma unroll
         for (int s = 0; s < 9; s++) a[s] = usl<0>(Ug, base + s);
@@ -762,19 +771,47 @@ __device__ __forceinline__ double uval(const double* __restrict__ U, int p, int 
 }
 
 // c = U(p, nb')^T x_p for upper block nb' (14..26) of padded node p
-__device__ __forceinline__ void ut_x(const double* __restrict__ U, const double* __restrict__ x, int p, int nbp,
-                                     double& c0, double& c1, double& c2) {
+// U(m, nbp)^T x_m with the block's 9 slots read as the 5 covering 16-B pairs (a pulled block
+// uses whole pairs: an 8-B scalar read would fetch the pair's line for half of it)
+__device__ __forceinline__ void ut_x2(const double* __restrict__ U, const double* __restrict__ x, int pu, int p,
+                                      int nbp, double& c0, double& c1, double& c2) {
+  const int base = 6 + 9 * (nbp - 14);
+  const double2* Ug = reinterpret_cast<const double2*>(U) + (int64_t)(pu >> 6) * (UPAIR * 64) + (pu & 63);
+  double a[10];
+  const int p0 = base >> 1, sh = base & 1;
+#pragma unroll
+  for (int q = 0; q < 5; q++) {
+    const double2 w = Ug[(p0 + q) * 64];
+    a[2 * q] = w.x;
+    a[2 * q + 1] = w.y;
+  }
+  const double* b = a + sh;
+  const double x0 = x[3 * (int64_t)p], x1 = x[3 * (int64_t)p + 1], x2 = x[3 * (int64_t)p + 2];
+  c0 = b[0] * x0;
+  c0 += b[3] * x1;
+  c0 += b[6] * x2;
+  c1 = b[1] * x0;
+  c1 += b[4] * x1;
+  c1 += b[7] * x2;
+  c2 = b[2] * x0;
+  c2 += b[5] * x1;
+  c2 += b[8] * x2;
+}
+
+// U(m, nbp)^T x_m for the node m at U index pu / padded-vector index p
+__device__ __forceinline__ void ut_x(const double* __restrict__ U, const double* __restrict__ x, int pu, int p,
+                                     int nbp, double& c0, double& c1, double& c2) {
   const int base = 6 + 9 * (nbp - 14);
   const double x0 = x[3 * (int64_t)p], x1 = x[3 * (int64_t)p + 1], x2 = x[3 * (int64_t)p + 2];
-  c0 = uval(U, p, base + 0) * x0;
-  c0 += uval(U, p, base + 3) * x1;
-  c0 += uval(U, p, base + 6) * x2;
-  c1 = uval(U, p, base + 1) * x0;
-  c1 += uval(U, p, base + 4) * x1;
-  c1 += uval(U, p, base + 7) * x2;
-  c2 = uval(U, p, base + 2) * x0;
-  c2 += uval(U, p, base + 5) * x1;
-  c2 += uval(U, p, base + 8) * x2;
+  c0 = uval(U, pu, base + 0) * x0;
+  c0 += uval(U, pu, base + 3) * x1;
+  c0 += uval(U, pu, base + 6) * x2;
+  c1 = uval(U, pu, base + 1) * x0;
+  c1 += uval(U, pu, base + 4) * x1;
+  c1 += uval(U, pu, base + 7) * x2;
+  c2 = uval(U, pu, base + 2) * x0;
+  c2 += uval(U, pu, base + 5) * x1;
+  c2 += uval(U, pu, base + 8) * x2;
 }
 
 template <bool DOT, bool GATED, int ZTX, int ZTY>
@@ -816,6 +853,7 @@ __global__ __launch_bounds__(ZTX * ZTY, (ZTX * ZTY >= 512 ? 1 : 2)) void k_spmv_
   };
   for (int k = k0; blk_ok && k < k1; k++) {
     const int pc = (i + 1) + (j + 1) * PX + (k + 1) * PXY;
+    const int uc = u_of(g, i, j, k);
     double y0 = 0., y1 = 0., y2 = 0.;
     // 1. lower blocks nb 0..8 (dz = -1), ascending nb
     if (active) {
@@ -828,7 +866,7 @@ __global__ __launch_bounds__(ZTX * ZTY, (ZTX * ZTY >= 512 ? 1 : 2)) void k_spmv_
           c1 = accN[nb][1][me];
           c2 = accN[nb][2][me];
         } else {
-          ut_x(U, x, pc + dx + dy * PX - PXY, 26 - nb, c0, c1, c2);
+          ut_x(U, x, uc + dx + dy * g.UX - g.UXY, pc + dx + dy * PX - PXY, 26 - nb, c0, c1, c2);
         }
         y0 += c0;
         y1 += c1;
@@ -844,7 +882,7 @@ __global__ __launch_bounds__(ZTX * ZTY, (ZTX * ZTY >= 512 ? 1 : 2)) void k_spmv_
       x0 = x[3 * (int64_t)pc];
       x1 = x[3 * (int64_t)pc + 1];
       x2 = x[3 * (int64_t)pc + 2];
-      const double* Ug = U + (int64_t)(pc >> 6) * (UPAIR * 128) + 2 * (pc & 63);
+      const double* Ug = U + (int64_t)(uc >> 6) * (UPAIR * 128) + 2 * (uc & 63);
       {
         const double d00 = Ug[0], d01 = Ug[1], d02 = Ug[128], d11 = Ug[129], d12 = Ug[256], d22 = Ug[257];
         s0 = d00 * x0;
@@ -919,7 +957,7 @@ __global__ __launch_bounds__(ZTX * ZTY, (ZTX * ZTY >= 512 ? 1 : 2)) void k_spmv_
           c1 = accC[nb - 9][1][me];
           c2 = accC[nb - 9][2][me];
         } else {
-          ut_x(U, x, pc + dx + dy * PX, 26 - nb, c0, c1, c2);
+          ut_x(U, x, uc + dx + dy * g.UX, pc + dx + dy * PX, 26 - nb, c0, c1, c2);
         }
         y0 += c0;
         y1 += c1;
@@ -941,6 +979,200 @@ __global__ __launch_bounds__(ZTX * ZTY, (ZTX * ZTY >= 512 ? 1 : 2)) void k_spmv_
   }
 }
 
+// Phased z-marching sbaij SpMV.  Same tile march as k_spmv_symz, but the 13 upper blocks are
+// processed in three phases (nbp 14..18 | 19..22 | 23..26) that reuse one 5-slot LDS buffer
+// (120 B per node instead of 312), so a 128x4 tile runs two blocks per CU and only the tile's
+// first and last rows pull across y edges.  Matrix values are loaded as 16-B slot pairs.
+// Row order (fixed, tiling-independent: a term is the same 3-vector whether it arrives through
+// LDS or is pulled by the target, and it is added at the same position):
+//   lower dz=-1: nb 8 | 4 5 6 7 | 0 1 2 3,  lower dz=0: nb 9 10 11 12,  then the upper sum
+//   (diagonal block, nbp 14..26 ascending).
+template <bool DOT, bool GATED, int TX, int TY>
+__global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* __restrict__ U,
+                                                        const double* __restrict__ x, double* __restrict__ y,
+                                                        double* __restrict__ part, const CgState* __restrict__ cg,
+                                                        ZTiling zt) {
+  constexpr int T = TX * TY;
+  __shared__ double buf[5][3][T];
+  __shared__ double sh[T / 64];
+  if (GATED && cg->reason) return;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, t8 = b >> 3;
+  const int slab = (zt.nty + 7) >> 3;
+  const int ty0 = xcd * slab;
+  const int nty_here = min(slab, zt.nty - ty0);
+  const int per = max(nty_here, 0) * zt.ntx * zt.nzc;
+  const bool blk_ok = t8 < per;
+  int tyi = 0, txi = 0, zc = 0;
+  if (blk_ok) {
+    zc = t8 % zt.nzc;
+    const int r = t8 / zt.nzc;
+    txi = r % zt.ntx;
+    tyi = ty0 + r / zt.ntx;
+  }
+  if (!blk_ok) {  // whole block idle (uniform): still write the partial
+    if (DOT && threadIdx.x == 0) part[blockIdx.x] = 0.;
+    return;
+  }
+  const int lx = threadIdx.x % TX, ly = threadIdx.x / TX, me = threadIdx.x;
+  const int i = txi * TX + lx, j = tyi * TY + ly;
+  const bool active = i < g.nx && j < g.ny;
+  const int k0 = zc * zt.kc, k1 = min(g.nz, k0 + zt.kc);
+  const int PX = g.PX, PXY = g.PX * g.PY;
+  // in-tile (pushed through LDS) test for a partner at (dx, dy) in the tile's plane
+  auto in_tile = [&](int dx, int dy) {
+    const int sx = lx + dx, sy = ly + dy;
+    if (sx < 0 || sx >= TX || sy < 0 || sy >= TY) return false;
+    return i + dx < g.nx && j + dy < g.ny;
+  };
+  double dot = 0.;
+  double a0 = 0., a1 = 0., a2 = 0.;  // this plane's node: lower sum so far
+  double n0 = 0., n1 = 0., n2 = 0.;  // next plane's node: lower dz=-1 sum so far
+  // lower term nb of the node at padded index pc: from LDS slot or pulled
+  auto term = [&](int nb, int slot, bool from_lds, int pcn, int ucn, double& c0, double& c1, double& c2) {
+    if (from_lds) {
+      c0 = buf[slot][0][me];
+      c1 = buf[slot][1][me];
+      c2 = buf[slot][2][me];
+    } else {
+      const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
+      ut_x2(U, x, ucn + dx + dy * g.UX + dz * g.UXY, pcn + dx + dy * PX + dz * PXY, 26 - nb, c0, c1, c2);
+    }
+  };
+  for (int k = k0; k < k1; k++) {
+    const int pc = (i + 1) + (j + 1) * PX + (k + 1) * PXY;
+    const int uc = u_of(g, i, j, k);
+    const bool has_next = k + 1 < k1;
+    if (k == k0 && active) {  // chunk start: the previous plane is not marched here, pull all nine
+      a0 = a1 = a2 = 0.;
+      constexpr int ord[9] = {8, 4, 5, 6, 7, 0, 1, 2, 3};
+#pragma unroll
+      for (int q = 0; q < 9; q++) {
+        double c0, c1, c2;
+        term(ord[q], 0, false, pc, uc, c0, c1, c2);
+        a0 += c0;
+        a1 += c1;
+        a2 += c2;
+      }
+    }
+    double x0 = 0., x1 = 0., x2 = 0., s0 = 0., s1 = 0., s2 = 0.;
+    const double2* Ug = reinterpret_cast<const double2*>(U) + (int64_t)(uc >> 6) * (UPAIR * 64) + (uc & 63);
+    if (active) {
+      x0 = x[3 * (int64_t)pc];
+      x1 = x[3 * (int64_t)pc + 1];
+      x2 = x[3 * (int64_t)pc + 2];
+    }
+    n0 = n1 = n2 = 0.;
+#pragma unroll
+    for (int ph = 0; ph < 3; ph++) {
+      const int lo = ph == 0 ? 14 : (ph == 1 ? 19 : 23), hi = ph == 0 ? 18 : (ph == 1 ? 22 : 26);
+      if (active) {
+        // slot s of this node = half (s & 1) of 16-B pair s >> 1; pairs shared by adjacent
+        // blocks are the same load (read-only, merged by the compiler)
+        auto sl = [&](int s) {
+          const double2 w = Ug[(s >> 1) * 64];
+          return (s & 1) ? w.y : w.x;
+        };
+        if (ph == 0) {
+          const double d00 = sl(0), d01 = sl(1), d02 = sl(2), d11 = sl(3), d12 = sl(4), d22 = sl(5);
+          s0 = d00 * x0;
+          s0 += d01 * x1;
+          s0 += d02 * x2;
+          s1 = d01 * x0;
+          s1 += d11 * x1;
+          s1 += d12 * x2;
+          s2 = d02 * x0;
+          s2 += d12 * x1;
+          s2 += d22 * x2;
+        }
+#pragma unroll 2
+        for (int nbp = lo; nbp <= hi; nbp++) {
+          const int dx = nbp % 3 - 1, dy = (nbp / 3) % 3 - 1, dz = nbp / 9 - 1;
+          const int base = 6 + 9 * (nbp - 14);
+          double a[9];
+#pragma unroll
+          for (int t = 0; t < 9; t++) a[t] = sl(base + t);
+          const int q = pc + dx + dy * PX + dz * PXY;
+          const double z0 = x[3 * (int64_t)q], z1 = x[3 * (int64_t)q + 1], z2 = x[3 * (int64_t)q + 2];
+          double u0 = a[0] * z0;
+          u0 += a[1] * z1;
+          u0 += a[2] * z2;
+          double u1 = a[3] * z0;
+          u1 += a[4] * z1;
+          u1 += a[5] * z2;
+          double u2 = a[6] * z0;
+          u2 += a[7] * z1;
+          u2 += a[8] * z2;
+          s0 += u0;
+          s1 += u1;
+          s2 += u2;
+          if (!in_tile(dx, dy)) continue;
+          if (dz == 1 && !has_next) continue;
+          double c0 = a[0] * x0;
+          c0 += a[3] * x1;
+          c0 += a[6] * x2;
+          double c1 = a[1] * x0;
+          c1 += a[4] * x1;
+          c1 += a[7] * x2;
+          double c2 = a[2] * x0;
+          c2 += a[5] * x1;
+          c2 += a[8] * x2;
+          const int tgt = me + dx + dy * TX;
+          buf[nbp - lo][0][tgt] = c0;
+          buf[nbp - lo][1][tgt] = c1;
+          buf[nbp - lo][2][tgt] = c2;
+        }
+      }
+      __syncthreads();
+      if (active) {
+        if (ph == 0) {
+          // this plane's node: dz = 0 lower terms nb 9..12 (sources pushed nbp 17..14)
+#pragma unroll
+          for (int nb = 9; nb <= 12; nb++) {
+            const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1;
+            double c0, c1, c2;
+            term(nb, (26 - nb) - lo, in_tile(dx, dy), pc, uc, c0, c1, c2);
+            a0 += c0;
+            a1 += c1;
+            a2 += c2;
+          }
+        }
+        if (has_next) {
+          // next plane's node (pc + PXY): dz = -1 terms of this phase, nb = 26 - nbp for the
+          // phase's dz = +1 blocks, in the canonical order (8 | 4..7 | 0..3)
+          const int nb_lo = ph == 0 ? 8 : 26 - hi, nb_hi = 26 - max(lo, 18);
+#pragma unroll
+          for (int nb = 0; nb <= 8; nb++) {
+            if (nb < nb_lo || nb > nb_hi) continue;
+            const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1;
+            double c0, c1, c2;
+            term(nb, (26 - nb) - lo, in_tile(dx, dy), pc + PXY, uc + g.UXY, c0, c1, c2);
+            n0 += c0;
+            n1 += c1;
+            n2 += c2;
+          }
+        }
+      }
+      __syncthreads();
+    }
+    if (active) {
+      const double y0 = a0 + s0, y1 = a1 + s1, y2 = a2 + s2;
+      const int n = i + j * g.nx + k * g.nx * g.ny;
+      __builtin_nontemporal_store(y0, &y[3 * (int64_t)n + 0]);
+      __builtin_nontemporal_store(y1, &y[3 * (int64_t)n + 1]);
+      __builtin_nontemporal_store(y2, &y[3 * (int64_t)n + 2]);
+      if (DOT) dot += x0 * y0 + x1 * y1 + x2 * y2;
+    }
+    a0 = n0;
+    a1 = n1;
+    a2 = n2;
+  }
+  if (DOT) {
+    double s = block_sum<T>(dot, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+  }
+}
+
 static void z_shape(int kern, int& ztx, int& zty) {
   switch (kern) {
     case 2: ztx = 32; zty = 4; break;
@@ -948,8 +1180,25 @@ static void z_shape(int kern, int& ztx, int& zty) {
     case 4: ztx = 128; zty = 2; break;
     case 5: ztx = 128; zty = 4; break;
     case 6: ztx = 256; zty = 2; break;
+    case 7: ztx = 128; zty = 4; break;  // phased (k_spmv_symp) from here on
+    case 8: ztx = 64; zty = 4; break;
+    case 9: ztx = 64; zty = 8; break;
+    case 10: ztx = 256; zty = 2; break;
     default: ztx = 64; zty = 4; break;
   }
+}
+
+template <int ZTX, int ZTY>
+static void launch_symp(Ctx& c, const double* xpad, double* y, bool dot, bool gated, const ZTiling& zt, int nb) {
+  if (dot && gated)
+    hipLaunchKernelGGL((k_spmv_symp<true, true, ZTX, ZTY>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g, c.U, xpad, y,
+                       c.partials, c.cg, zt);
+  else if (dot)
+    hipLaunchKernelGGL((k_spmv_symp<true, false, ZTX, ZTY>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g, c.U, xpad, y,
+                       c.partials, c.cg, zt);
+  else
+    hipLaunchKernelGGL((k_spmv_symp<false, false, ZTX, ZTY>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g, c.U, xpad,
+                       y, c.partials, c.cg, zt);
 }
 
 template <int ZTX, int ZTY>
@@ -1004,6 +1253,13 @@ __global__ __launch_bounds__(TPB) void k_cg_init(Geo g, const double* __restrict
 }
 
 // p <- z (i == 0) or z + (beta/betaold) p   (VecCopy / VecAYPX)
+template <bool NT>
+__device__ __forceinline__ void st(double* p, double v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+template <bool NT>
 __global__ void k_cg_pupdate(Geo g, const double* __restrict__ z, double* __restrict__ ppad,
                              const CgState* __restrict__ cg) {
   if (cg->reason) return;
@@ -1014,15 +1270,16 @@ __global__ void k_cg_pupdate(Geo g, const double* __restrict__ z, double* __rest
   const int pc = pad_of(g, i, j, k);
   if (cg->i == 0) {
 #pragma unroll
-    for (int d = 0; d < 3; d++) ppad[3 * pc + d] = z[3 * n + d];
+    for (int d = 0; d < 3; d++) st<NT>(&ppad[3 * pc + d], z[3 * n + d]);
   } else {
     const double bc = cg->bcoef;
 #pragma unroll
-    for (int d = 0; d < 3; d++) ppad[3 * pc + d] = z[3 * n + d] + bc * ppad[3 * pc + d];
+    for (int d = 0; d < 3; d++) st<NT>(&ppad[3 * pc + d], z[3 * n + d] + bc * ppad[3 * pc + d]);
   }
 }
 
 // x += a p; r += (-a) w; z = D^-1 r; partials z.z, z.r
+template <bool NT>
 __global__ __launch_bounds__(TPB) void k_cg_update(Geo g, const double* __restrict__ ppad, const double* __restrict__ w,
                                                    const double* __restrict__ dinv, double* __restrict__ x,
                                                    double* __restrict__ r, double* __restrict__ z,
@@ -1040,11 +1297,11 @@ __global__ __launch_bounds__(TPB) void k_cg_update(Geo g, const double* __restri
 #pragma unroll
     for (int d = 0; d < 3; d++) {
       const int q = 3 * n + d;
-      x[q] = x[q] + a * ppad[3 * pc + d];
+      st<NT>(&x[q], x[q] + a * ppad[3 * pc + d]);
       const double rv = r[q] + ma * w[q];
-      r[q] = rv;
+      st<NT>(&r[q], rv);
       const double zv = rv * dinv[q];
-      z[q] = zv;
+      st<NT>(&z[q], zv);
       zz += zv * zv;
       zr += zv * rv;
     }
@@ -1157,12 +1414,34 @@ __global__ void k_cg_logic(const double* __restrict__ red, int mode, CgState* cg
 }
 
 // in-process all-reduce: out[v] = sum over ranks (rank order) of ptrs[r][v]
-__global__ void k_group_sum(const double* const* __restrict__ ptrs, int nranks, int count, double* __restrict__ out) {
+// in-process all-reduce over the group members' buffers, in rank order (op 0 sum, 1 max)
+__global__ void k_group_sum(const double* const* __restrict__ ptrs, int nranks, int count, double* __restrict__ out,
+                            int op) {
   int v = threadIdx.x;
   if (v >= count) return;
-  double s = 0.;
-  for (int r = 0; r < nranks; r++) s += ptrs[r][v];
+  double s = op ? ptrs[0][v] : 0.;
+  for (int r = op ? 1 : 0; r < nranks; r++) s = op ? fmax(s, ptrs[r][v]) : s + ptrs[r][v];
   out[v] = s;
+}
+
+// reaction-force post-processing (src/forces.c:82-91, :145-155): per element of one boundary
+// layer, the plain sum over its 8 Gauss points of stress component `comp`, in GP order.
+// The layer is global element index `fixed` along axis `fa`; (a, b) = the other two axes in
+// the reference's loop order (outer a over [a0, a0+na), inner b over [b0, b0+nb)).
+__global__ void k_force_layer(Geo g, const double* __restrict__ sig, int comp, int fa, int fixed, int a0, int na,
+                              int b0, int nb, double* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= na * nb) return;
+  const int ia = t / nb, ib = t % nb;
+  int e[3];
+  e[fa] = fixed;
+  e[fa == 0 ? 1 : 0] = a0 + ia;
+  e[2] = b0 + ib;
+  const int64_t le = (e[0] - g.ex0) + (int64_t)(e[1] - g.ey0) * g.nex + (int64_t)(e[2] - g.ez0) * g.nex * g.ney;
+  double s = 0.;
+#pragma unroll
+  for (int gp = 0; gp < 8; gp++) s += sig[((int64_t)comp * 8 + gp) * g.nelem + le];
+  out[t] = s;
 }
 
 // ---------------------------------------------------------------------------- misc vectors
@@ -1295,6 +1574,10 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
       case 4: launch_symz<128, 2>(c, xpad, y, dot, gated, zt, nb); break;
       case 5: launch_symz<128, 4>(c, xpad, y, dot, gated, zt, nb); break;
       case 6: launch_symz<256, 2>(c, xpad, y, dot, gated, zt, nb); break;
+      case 7: launch_symp<128, 4>(c, xpad, y, dot, gated, zt, nb); break;
+      case 8: launch_symp<64, 4>(c, xpad, y, dot, gated, zt, nb); break;
+      case 9: launch_symp<64, 8>(c, xpad, y, dot, gated, zt, nb); break;
+      case 10: launch_symp<256, 2>(c, xpad, y, dot, gated, zt, nb); break;
       default: launch_symz<64, 4>(c, xpad, y, dot, gated, zt, nb); break;
     }
     return;
@@ -1364,8 +1647,15 @@ void launch_unpack(Ctx& c, double* xpad) {
 
 // reduce partials into out (and, for RED_NORM, out[0] = sqrt); multi-rank: local sums are
 // all-reduced over RCCL first.
-void launch_group_sum(Ctx& c, const double* const* ptrs, int nranks, int count, double* out) {
-  hipLaunchKernelGGL(k_group_sum, dim3(1), dim3(64), 0, c.stream, ptrs, nranks, count, out);
+void launch_group_sum(Ctx& c, const double* const* ptrs, int nranks, int count, double* out, int op) {
+  hipLaunchKernelGGL(k_group_sum, dim3(1), dim3(64), 0, c.stream, ptrs, nranks, count, out, op);
+}
+
+void launch_force_layer(Ctx& c, int comp, int fa, int fixed, int a0, int na, int b0, int nb, double* out) {
+  const int n = na * nb;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_force_layer, dim3((n + TPB - 1) / TPB), dim3(TPB), 0, c.stream, c.g, c.sig, comp, fa, fixed,
+                     a0, na, b0, nb, out);
 }
 
 static int reduce_and_logic(Ctx& c, int nvals, int nparts, int mode, bool gated) {
@@ -1402,7 +1692,10 @@ int cg_finish_init(Ctx& c) {
 int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1) {
   const int nbn = (int)nblk(c.g.nown);
   const int nbs = (int)spmv_grid_blocks(c);
-  hipLaunchKernelGGL(k_cg_pupdate, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.cg);
+  if (c.cg_nt)
+    hipLaunchKernelGGL(k_cg_pupdate<true>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.cg);
+  else
+    hipLaunchKernelGGL(k_cg_pupdate<false>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.cg);
   int rc = halo_exchange(c, c.p_pad);
   if (rc) return rc;
   if (ev0) MCX_HIP(hipEventRecord(ev0, c.stream));
@@ -1410,7 +1703,11 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1) {
   if (ev1) MCX_HIP(hipEventRecord(ev1, c.stream));
   rc = reduce_and_logic(c, 1, nbs, RED_ALPHA, true);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_cg_update, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.p_pad, c.w, c.dinv, c.du, c.r, c.z,
+  if (c.cg_nt)
+    hipLaunchKernelGGL(k_cg_update<true>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.p_pad, c.w, c.dinv, c.du, c.r, c.z,
+                     c.partials, nbn, c.cg);
+  else
+    hipLaunchKernelGGL(k_cg_update<false>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.p_pad, c.w, c.dinv, c.du, c.r, c.z,
                      c.partials, nbn, c.cg);
   rc = reduce_and_logic(c, 2, nbn, RED_BETA, true);
   return rc;

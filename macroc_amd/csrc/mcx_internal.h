@@ -28,6 +28,7 @@ struct Geo {
   int xs, ys, zs;          // first owned node (global)
   int nx, ny, nz;          // owned node counts
   int PX, PY, PZ;          // padded box = owned + 1 ghost layer each side
+  int UX, UXY;             // sbaij storage pitch: rows of UX = roundup(nx+2, 64) nodes (u_of)
   int nown;                // nx*ny*nz
   int ex0, ey0, ez0;       // first element evaluated on this device (global)
   int nex, ney, nez;       // extended element counts (owned + upper ghost layer)
@@ -106,6 +107,7 @@ struct Ctx {
   int64_t nupper_local = 0;  // sbaij: stored upper values of the owned rows
   int spmv_subl = 0;         // SpMV sweep: lines per sub-slab of an XCD's slab (0 = whole slab, -1 = linear order)
   int spmv_kernel = 0;       // sbaij: 0 = pull, 1..4 = z-marching push/pull tiles (shapes, see z_shape)
+  int cg_nt = 0;             // CG vector kernels: non-temporal stores of x, r, z, p
   int spmv_zblocks = 1024;   // z-marching: target block count (sets the z-chunk length)
   int spmv_nt = 2;           // aij: 1 = non-temporal matrix loads, 2 = + non-temporal y stores (-3 %, spmv_ab)
   int64_t partials_cap = 0;
@@ -154,8 +156,10 @@ int comm_init(Ctx& c, const void* id);
 void comm_destroy(Ctx& c);
 int halo_exchange(Ctx& c, double* xpad);
 int allreduce_sum(Ctx& c, const double* in, double* out, int count);
+int allreduce_max(Ctx& c, const double* in, double* out, int count);
 int allreduce_prepare(Ctx& c);
-void launch_group_sum(Ctx& c, const double* const* ptrs, int nranks, int count, double* out);
+void launch_group_sum(Ctx& c, const double* const* ptrs, int nranks, int count, double* out, int op = 0);
+void launch_force_layer(Ctx& c, int comp, int fa, int fixed, int a0, int na, int b0, int nb, double* out);
 
 // ---- kernel launchers (kernels.hip)
 int upload_constants(Ctx& c);

@@ -3,10 +3,11 @@
  *
  * Mirrors the reference driver src/main.c:25-125: same flags (mcx_parse_args accepts the
  * options-DB names of src/init.c:66-83, -da_* and -ksp_*), same time loop and Newton loop
- * (:49-82), same log lines ("|RES| = ", "KSP : |Ax - b|/|Ax| = ... Its = ..."), info.dat rows
- * (:96-97; reaction force / f_trial / non-linear GP counts are post-processing, out of scope,
- * printed as 0) and the final "Elapsed time".  Multi-GPU runs go through bench.py (one
- * process per GPU over RCCL); this driver is the single-rank drop-in.
+ * (:49-82), same log lines ("|RES| = ", "KSP : |Ax - b|/|Ax| = ... Its = ..."), the history
+ * commit of :83, the per-time-step post-processing of :86-97 (non-linear GP count, reaction
+ * force, f_trial_max; info.dat row; gauss_evolution.dat row of src/util.c:77-84) and the final
+ * "Elapsed time".  Multi-GPU runs go through bench.py (one process per GPU over RCCL); this
+ * driver is the single-rank drop-in.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -34,6 +35,7 @@ int main(int argc, char** argv) {
   mcx_default_opts(&o);
   CHK(mcx_parse_args(&o, argc - 1, (const char* const*)argv + 1));
   FILE* file_out = fopen("info.dat", "w");
+  FILE* file_gps = fopen("gauss_evolution.dat", "w");  // src/init.c:135
   printf("\nMacroC : A HPC for FE2 Multi-scale Simulations\n\n");
   void* ctx = NULL;
   CHK(mcx_init(&o, 0, 1, NULL, &ctx));
@@ -76,7 +78,16 @@ int main(int argc, char** argv) {
       CHK(mcx_update_u(ctx));
       newton_it++;
     }
-    if (file_out) fprintf(file_out, "%d\t%e\t%e\t%e\t%e\t%d\n", time_s, time_s * o.dt, U, 0.0, 0.0, 0);
+    CHK(mcx_update_vars(ctx));  // micropp_C_update_vars(), src/main.c:83
+    int64_t nl_local = 0, nl = 0;
+    double f_trial_max = 0., force = 0.;
+    CHK(mcx_reduce_nonlinear(ctx, &nl_local, &nl, &f_trial_max));
+    if (file_gps) fprintf(file_gps, "%d\t%ld\t\n", time_s, (long)nl_local);
+    printf("Non-Linear Gauss points : %ld\n", (long)nl);
+    CHK(mcx_calc_force(ctx, &force));
+    printf("F_trial_max             : %e\n", f_trial_max);
+    if (file_out)
+      fprintf(file_out, "%d\t%e\t%e\t%e\t%e\t%d\n", time_s, time_s * o.dt, U, force, f_trial_max, (int)nl);
   }
   CHK(mcx_synchronize(ctx));
   double t2 = wtime();
@@ -86,5 +97,6 @@ int main(int argc, char** argv) {
          "------------------------------------------------------------\n");
   printf("Elapsed time : %f\n", t2 - t1);
   if (file_out) fclose(file_out);
+  if (file_gps) fclose(file_gps);
   return mcx_finalize(ctx);
 }

@@ -10,6 +10,8 @@ int main(int argc, char** argv) {
   orc_opts o;
   orc_default_opts(&o);
   const char* log = NULL;
+  const char* info = NULL;
+  const char* gauss = NULL;
   for (int a = 1; a < argc; a++) {
     const char* k = argv[a];
     const char* v = a + 1 < argc ? argv[a + 1] : "0";
@@ -23,13 +25,15 @@ int main(int argc, char** argv) {
     DBL("-newton_min_tol", newton_min_tol) DBL("-newton_rel_tol", newton_rel_tol)
     DBL("-ksp_rtol", rtol) DBL("-ksp_atol", abstol) DBL("-ksp_divtol", dtol) INT("-ksp_max_it", maxits)
     if (!strcmp(k, "-log")) { log = v; a++; continue; }
+    if (!strcmp(k, "-info")) { info = v; a++; continue; }
+    if (!strcmp(k, "-gauss")) { gauss = v; a++; continue; }
     INT("-mat_law", law)
     fprintf(stderr, "warning: unknown option %s ignored\n", k);
   }
   orc_problem* P = orc_create(&o);
   if (!P) { fprintf(stderr, "bad options / partition\n"); return 1; }
   double t = 0;
-  orc_run(P, log, &t);
+  orc_run_files(P, log, info, gauss, &t);
   printf("newton_solve_iter_s %.6f ndofs %lld\n", t, (long long)orc_ndofs(P));
   orc_destroy(P);
   return 0;

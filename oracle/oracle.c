@@ -766,6 +766,63 @@ int64_t orc_nonlinear_gps(const orc_problem* P, double* fmax) {
 
 double* orc_ctan(orc_problem* P) { return P->ctan; }
 
+/* micropp_C_get_non_linear_gps() of one emulated rank (its GP range), the per-rank column
+   of gauss_evolution.dat (src/util.c:69-87) */
+int64_t orc_rank_nonlinear_gps(const orc_problem* P, int r) {
+  int64_t n = 0;
+  for (int64_t g = P->gp_off[r]; g < P->gp_off[r] + P->ne[r] * NGP; g++) n += P->ftrial[g] > 0.;
+  return n;
+}
+
+/* calc_force src/forces.c:25-50: per rank calc_force_circle (:115-166) or calc_force_bending
+   (:58-106) over the rank's own elements and GP stresses, then MPI_Reduce(SUM) — emulated in
+   rank order.  Quirks kept: the circle test uses the GHOST corners si, sk, sj and the owned
+   ny (:130-133), so only ranks with no lower y ghost (ys == 0) that also reach NY contribute
+   (with more than one rank in y the force is 0); stress_ave is the plain sum over the 8 GPs
+   (:145-154). */
+double orc_calc_force(const orc_problem* P) {
+  double force = 0.0;
+  for (int r = 0; r < P->nranks; r++) {
+    int64_t c[12], lo[3], cnt[3];
+    orc_rank_corners(P, r, c);
+    rank_elem_range(P, r, lo, cnt);
+    const int64_t nex = cnt[0], ney = cnt[1], nez = cnt[2];
+    const double* sig = P->sig + P->gp_off[r] * NVOI;
+    double mpi_force = 0.0;
+    double stress_ave[NVOI];
+    if (P->o.bc_type == 0) { /* BC_BENDING */
+      if (c[0] + c[3] == P->o.NX) {
+        for (int64_t ey = 0; ey < ney; ++ey)
+          for (int64_t ez = 0; ez < nez; ++ez) {
+            const int64_t e = (nex - 1) + ey * nex + ez * (nex * ney);
+            memset(stress_ave, 0, sizeof(stress_ave));
+            for (int gp = 0; gp < NGP; ++gp)
+              for (int i = 0; i < NVOI; ++i) stress_ave[i] += sig[(e * NGP + gp) * NVOI + i];
+            mpi_force += stress_ave[3] * P->dy * P->dz;
+          }
+      }
+    } else { /* BC_CIRCLE */
+      const int64_t si = c[6], sj = c[7], sk = c[8];
+      if (sj + c[4] == P->o.NY) {
+        for (int64_t ex = 0; ex < nex; ++ex)
+          for (int64_t ez = 0; ez < nez; ++ez) {
+            const double x = P->o.lx / 2. - ((si + ex) * P->dx + P->dx / 2.);
+            const double z = P->o.lz / 2. - ((sk + ez) * P->dz + P->dz / 2.);
+            if ((x * x + z * z) < 1 * (P->o.rad * P->o.rad)) {
+              const int64_t e = ex + (ney - 1) * nex + ez * (nex * ney);
+              memset(stress_ave, 0, sizeof(stress_ave));
+              for (int gp = 0; gp < NGP; ++gp)
+                for (int i = 0; i < NVOI; ++i) stress_ave[i] += sig[(e * NGP + gp) * NVOI + i];
+              mpi_force += stress_ave[1] * P->dx * P->dz;
+            }
+          }
+      }
+    }
+    force += mpi_force;
+  }
+  return force;
+}
+
 /* assembly_res src/assembly.c:120-176 with DMLocalToGlobal(ADD) emulated as
    owned part first, then remote ghost contributions by source rank */
 void orc_assembly_res(orc_problem* P) {
@@ -1038,9 +1095,14 @@ static double now_s(void) {
   return t.tv_sec + 1e-9 * t.tv_nsec;
 }
 
-/* src/main.c:49-109 (post-processing of :83-108 is out of scope) */
-int orc_run(orc_problem* P, const char* log_path, double* t_newton_solve_s) {
+/* src/main.c:49-109 with the per-time-step post-processing of :86-97: non-linear GP counts
+   (gauss_evolution.dat, src/util.c:69-87), reaction force (src/forces.c:25-50), f_trial_max
+   (src/util.c:94-102) and the info.dat row (:96-97; the int64 count is printed with %d). */
+int orc_run_files(orc_problem* P, const char* log_path, const char* info_path, const char* gauss_path,
+                  double* t_newton_solve_s) {
   FILE* f = log_path ? fopen(log_path, "w") : NULL;
+  FILE* fi = info_path ? fopen(info_path, "w") : NULL;
+  FILE* fg = gauss_path ? fopen(gauss_path, "w") : NULL;
   double norm = 0., norm_0 = 0.;
   double t_first = -1.;
   for (int time_s = 0; time_s < P->o.ts; ++time_s) {
@@ -1068,10 +1130,30 @@ int orc_run(orc_problem* P, const char* log_path, double* t_newton_solve_s) {
       newton_it++;
     }
     orc_update_vars(P);
+    if (fg) fprintf(fg, "%d\t", time_s);
+    int64_t nl = 0;
+    for (int r = 0; r < P->nranks; r++) {
+      const int64_t q = orc_rank_nonlinear_gps(P, r);
+      if (fg) fprintf(fg, "%ld\t", (long)q);
+      nl += q;
+    }
+    if (fg) fprintf(fg, "\n");
+    if (f) fprintf(f, "Non-Linear Gauss points : %ld\n", (long)nl);
+    const double force = orc_calc_force(P);
+    double ftm = 0.;
+    orc_nonlinear_gps(P, &ftm);
+    if (f) fprintf(f, "F_trial_max             : %e\n", ftm);
+    if (fi) fprintf(fi, "%d\t%e\t%e\t%e\t%e\t%d\n", time_s, time_s * P->o.dt, U, force, ftm, (int)nl);
   }
   if (f) fclose(f);
+  if (fi) fclose(fi);
+  if (fg) fclose(fg);
   if (t_newton_solve_s) *t_newton_solve_s = t_first;
   return 0;
+}
+
+int orc_run(orc_problem* P, const char* log_path, double* t_newton_solve_s) {
+  return orc_run_files(P, log_path, NULL, NULL, t_newton_solve_s);
 }
 
 /* DMDA natural -> PETSc node numbering for any M,N,P >= 1 (used to pin the known answer of

@@ -139,6 +139,11 @@ double* orc_ctan(orc_problem* P);  /* [ngp][36] */
 /* full run of src/main.c:49-109; writes log lines to `log` (may be NULL).
    newton_out: per (time step, newton it) records: |RES|, ksp its, ksp rnorm (cap entries) */
 int orc_run(orc_problem* P, const char* log_path, double* t_newton_solve_s);
+int orc_run_files(orc_problem* P, const char* log_path, const char* info_path, const char* gauss_path,
+                  double* t_newton_solve_s);
+/* post-processing of src/main.c:86-97 */
+double orc_calc_force(const orc_problem* P);                 /* src/forces.c:25-166 */
+int64_t orc_rank_nonlinear_gps(const orc_problem* P, int r); /* src/util.c:69-87, one rank */
 int orc_set_threads(int n);
 
 #ifdef __cplusplus

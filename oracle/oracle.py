@@ -81,6 +81,11 @@ def lib():
         L.orc_dmda_decide.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int,
                                       C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.orc_run.argtypes = [P, C.c_char_p, d]
+        L.orc_run_files.argtypes = [P, C.c_char_p, C.c_char_p, C.c_char_p, d]
+        L.orc_calc_force.argtypes = [P]
+        L.orc_calc_force.restype = C.c_double
+        L.orc_rank_nonlinear_gps.argtypes = [P, C.c_int]
+        L.orc_rank_nonlinear_gps.restype = C.c_int64
         L.orc_nonlinear_gps.argtypes = [P, d]
         L.orc_nonlinear_gps.restype = C.c_int64
         L.orc_ctan.argtypes = [P]
@@ -285,10 +290,20 @@ class Problem:
     def update_u(self):
         lib().orc_update_u(self._p)
 
-    def run(self, log_path=None):
+    def run(self, log_path=None, info_path=None, gauss_path=None):
+        """src/main.c:49-109: time loop, Newton loop, post-processing rows (info.dat,
+        gauss_evolution.dat)."""
         t = np.zeros(1)
-        lib().orc_run(self._p, log_path.encode() if log_path else None, _dp(t))
+        enc = lambda s: s.encode() if s else None  # noqa: E731
+        lib().orc_run_files(self._p, enc(log_path), enc(info_path), enc(gauss_path), _dp(t))
         return float(t[0])
+
+    def calc_force(self):
+        """calc_force src/forces.c:25-166 (rank partials summed in rank order)."""
+        return lib().orc_calc_force(self._p)
+
+    def rank_nonlinear_gps(self, r):
+        return lib().orc_rank_nonlinear_gps(self._p, r)
 
     def newton_step1(self):
         """Time step 1, Newton iteration 0 of src/main.c (the path that solves).

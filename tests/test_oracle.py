@@ -83,3 +83,23 @@ def test_oracle_log_matches_reference_format(tmp_path):
     txt = log.read_text()
     assert "Time Step = 1" in txt and "|RES| = 1.029218e+06" in txt
     assert "KSP : |Ax - b|/|Ax| = " in txt and "Its = 39" in txt
+
+
+def test_oracle_force_and_info_rows(tmp_path):
+    """Post-processing restatement (src/main.c:86-97, src/forces.c:115-166): the reaction force
+    is a property of the field, so emulated rank grids with one rank in y agree to the solver
+    tolerance (their CG dot products differ in summation order);
+    the info.dat row has the reference's six tab-separated columns."""
+    forces = []
+    for nr in (1, 2, 4):
+        P = O.Problem(41, 5, 41, ts=2, rtol=1e-10, nranks=nr)
+        P.run(None, str(tmp_path / f"info{nr}.dat"), str(tmp_path / f"gauss{nr}.dat"))
+        forces.append(P.calc_force())
+        rows = (tmp_path / f"info{nr}.dat").read_text().splitlines()
+        assert len(rows) == 2 and all(len(r.split("\t")) == 6 for r in rows)
+        assert rows[1].split("\t")[:3] == ["1", "1.000000e-03", "-1.000000e-03"]
+        assert len((tmp_path / f"gauss{nr}.dat").read_text().splitlines()[0].split("\t")) == nr + 2
+        P.close()
+    assert forces[0] < 0.0
+    for f in forces[1:]:
+        assert abs(f - forces[0]) <= 1e-9 * abs(forces[0])
