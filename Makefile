@@ -3,7 +3,8 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 CXXFLAGS ?= -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=$(ARCH) -Wall -Wno-unused-function
-SRC = macroc_amd/csrc/api.cpp macroc_amd/csrc/dmda.cpp macroc_amd/csrc/comm.cpp macroc_amd/csrc/kernels.hip
+SRC = macroc_amd/csrc/api.cpp macroc_amd/csrc/dmda.cpp macroc_amd/csrc/comm.cpp macroc_amd/csrc/vtu.cpp \
+      macroc_amd/csrc/kernels.hip
 HDR = macroc_amd/csrc/mcx_internal.h include/macroc_amd.h
 LIB = macroc_amd/libmacroc_amd.so
 OBJ = $(patsubst macroc_amd/csrc/%,build/%.o,$(SRC))

@@ -67,7 +67,7 @@ typedef struct {
   double lx, ly, lz;           /* -lx -ly -lz             (50 1 50) */
   double dt, final_time;       /* -dt                     (0.001, FINAL_TIME 1.0) */
   int ts;                      /* -ts                     (1) */
-  int vtu_freq;                /* -vtu_freq               (-1; VTU output is out of scope) */
+  int vtu_freq;                /* -vtu_freq               (-1: no VTU output; mcx_write_vtu) */
   int bc_type;                 /* -bc_type                (BC_CIRCLE) */
   double rad;                  /* load-circle radius      (1.0, src/init.c:141) */
   int newton_max_its;          /* -newton_max_its         (5) */
@@ -171,6 +171,12 @@ int mcx_reduce_nonlinear(void* ctx, int64_t* n_local, int64_t* n_total, double* 
  * layer, sigma_xy * dy * dz; per rank in the reference's loop order and element set, then
  * summed over ranks.  Collective; every rank receives the total. */
 int mcx_calc_force(void* ctx, double* force);
+
+/* write_pvtu (src/output.c:25-267, called at src/main.c:100-108 every -vtu_freq time steps):
+ * "<prefix>.pvtu" (rank 0) + "<prefix>-subdo-<rank>.vtu" with the ghosted box points, the
+ * rank's elements, the ghosted displacement and cell data (part, cost = 0: no micro solver,
+ * non-linear GP count, wg-weighted GP sums of strain and stress).  Collective (u halo). */
+int mcx_write_vtu(void* ctx, const char* file_prefix);
 
 /* src/main.c:57-82 for one time step; returns Newton iterations done, per-iteration
    |RES|, KSP its and KSP rnorm in caller arrays of length >= newton_max_its (may be NULL) */

@@ -34,7 +34,7 @@ EXPORTS = [
     "mcx_local_group_create", "mcx_local_group_destroy", "mcx_init_local",
     "mcx_finalize", "mcx_get_info", "mcx_material_set", "mcx_get_displacement", "mcx_zero_u", "mcx_apply_bc_u",
     "mcx_set_strains", "mcx_homogenize", "mcx_assembly_res", "mcx_assembly_jac", "mcx_solve", "mcx_update_u", "mcx_update_vars",
-    "mcx_get_nonlinear_stats", "mcx_reduce_nonlinear", "mcx_calc_force",
+    "mcx_get_nonlinear_stats", "mcx_reduce_nonlinear", "mcx_calc_force", "mcx_write_vtu",
     "mcx_time_step", "mcx_get_u", "mcx_set_u", "mcx_get_b", "mcx_get_du", "mcx_get_strain", "mcx_get_stress",
     "mcx_owned_dofs", "mcx_dump_csr", "mcx_dump_dirichlet", "mcx_spmv", "mcx_get_ksp_history",
     "mcx_set_timing", "mcx_get_timing", "mcx_synchronize", "mcx_set_option", "mcx_time_spmv",
@@ -129,6 +129,7 @@ def lib():
     L.mcx_get_nonlinear_stats.argtypes = [vp, i64, d]
     L.mcx_reduce_nonlinear.argtypes = [vp, i64, i64, d]
     L.mcx_calc_force.argtypes = [vp, d]
+    L.mcx_write_vtu.argtypes = [vp, C.c_char_p]
     L.mcx_dump_csr.argtypes = [vp, i64, i64, d]
     L.mcx_dump_dirichlet.argtypes = [vp, i64, i64]
     L.mcx_spmv.argtypes = [vp, d, d]
@@ -303,6 +304,10 @@ class Macroc:
         nl, nt, f = C.c_int64(), C.c_int64(), C.c_double()
         _check(lib().mcx_reduce_nonlinear(self._ctx, C.byref(nl), C.byref(nt), C.byref(f)), "reduce_nonlinear")
         return nl.value, nt.value, f.value
+
+    def write_vtu(self, prefix):
+        """write_pvtu (src/output.c:25-267), collective."""
+        _check(lib().mcx_write_vtu(self._ctx, str(prefix).encode()), "write_vtu")
 
     def calc_force(self):
         """calc_force (src/forces.c:25-166), collective; every rank gets the total."""

@@ -218,6 +218,50 @@ __global__ void k_strains(Geo g, const double* __restrict__ u, double* __restric
   }
 }
 
+// VTU cell data (write_pvtu src/output.c:180-248) for the rank's own elements as PETSc lists
+// them ([lo, lo+cnt) per axis, x fastest): out[13 e + 0..5] = sum_gp wg * (B_gp u_e) recomputed
+// from u (:204-223, strain_gp summed like set_strains), [6..11] = sum_gp wg * sigma_gp
+// (:232-240), [12] = non-linear GPs (f_trial > 0, micropp_C_is_non_linear :197-201)
+__global__ void k_vtu_cells(Geo g, const double* __restrict__ u, const double* __restrict__ sig,
+                            const double* __restrict__ ftrial, int lx0, int ly0, int lz0, int cx, int cy, int cz,
+                            double* __restrict__ out) {
+  const int64_t e = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (e >= (int64_t)cx * cy * cz) return;
+  const int ex = lx0 + (int)(e % cx), ey = ly0 + (int)((e / cx) % cy), ez = lz0 + (int)(e / ((int64_t)cx * cy));
+  const int64_t le = (ex - g.ex0) + (int64_t)(ey - g.ey0) * g.nex + (int64_t)(ez - g.ez0) * g.nex * g.ney;
+  const int PXY = g.PX * g.PY;
+  const int p0 = (ex - g.xs + 1) + (ey - g.ys + 1) * g.PX + (ez - g.zs + 1) * PXY;
+  const int noff[8] = {0, 1, 1 + g.PX, g.PX, PXY, 1 + PXY, 1 + g.PX + PXY, g.PX + PXY};
+  double ue[24];
+#pragma unroll
+  for (int a = 0; a < 8; a++)
+#pragma unroll
+    for (int d = 0; d < 3; d++) ue[3 * a + d] = u[3 * (p0 + noff[a]) + d];
+  double strain[6] = {0., 0., 0., 0., 0., 0.}, stress[6] = {0., 0., 0., 0., 0., 0.};
+  int nl = 0;
+  for (int gp = 0; gp < 8; gp++) {
+#pragma unroll
+    for (int kk = 0; kk < 6; kk++) {
+      double s = 0.;
+#pragma unroll
+      for (int jj = 0; jj < 24; jj++) {
+        const int d = jj % 3;
+        const bool nz = (kk < 3) ? (d == kk) : (kk == 3 ? d != 2 : (kk == 4 ? d != 1 : d != 0));
+        if (nz) s += cB[gp][kk][jj] * ue[jj];
+      }
+      strain[kk] += s * g.wg;
+      stress[kk] += sig[((int64_t)kk * 8 + gp) * g.nelem + le] * g.wg;
+    }
+    if (ftrial && ftrial[(int64_t)gp * g.nelem + le] > 0.) nl++;
+  }
+#pragma unroll
+  for (int kk = 0; kk < 6; kk++) {
+    out[13 * e + kk] = strain[kk];
+    out[13 * e + 6 + kk] = stress[kk];
+  }
+  out[13 * e + 12] = nl;
+}
+
 // ---------------------------------------------------------------------------- material
 // Gauss-point callback, isotropic linear elastic (MicroPP surrogate): sigma = C eps,
 // ctan = C, per Gauss point (micropp_C_homogenize / get_stress3 / get_ctan3).
@@ -1649,6 +1693,13 @@ void launch_unpack(Ctx& c, double* xpad) {
 // all-reduced over RCCL first.
 void launch_group_sum(Ctx& c, const double* const* ptrs, int nranks, int count, double* out, int op) {
   hipLaunchKernelGGL(k_group_sum, dim3(1), dim3(64), 0, c.stream, ptrs, nranks, count, out, op);
+}
+
+void launch_vtu_cells(Ctx& c, const int* lo, const int* cnt, double* out) {
+  const int64_t n = (int64_t)cnt[0] * cnt[1] * cnt[2];
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_vtu_cells, dim3((unsigned)((n + TPB - 1) / TPB)), dim3(TPB), 0, c.stream, c.g, c.u_pad, c.sig,
+                     c.ftrial, lo[0], lo[1], lo[2], cnt[0], cnt[1], cnt[2], out);
 }
 
 void launch_force_layer(Ctx& c, int comp, int fa, int fixed, int a0, int na, int b0, int nb, double* out) {

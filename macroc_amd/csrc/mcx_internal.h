@@ -159,6 +159,7 @@ int allreduce_sum(Ctx& c, const double* in, double* out, int count);
 int allreduce_max(Ctx& c, const double* in, double* out, int count);
 int allreduce_prepare(Ctx& c);
 void launch_group_sum(Ctx& c, const double* const* ptrs, int nranks, int count, double* out, int op = 0);
+void launch_vtu_cells(Ctx& c, const int* lo, const int* cnt, double* out);
 void launch_force_layer(Ctx& c, int comp, int fa, int fixed, int a0, int na, int b0, int nb, double* out);
 
 // ---- kernel launchers (kernels.hip)

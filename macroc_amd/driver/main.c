@@ -88,6 +88,11 @@ int main(int argc, char** argv) {
     printf("F_trial_max             : %e\n", f_trial_max);
     if (file_out)
       fprintf(file_out, "%d\t%e\t%e\t%e\t%e\t%d\n", time_s, time_s * o.dt, U, force, f_trial_max, (int)nl);
+    if (o.vtu_freq > 0 && time_s % o.vtu_freq == 0) {  // src/main.c:100-108
+      char file_prefix[256];
+      snprintf(file_prefix, sizeof(file_prefix), "solution_%d", time_s);
+      CHK(mcx_write_vtu(ctx, file_prefix));
+    }
   }
   CHK(mcx_synchronize(ctx));
   double t2 = wtime();

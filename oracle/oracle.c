@@ -1095,6 +1095,125 @@ static double now_s(void) {
   return t.tv_sec + 1e-9 * t.tv_nsec;
 }
 
+/* write_pvtu src/output.c:25-267 for every emulated rank: "<prefix>.pvtu" + one
+   "<prefix>-subdo-<r>.vtu" piece per rank (ghosted box points, the rank's DMDAGetElements
+   elements, ghosted u, cell data).  micropp_C_get_sigma_cost3 (:180-187) has no counterpart
+   without a micro solver: cost = 0.  micropp_C_is_non_linear = f_trial > 0. */
+int orc_write_vtu(const orc_problem* P, const char* prefix) {
+  char name[1024];
+  snprintf(name, sizeof(name), "%s.pvtu", prefix);
+  FILE* fp = fopen(name, "w");
+  if (!fp) return 1;
+  fprintf(fp,
+          "<?xml version=\"1.0\"?>\n"
+          "<VTKFile type=\"PUnstructuredGrid\" version=\"0.1\" byte_order=\"LittleEndian\">\n"
+          "<PUnstructuredGrid GhostLevel=\"0\">\n"
+          "<PPoints>\n"
+          "  <PDataArray type=\"Float64\" Name=\"Position\"   NumberOfComponents=\"3\"/>\n"
+          "</PPoints>\n"
+          "<PCells>\n"
+          "  <PDataArray type=\"Int32\" Name=\"connectivity\" NumberOfComponents=\"1\"/>\n"
+          "  <PDataArray type=\"Int32\" Name=\"offsets\"      NumberOfComponents=\"1\"/>\n"
+          "  <PDataArray type=\"UInt8\" Name=\"types\"        NumberOfComponents=\"1\"/>\n"
+          "</PCells>\n"
+          "<PPointData Vectors=\"displ\">\n"
+          "  <PDataArray type=\"Float64\" Name=\"displ\"      NumberOfComponents=\"3\" />\n"
+          "</PPointData>\n"
+          "<PCellData>\n"
+          "  <PDataArray type=\"Int32\"   Name=\"part\"       NumberOfComponents=\"1\"/>\n"
+          "  <PDataArray type=\"Float64\" Name=\"cost\"       NumberOfComponents=\"1\"/>\n"
+          "  <PDataArray type=\"Int32\"   Name=\"non-linear\" NumberOfComponents=\"1\"/>\n"
+          "<PDataArray type=\"Float64\" Name=\"strain\"       NumberOfComponents=\"6\"/>\n"
+          "<PDataArray type=\"Float64\" Name=\"stress\"       NumberOfComponents=\"6\"/>\n"
+          "</PCellData>\n");
+  for (int r = 0; r < P->nranks; ++r) fprintf(fp, "  <Piece Source=\"%s-subdo-%d.vtu\"/>\n", prefix, r);
+  fprintf(fp, "</PUnstructuredGrid>\n</VTKFile>\n");
+  fclose(fp);
+  for (int r = 0; r < P->nranks; ++r) {
+    int64_t c[12];
+    orc_rank_corners(P, r, c);
+    const int64_t si = c[6], sj = c[7], sk = c[8], nx = c[9], ny = c[10], nz = c[11], N = nx * ny * nz;
+    const int64_t nelem = P->ne[r];
+    int32_t* eix = malloc((nelem * NPE + 1) * sizeof(int32_t));
+    orc_rank_elements(P, r, eix);
+    double* u_arr = malloc((N * DIM + 1) * sizeof(double));
+    for (int64_t l = 0; l < N; ++l)
+      for (int d = 0; d < DIM; ++d) u_arr[l * DIM + d] = P->u[ltog_node(P, c, l) * DIM + d];
+    snprintf(name, sizeof(name), "%s-subdo-%d.vtu", prefix, r);
+    fp = fopen(name, "w");
+    if (!fp) return 1;
+    fprintf(fp,
+            "<?xml version=\"1.0\"?>\n"
+            "<VTKFile type=\"UnstructuredGrid\" version=\"0.1\" byte_order=\"LittleEndian\">\n"
+            "<UnstructuredGrid>\n"
+            "<Piece NumberOfPoints=\"%d\" NumberOfCells=\"%d\">\n"
+            "<Points>\n",
+            (int)N, (int)nelem);
+    fprintf(fp, "<DataArray type=\"Float64\" Name=\"Position\" NumberOfComponents=\"3\" format=\"ascii\">\n");
+    for (int64_t k = sk; k < sk + nz; ++k)
+      for (int64_t j = sj; j < sj + ny; ++j)
+        for (int64_t i = si; i < si + nx; ++i) fprintf(fp, "%01.6e\t%01.6e\t%01.6e\n", i * P->dx, j * P->dy, k * P->dz);
+    fprintf(fp, "</DataArray>\n</Points>\n<Cells>\n");
+    fprintf(fp, "<DataArray type=\"Int32\" Name=\"connectivity\" NumberOfComponents=\"1\" format=\"ascii\">\n");
+    for (int64_t e = 0; e < nelem; ++e) {
+      for (int n = 0; n < NPE; ++n) fprintf(fp, "%-6d\t", eix[e * NPE + n]);
+      fprintf(fp, "\n");
+    }
+    fprintf(fp, "</DataArray>\n");
+    fprintf(fp, "<DataArray type=\"Int32\" Name=\"offsets\" NumberOfComponents=\"1\" format=\"ascii\">\n");
+    for (int64_t e = 1; e < nelem + 1; ++e) fprintf(fp, "%d\t", (int)(e * NPE));
+    fprintf(fp, "\n</DataArray>\n");
+    fprintf(fp, "<DataArray type=\"UInt8\"  Name=\"types\" NumberOfComponents=\"1\" format=\"ascii\">\n");
+    for (int64_t e = 0; e < nelem; ++e) fprintf(fp, "12\t");
+    fprintf(fp, "\n</DataArray>\n</Cells>\n<PointData Vectors=\"displ\">\n");
+    fprintf(fp, "<DataArray type=\"Float64\" Name=\"displ\" NumberOfComponents=\"3\" format=\"ascii\" >\n");
+    for (int64_t n = 0; n < N; ++n)
+      fprintf(fp, "%01.6e\t%01.6e\t%01.6e\n", u_arr[n * DIM + 0], u_arr[n * DIM + 1], u_arr[n * DIM + 2]);
+    fprintf(fp, "</DataArray>\n</PointData>\n<CellData>\n");
+    fprintf(fp, "<DataArray type=\"Int32\" Name=\"part\" NumberOfComponents=\"1\" format=\"ascii\">\n");
+    for (int64_t e = 0; e < nelem; ++e) fprintf(fp, "%d\t", r);
+    fprintf(fp, "\n</DataArray>\n");
+    fprintf(fp, "<DataArray type=\"Float64\" Name=\"cost\" NumberOfComponents=\"1\" format=\"ascii\">\n");
+    for (int64_t e = 0; e < nelem; ++e) fprintf(fp, "%lf\t", 0. / NGP);
+    fprintf(fp, "\n</DataArray>\n");
+    fprintf(fp, "<DataArray type=\"Int32\" Name=\"non-linear\" NumberOfComponents=\"1\" format=\"ascii\">\n");
+    const double* ft = P->ftrial + P->gp_off[r];
+    for (int64_t e = 0; e < nelem; ++e) {
+      int non_linear = 0;
+      for (int gp = 0; gp < NGP; ++gp) non_linear += ft[e * NPE + gp] > 0.;
+      fprintf(fp, "%d\t", non_linear);
+    }
+    fprintf(fp, "\n</DataArray>\n");
+    fprintf(fp, "<DataArray type=\"Float64\" Name=\"strain\" NumberOfComponents=\"6\" format=\"ascii\">");
+    for (int64_t e = 0; e < nelem; ++e) {
+      double u_e[NPE * DIM], strain[NVOI] = {0.}, strain_gp[NVOI];
+      for (int n = 0; n < NPE; ++n)
+        for (int i = 0; i < DIM; ++i) u_e[n * DIM + i] = u_arr[eix[e * NPE + n] * DIM + i];
+      for (int gp = 0; gp < NGP; ++gp) {
+        memset(strain_gp, 0, sizeof(strain_gp));
+        for (int i = 0; i < NVOI; ++i)
+          for (int j = 0; j < NPE * DIM; ++j) strain_gp[i] += P->Btab[gp][i][j] * u_e[j];
+        for (int i = 0; i < NVOI; ++i) strain[i] += strain_gp[i] * P->wg;
+      }
+      for (int i = 0; i < NVOI; ++i) fprintf(fp, "%e\t", strain[i]);
+    }
+    fprintf(fp, "\n</DataArray>\n");
+    fprintf(fp, "<DataArray type=\"Float64\" Name=\"stress\" NumberOfComponents=\"6\" format=\"ascii\">");
+    const double* sg = P->sig + P->gp_off[r] * NVOI;
+    for (int64_t e = 0; e < nelem; ++e) {
+      double stress[NVOI] = {0.};
+      for (int gp = 0; gp < NGP; ++gp)
+        for (int i = 0; i < NVOI; ++i) stress[i] += sg[(e * NPE + gp) * NVOI + i] * P->wg;
+      for (int i = 0; i < NVOI; ++i) fprintf(fp, "%e\t", stress[i]);
+    }
+    fprintf(fp, "\n</DataArray>\n</CellData>\n</Piece>\n</UnstructuredGrid>\n</VTKFile>\n");
+    fclose(fp);
+    free(eix);
+    free(u_arr);
+  }
+  return 0;
+}
+
 /* src/main.c:49-109 with the per-time-step post-processing of :86-97: non-linear GP counts
    (gauss_evolution.dat, src/util.c:69-87), reaction force (src/forces.c:25-50), f_trial_max
    (src/util.c:94-102) and the info.dat row (:96-97; the int64 count is printed with %d). */

@@ -143,6 +143,7 @@ int orc_run_files(orc_problem* P, const char* log_path, const char* info_path, c
                   double* t_newton_solve_s);
 /* post-processing of src/main.c:86-97 */
 double orc_calc_force(const orc_problem* P);                 /* src/forces.c:25-166 */
+int orc_write_vtu(const orc_problem* P, const char* prefix); /* src/output.c:25-267 */
 int64_t orc_rank_nonlinear_gps(const orc_problem* P, int r); /* src/util.c:69-87, one rank */
 int orc_set_threads(int n);
 

@@ -82,6 +82,7 @@ def lib():
                                       C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
         L.orc_run.argtypes = [P, C.c_char_p, d]
         L.orc_run_files.argtypes = [P, C.c_char_p, C.c_char_p, C.c_char_p, d]
+        L.orc_write_vtu.argtypes = [P, C.c_char_p]
         L.orc_calc_force.argtypes = [P]
         L.orc_calc_force.restype = C.c_double
         L.orc_rank_nonlinear_gps.argtypes = [P, C.c_int]
@@ -301,6 +302,10 @@ class Problem:
     def calc_force(self):
         """calc_force src/forces.c:25-166 (rank partials summed in rank order)."""
         return lib().orc_calc_force(self._p)
+
+    def write_vtu(self, prefix):
+        """write_pvtu src/output.c:25-267 for every emulated rank."""
+        assert lib().orc_write_vtu(self._p, str(prefix).encode()) == 0
 
     def rank_nonlinear_gps(self, r):
         return lib().orc_rank_nonlinear_gps(self._p, r)
