@@ -83,6 +83,9 @@ typedef struct {
   int mat_type;                /* -dm_mat_type aij|sbaij  (MCX_MAT_AIJ) */
   int mat_law;                 /* -mat_law elastic|plastic (MCX_LAW_ELASTIC; plastic = J2 with
                                   micro_mat_1's Sy, Ka: MicroPP material type 1) */
+  int mat_aij_split;           /* -mat_aij_split 0|1 (1): hold the AIJ matrix exactly as upper blocks +
+                                  bf16 lower corrections when all are exact (else plain AIJ blocks);
+                                  0: AIJ blocks, rows summed in the CPU AIJ order (bit-exact SpMV) */
 } mcx_opts;
 
 typedef struct {
@@ -101,6 +104,9 @@ typedef struct {
   double dx, dy, dz, wg;        /* src/init.c:137-140 */
   int64_t device_bytes;         /* device memory held by the context */
   int device;
+  int storage;                  /* matrix as last assembled: 0 AIJ blocks, 1 SBAIJ upper blocks,
+                                   2 AIJ-split (upper blocks + bf16 lower corrections) */
+  int split_slots;              /* AIJ-split: correction slots stored per node (of 117) */
 } mcx_info;
 
 typedef struct {

@@ -53,6 +53,7 @@ class Opts(C.Structure):
         ("ksp_max_it", C.c_int), ("micro_n", C.c_int), ("micro_type", C.c_int),
         ("micro_mat_1", C.c_double * 4), ("micro_mat_2", C.c_double * 4),
         ("device", C.c_int), ("ksp_monitor", C.c_int), ("mat_type", C.c_int), ("mat_law", C.c_int),
+        ("mat_aij_split", C.c_int),
     ]
 
 
@@ -65,7 +66,7 @@ class Info(C.Structure):
         ("ndofs_global", C.c_int64), ("ndofs_local", C.c_int64), ("dof_offset", C.c_int64),
         ("nnz_local", C.c_int64), ("nnz_global", C.c_int64), ("nelem_local", C.c_int64), ("nelem_ext", C.c_int64),
         ("dx", C.c_double), ("dy", C.c_double), ("dz", C.c_double), ("wg", C.c_double),
-        ("device_bytes", C.c_int64), ("device", C.c_int),
+        ("device_bytes", C.c_int64), ("device", C.c_int), ("storage", C.c_int), ("split_slots", C.c_int),
     ]
 
     def as_dict(self):
@@ -291,6 +292,12 @@ class Macroc:
 
     def update_vars(self):
         _check(lib().mcx_update_vars(self._ctx), "micropp_C_update_vars")
+
+    def get_info(self):
+        """mcx_get_info now (storage reflects the last assembly)."""
+        inf = Info()
+        _check(lib().mcx_get_info(self._ctx, C.byref(inf)), "mcx_get_info")
+        return inf.as_dict()
 
     def nonlinear_stats(self):
         """micropp_C_get_non_linear_gps / get_f_trial_max of this rank."""

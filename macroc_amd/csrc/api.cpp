@@ -53,7 +53,7 @@ static int free_ctx(Ctx* c) {
   if (!c) return 0;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->V, c->U, c->eps, c->sig, c->ctan,
+  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->V, c->U, c->D, c->d_mask, c->eps, c->sig, c->ctan,
                   c->Ke, c->be, c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf};
   for (void* p : ptrs)
@@ -72,13 +72,16 @@ static int free_ctx(Ctx* c) {
 
 // largest SpMV grid over the selectable kernels (mcx_set_option may switch between them)
 static int64_t max_spmv_blocks(Ctx& c) {
-  const int keep = c.spmv_kernel;
+  const int keep = c.spmv_kernel, keep_fmt = c.fmt;
   int64_t m = 0;
-  for (int k = 0; k <= 10; k++) {
-    c.spmv_kernel = k;
-    m = std::max(m, spmv_grid_blocks(c));
-  }
+  for (int f : {FMT_V, FMT_U, FMT_SPLIT})
+    for (int k = 0; k <= 10; k++) {
+      c.fmt = f;
+      c.spmv_kernel = k;
+      m = std::max(m, spmv_grid_blocks(c));
+    }
   c.spmv_kernel = keep;
+  c.fmt = keep_fmt;
   return m;
 }
 
@@ -99,11 +102,13 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   if (rc) return rc;
   int ncu = 0;
   MCX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c.device));
+  // z-marching tiles (sbaij and AIJ-split): one resident round of blocks (two per CU), 128-wide
+  // tiles where the subdomain is wide enough — tools/spmv_ab.py sweeps, DESIGN.md §4
+  c.spmv_zblocks = 2 * std::max(ncu, 1);
+  c.aij_split = o->mat_type == MCX_MAT_AIJ && o->mat_aij_split;
   if (o->mat_type == MCX_MAT_SBAIJ) {
-    // z-marching tiles: 128x2 where the subdomain is wide enough, one resident round of
-    // blocks (two 80 KB-LDS blocks per CU) — tools/spmv_ab.py sweep, DESIGN.md §6
     c.spmv_kernel = c.g.nx >= 128 ? 4 : 1;
-    c.spmv_zblocks = 2 * std::max(ncu, 1);
+    c.fmt = FMT_U;
   }
   MCX_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
   MCX_HIP(hipEventCreate(&c.ev_a));
@@ -119,6 +124,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
       (rc = dalloc(c, &c.w, nown3)) || (rc = dalloc(c, &c.dinv, nown3)) || (rc = dalloc(c, &c.tmp, nown3)) ||
       (c.o.mat_type == MCX_MAT_SBAIJ ? (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))
                                      : (rc = dalloc(c, &c.V, c.ngroups * NPAIR * 128))) ||
+      (c.aij_split && (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))) ||
       (rc = dalloc(c, &c.eps, 6 * 8 * E)) ||
       (rc = dalloc(c, &c.sig, 6 * 8 * E)) || (rc = dalloc(c, &c.ctan, 36 * 8 * E)) ||
       (rc = dalloc(c, &c.Ke, (int64_t)NKE * E)) || (rc = dalloc(c, &c.be, 24 * E)) ||
@@ -130,6 +136,11 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
       ((rc = dalloc(c, &c.hist_old, 7 * 8 * E)) || (rc = dalloc(c, &c.hist_new, 7 * 8 * E)) ||
        (rc = dalloc(c, &c.ftrial, 8 * E))))
     return rc;
+  if (c.aij_split) {
+    MCX_HIP(hipMalloc(&c.D, sizeof(uint16_t) * 8 * 15 * 64 * c.ngroups));
+    MCX_HIP(hipMalloc(&c.d_mask, 16 * sizeof(unsigned)));
+    c.device_bytes += sizeof(uint16_t) * 8 * 15 * 64 * c.ngroups;
+  }
   MCX_HIP(hipHostMalloc((void**)&c.h_cg, sizeof(CgState) * 2, hipHostMallocDefault));
   std::memset(c.h_cg, 0, sizeof(CgState) * 2);
   c.mat.law = o->mat_law;
@@ -267,6 +278,7 @@ void mcx_default_opts(mcx_opts* o) {
   std::memcpy(o->micro_mat_1, mat, sizeof(mat));
   std::memcpy(o->micro_mat_2, mat, sizeof(mat));
   o->device = -1;
+  o->mat_aij_split = 1;
 }
 
 int mcx_parse_args(mcx_opts* o, int argc, const char* const* argv) {
@@ -308,7 +320,8 @@ int mcx_parse_args(mcx_opts* o, int argc, const char* const* argv) {
         D("-newton_min_tol", &o->newton_min_tol) || D("-newton_rel_tol", &o->newton_rel_tol) ||
         D("-ksp_rtol", &o->ksp_rtol) || D("-ksp_atol", &o->ksp_abstol) || D("-ksp_divtol", &o->ksp_dtol) ||
         I("-ksp_max_it", &o->ksp_max_it) || I("-micro_n", &o->micro_n) || I("-micro_type", &o->micro_type) ||
-        A4("-micro_mat_1", o->micro_mat_1) || A4("-micro_mat_2", o->micro_mat_2) || I("-device", &o->device))
+        A4("-micro_mat_1", o->micro_mat_1) || A4("-micro_mat_2", o->micro_mat_2) || I("-device", &o->device) ||
+        I("-mat_aij_split", &o->mat_aij_split))
       continue;
     if (!std::strcmp(k, "-dm_mat_type")) {
       if (!v || (std::strcmp(v, "aij") && std::strcmp(v, "sbaij"))) {
@@ -436,6 +449,8 @@ static void fill_info(const Ctx& c, mcx_info* in) {
   in->wg = g.wg;
   in->device_bytes = c.device_bytes;
   in->device = c.device;
+  in->storage = c.fmt;
+  in->split_slots = c.fmt == FMT_SPLIT ? c.dsl.L : 0;
 }
 
 
@@ -577,8 +592,20 @@ int mcx_assembly_jac(void* ctx) {
   CTX(ctx);
   PhaseTimer t(c, &c.t.jacobian_ms);
   launch_element_ke(c);
-  if (c.U) launch_gather_matrix_sym(c);
-  else launch_gather_matrix(c);
+  if (c.o.mat_type == MCX_MAT_SBAIJ) {
+    launch_gather_matrix_sym(c);
+    c.fmt = FMT_U;
+  } else if (c.aij_split) {
+    launch_gather_matrix_sym(c);
+    bool exact = false;
+    int rc = build_split(c, &exact);
+    if (rc) return rc;
+    c.fmt = exact ? FMT_SPLIT : FMT_V;
+    if (!exact) launch_gather_matrix(c);  // a correction is not exact in bf16: plain AIJ blocks
+  } else {
+    launch_gather_matrix(c);
+    c.fmt = FMT_V;
+  }
   MCX_HIP(hipGetLastError());
   return 0;
 }
@@ -851,12 +878,31 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
   GUARD(ctx);
   CTX(ctx);
   const Geo& g = c.g;
+  const bool up = c.fmt != FMT_V;  // FMT_U / FMT_SPLIT: values from the upper blocks
   std::vector<double> V;
+  std::vector<uint16_t> Dh;
   if (vals) {
-    V.resize(c.U ? c.npgroups * UPAIR * 128 : c.ngroups * NPAIR * 128);
-    MCX_HIP(hipMemcpyAsync(V.data(), c.U ? c.U : c.V, sizeof(double) * V.size(), hipMemcpyDeviceToHost, c.stream));
+    V.resize(up ? c.npgroups * UPAIR * 128 : c.ngroups * NPAIR * 128);
+    MCX_HIP(hipMemcpyAsync(V.data(), up ? c.U : c.V, sizeof(double) * V.size(), hipMemcpyDeviceToHost, c.stream));
+    if (c.fmt == FMT_SPLIT && c.dsl.Lq) {
+      Dh.resize((size_t)c.ngroups * c.dsl.Lq * 64 * 8);
+      MCX_HIP(hipMemcpyAsync(Dh.data(), c.D, sizeof(uint16_t) * Dh.size(), hipMemcpyDeviceToHost, c.stream));
+    }
     MCX_HIP(hipStreamSynchronize(c.stream));
   }
+  // AIJ-split: packed position of each correction slot (-1: no correction stored)
+  int dpos[117];
+  for (int s = 0; s < 117; s++) dpos[s] = -1;
+  for (int p = 0; p < c.dsl.L; p++) dpos[c.dsl.s[p]] = p;
+  auto corr = [&](int64_t n, int s) -> double {
+    const int p = dpos[s];
+    if (p < 0) return 0.;
+    const uint16_t b = Dh[(((n >> 6) * c.dsl.Lq + (p >> 3)) * 64 + (n & 63)) * 8 + (p & 7)];
+    uint32_t f = (uint32_t)b << 16;
+    float fv;
+    std::memcpy(&fv, &f, 4);
+    return (double)fv;
+  };
   auto uval = [&](int64_t p, int s) { return V[(p >> 6) * (UPAIR * 128) + (int64_t)(s >> 1) * 128 + 2 * (p & 63) + (s & 1)]; };
   int64_t pos = 0;
   if (rowptr) rowptr[0] = 0;
@@ -872,12 +918,15 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
         int64_t col0 = 3 * petsc_node(c, hi, hj, hk);
         for (int cc = 0; cc < 3; cc++) {
           double v = 0.;
-          if (vals && c.U) {
+          if (vals && up) {
             // storage index u_of (kernels.hip): 64-aligned rows of UX nodes
             const int64_t pc = 64 + i + (j + 1) * (int64_t)g.UX + (k + 1) * (int64_t)g.UXY;
             const int64_t q = pc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * (int64_t)g.UX + (nb / 9 - 1) * (int64_t)g.UXY;
             static const int dsl[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
-            if (nb < 13) v = uval(q, 6 + 9 * (12 - nb) + cc * 3 + r);
+            if (nb < 13) {
+              v = uval(q, 6 + 9 * (12 - nb) + cc * 3 + r);
+              if (c.fmt == FMT_SPLIT) v = v + corr(n, nb * 9 + r * 3 + cc);  // exact AIJ lower value
+            }
             else if (nb == 13) v = uval(pc, dsl[r][cc]);
             else v = uval(pc, 6 + 9 * (nb - 14) + r * 3 + cc);
           } else if (vals) {
@@ -960,7 +1009,8 @@ int mcx_get_timing(void* ctx, mcx_timing* t) {
   *t = c.t;
   // algorithmic bytes of one SpMV in this format: the stencil-block values actually present
   // (AIJ nonzeros of the owned rows x 8 B), x read once, y written once
-  t->spmv_bytes_per_launch = (c.U ? c.nupper_local : c.nnz_local) * 8 + 2 * 3 * (int64_t)c.g.nown * 8;
+  t->spmv_bytes_per_launch = (c.fmt == FMT_V ? c.nnz_local : c.nupper_local) * 8 + 2 * 3 * (int64_t)c.g.nown * 8;
+  if (c.fmt == FMT_SPLIT) t->spmv_bytes_per_launch += (int64_t)c.g.nown * c.dsl.Lq * 16;
   return 0;
 }
 
@@ -981,6 +1031,18 @@ int mcx_set_option(void* ctx, const char* name, double value) {
       set_error("spmv_zblocks: partials buffer too small");
       return 2;
     }
+    return 0;
+  }
+  if (!std::strcmp(name, "spmv_nt_u")) {
+    c.g.nt_u = (int)value;
+    return 0;
+  }
+  if (!std::strcmp(name, "aij_split")) {  // takes effect at the next mcx_assembly_jac
+    if (value != 0. && !c.D) {
+      set_error("aij_split: context created with -mat_aij_split 0 (no split storage)");
+      return 2;
+    }
+    c.aij_split = value != 0.;
     return 0;
   }
   if (!std::strcmp(name, "cg_nt")) {

@@ -603,6 +603,64 @@ __global__ __launch_bounds__(TPB) void k_gather_matrix_sym(Geo g, const double* 
   }
 }
 
+// AIJ-split assembly, pass 1: thread = (owned node n, lower block nb < 13).  The AIJ value
+// A(n,nb)[r][c] (matrix_block, exactly what k_gather_matrix stores) minus the mirrored upper
+// value U(m, 26-nb)[c][r] of the neighbour m, as bf16 bits in S[(nb*9 + r*3 + c) * nown + n].
+// A correction is usable only if it is exact in bf16 and mirror + bf16 == A bit for bit;
+// d_mask[nb] collects the slots that are non-zero anywhere, d_mask[13] any inexact one.
+__global__ __launch_bounds__(TPB) void k_split_deltas(Geo g, const double* __restrict__ Ke,
+                                                      const double* __restrict__ U, uint16_t* __restrict__ S,
+                                                      unsigned* __restrict__ mask) {
+  __shared__ unsigned s_bits, s_bad;
+  if (threadIdx.x == 0) s_bits = s_bad = 0;
+  __syncthreads();
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  const int nb = blockIdx.y;
+  if (n < g.nown) {
+    int i, j, k;
+    node_ijk(g, n, i, j, k);
+    const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
+    double low[9];
+    matrix_block(g, Ke, g.xs + i, g.ys + j, g.zs + k, dx, dy, dz, low);
+    const int um = u_of(g, i + dx, j + dy, k + dz);
+    const double* Um = U + (int64_t)(um >> 6) * (UPAIR * 128) + 2 * (um & 63);
+    const int base = 6 + 9 * (12 - nb);
+    unsigned bits = 0, bad = 0;
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        const int s = base + c * 3 + r;
+        const double mir = Um[(s >> 1) * 128 + (s & 1)];
+        const double d = low[r * 3 + c] - mir;
+        const unsigned fb = __float_as_uint((float)d) & 0xffff0000u;
+        const double db = (double)__uint_as_float(fb);
+        if (db != d || mir + db != low[r * 3 + c]) bad = 1;
+        if (d != 0.) bits |= 1u << (r * 3 + c);
+        S[(int64_t)(nb * 9 + r * 3 + c) * g.nown + n] = (uint16_t)(fb >> 16);
+      }
+    if (bits) atomicOr(&s_bits, bits);
+    if (bad) atomicOr(&s_bad, 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (s_bits) atomicOr(&mask[nb], s_bits);
+    if (s_bad) atomicOr(&mask[13], 1u);
+  }
+}
+
+// AIJ-split assembly, pass 2: pack the active slots of every owned node, 8 bf16 per 16 B,
+// D[((n/64) * Lq + p/8) * 64 + n%64] quad, element p%8
+__global__ __launch_bounds__(TPB) void k_split_pack(Geo g, const uint16_t* __restrict__ S, uint16_t* __restrict__ D,
+                                                    DSlots dl) {
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  for (int p = 0; p < dl.Lq * 8; p++) {
+    const uint16_t v = p < dl.L ? S[(int64_t)dl.s[p] * g.nown + n] : (uint16_t)0;
+    D[(((int64_t)(n >> 6) * dl.Lq + (p >> 3)) * 64 + (n & 63)) * 8 + (p & 7)] = v;
+  }
+}
+
 // PCSetUp_Jacobi: diag, VecReciprocal (non-zeros only), zeros -> 1
 __global__ void k_jacobi(Geo g, const double* __restrict__ V, double* __restrict__ dinv) {
   int n = blockIdx.x * TPB + threadIdx.x;
@@ -1031,11 +1089,25 @@ __global__ __launch_bounds__(ZTX * ZTY, (ZTX * ZTY >= 512 ? 1 : 2)) void k_spmv_
 // LDS or is pulled by the target, and it is added at the same position):
 //   lower dz=-1: nb 8 | 4 5 6 7 | 0 1 2 3,  lower dz=0: nb 9 10 11 12,  then the upper sum
 //   (diagonal block, nbp 14..26 ascending).
-template <bool DOT, bool GATED, int TX, int TY>
+// AIJ-split lower corrections: per owned node the 117 lower-block values minus their mirrored
+// upper values, exact in bf16, as 15 x 16-B quads [node/64][15][node%64] (slot nb*9 + r*3 + c)
+constexpr int DQUAD = 15;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double bf16_slot(const u32x4 (&q)[DQUAD], int t) {
+  const u32x4 w = q[t >> 3];
+  const int h = (t >> 1) & 3;
+  const unsigned v = w[h];
+  const unsigned b = (t & 1) ? (v & 0xffff0000u) : (v << 16);
+  return (double)__uint_as_float(b);
+}
+
+template <bool DOT, bool GATED, int TX, int TY, bool AIJS = false>
 __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* __restrict__ U,
                                                         const double* __restrict__ x, double* __restrict__ y,
                                                         double* __restrict__ part, const CgState* __restrict__ cg,
-                                                        ZTiling zt) {
+                                                        ZTiling zt, const uint16_t* __restrict__ Dq = nullptr,
+                                                        DSlots dl = DSlots()) {
   constexpr int T = TX * TY;
   __shared__ double buf[5][3][T];
   __shared__ double sh[T / 64];
@@ -1080,7 +1152,11 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
       c2 = buf[slot][2][me];
     } else {
       const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
-      ut_x2(U, x, ucn + dx + dy * g.UX + dz * g.UXY, pcn + dx + dy * PX + dz * PXY, 26 - nb, c0, c1, c2);
+      if (g.nt_u & 2) {
+        c0 = c1 = c2 = 0.;
+      } else {
+        ut_x2(U, x, ucn + dx + dy * g.UX + dz * g.UXY, pcn + dx + dy * PX + dz * PXY, 26 - nb, c0, c1, c2);
+      }
     }
   };
   for (int k = k0; k < k1; k++) {
@@ -1114,7 +1190,14 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
         // slot s of this node = half (s & 1) of 16-B pair s >> 1; pairs shared by adjacent
         // blocks are the same load (read-only, merged by the compiler)
         auto sl = [&](int s) {
-          const double2 w = Ug[(s >> 1) * 64];
+          const double2* pp = Ug + (s >> 1) * 64;
+          double2 w;
+          if (g.nt_u & 1) {
+            w.x = __builtin_nontemporal_load(&pp->x);
+            w.y = __builtin_nontemporal_load(&pp->y);
+          } else {
+            w = *pp;
+          }
           return (s & 1) ? w.y : w.x;
         };
         if (ph == 0) {
@@ -1136,7 +1219,7 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
           double a[9];
 #pragma unroll
           for (int t = 0; t < 9; t++) a[t] = sl(base + t);
-          const int q = pc + dx + dy * PX + dz * PXY;
+          const int q = (g.nt_u & 4) ? pc : pc + dx + dy * PX + dz * PXY;
           const double z0 = x[3 * (int64_t)q], z1 = x[3 * (int64_t)q + 1], z2 = x[3 * (int64_t)q + 2];
           double u0 = a[0] * z0;
           u0 += a[1] * z1;
@@ -1200,8 +1283,35 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
       __syncthreads();
     }
     if (active) {
-      const double y0 = a0 + s0, y1 = a1 + s1, y2 = a2 + s2;
       const int n = i + j * g.nx + k * g.nx * g.ny;
+      if constexpr (AIJS) {
+        // exact AIJ lower blocks = mirrored upper (summed above) + the bf16 corrections of the
+        // active slots, ascending (nb, c) per row
+        const u32x4* Dn = reinterpret_cast<const u32x4*>(Dq) + (int64_t)(n >> 6) * (dl.Lq * 64) + (n & 63);
+        double d0 = 0., d1 = 0., d2 = 0.;
+#pragma unroll
+        for (int t = 0; t < DQUAD; t++) {
+          if (t >= dl.Lq) break;
+          const u32x4 w = __builtin_nontemporal_load(Dn + t * 64);
+#pragma unroll
+          for (int e = 0; e < 8; e++) {
+            const int p = 8 * t + e;
+            if (p >= dl.L) break;
+            const int s = dl.s[p], nb = s / 9, rc = s - 9 * nb, r = rc / 3, cc = rc - 3 * r;
+            const int qn = pc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
+            const unsigned h = w[e >> 1];
+            const double v = (double)__uint_as_float((e & 1) ? (h & 0xffff0000u) : (h << 16));
+            const double tv = v * x[3 * (int64_t)qn + cc];
+            if (r == 0) d0 += tv;
+            else if (r == 1) d1 += tv;
+            else d2 += tv;
+          }
+        }
+        a0 += d0;
+        a1 += d1;
+        a2 += d2;
+      }
+      const double y0 = a0 + s0, y1 = a1 + s1, y2 = a2 + s2;
       __builtin_nontemporal_store(y0, &y[3 * (int64_t)n + 0]);
       __builtin_nontemporal_store(y1, &y[3 * (int64_t)n + 1]);
       __builtin_nontemporal_store(y2, &y[3 * (int64_t)n + 2]);
@@ -1232,17 +1342,18 @@ static void z_shape(int kern, int& ztx, int& zty) {
   }
 }
 
-template <int ZTX, int ZTY>
+template <int ZTX, int ZTY, bool AIJS = false>
 static void launch_symp(Ctx& c, const double* xpad, double* y, bool dot, bool gated, const ZTiling& zt, int nb) {
+  const uint16_t* Dq = c.D;
   if (dot && gated)
-    hipLaunchKernelGGL((k_spmv_symp<true, true, ZTX, ZTY>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g, c.U, xpad, y,
-                       c.partials, c.cg, zt);
+    hipLaunchKernelGGL((k_spmv_symp<true, true, ZTX, ZTY, AIJS>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g, c.U,
+                       xpad, y, c.partials, c.cg, zt, Dq, c.dsl);
   else if (dot)
-    hipLaunchKernelGGL((k_spmv_symp<true, false, ZTX, ZTY>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g, c.U, xpad, y,
-                       c.partials, c.cg, zt);
+    hipLaunchKernelGGL((k_spmv_symp<true, false, ZTX, ZTY, AIJS>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g, c.U,
+                       xpad, y, c.partials, c.cg, zt, Dq, c.dsl);
   else
-    hipLaunchKernelGGL((k_spmv_symp<false, false, ZTX, ZTY>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g, c.U, xpad,
-                       y, c.partials, c.cg, zt);
+    hipLaunchKernelGGL((k_spmv_symp<false, false, ZTX, ZTY, AIJS>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g, c.U,
+                       xpad, y, c.partials, c.cg, zt, Dq, c.dsl);
 }
 
 template <int ZTX, int ZTY>
@@ -1541,10 +1652,17 @@ static inline unsigned nblk(int64_t n) { return (unsigned)((n + TPB - 1) / TPB);
 int dirichlet_mask_host(const Geo& g, int gi, int gj, int gk) { return dirichlet_mask(g, gi, gj, gk); }
 
 int64_t node_blocks(const Ctx& c) { return nblk(c.g.nown); }
+// AIJ-split SpMV tile: the phased z-marching kernel, 128x4 where the subdomain is wide enough
+static void split_shape(const Ctx& c, int& ztx, int& zty) {
+  ztx = c.g.nx >= 128 ? 128 : 64;
+  zty = 4;
+}
+
 int64_t spmv_grid_blocks(const Ctx& c) {
-  if (c.U && c.spmv_kernel >= 1) {
+  if (c.fmt == FMT_SPLIT || (c.fmt == FMT_U && c.spmv_kernel >= 1)) {
     int ztx, zty;
-    z_shape(c.spmv_kernel, ztx, zty);
+    if (c.fmt == FMT_SPLIT) split_shape(c, ztx, zty);
+    else z_shape(c.spmv_kernel, ztx, zty);
     const ZTiling zt = z_tiling(c.g, ztx, zty, c.spmv_zblocks);
     return 8 * (int64_t)(((zt.nty + 7) / 8) * zt.ntx * zt.nzc);
   }
@@ -1552,7 +1670,6 @@ int64_t spmv_grid_blocks(const Ctx& c) {
   if (c.spmv_subl < 0) return (int64_t)c.g.nz * t.jgroups * t.nxc;
   return 8 * (int64_t)t.per_xcd;
 }
-
 int upload_constants(Ctx& c) {
   double B[8][6][24];
   compute_B_table(B);
@@ -1598,8 +1715,28 @@ void launch_gather_matrix_sym(Ctx& c) {
   hipLaunchKernelGGL(k_gather_matrix_sym, dim3(nblk(npad), 14), dim3(TPB), 0, c.stream, c.g, c.Ke, c.U, npad);
 }
 
+int build_split(Ctx& c, bool* exact) {
+  // pass-1 scratch: 117 bf16 per owned node in the (then unused) AIJ block storage
+  uint16_t* S = reinterpret_cast<uint16_t*>(c.V);
+  MCX_HIP(hipMemsetAsync(c.d_mask, 0, 16 * sizeof(unsigned), c.stream));
+  hipLaunchKernelGGL(k_split_deltas, dim3(nblk(c.g.nown), 13), dim3(TPB), 0, c.stream, c.g, c.Ke, c.U, S, c.d_mask);
+  unsigned hm[16];
+  MCX_HIP(hipMemcpyAsync(hm, c.d_mask, sizeof(hm), hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  *exact = hm[13] == 0;
+  if (!*exact) return 0;
+  DSlots dl;
+  for (int nb = 0; nb < 13; nb++)
+    for (int q = 0; q < 9; q++)
+      if (hm[nb] >> q & 1) dl.s[dl.L++] = (unsigned char)(nb * 9 + q);
+  dl.Lq = (dl.L + 7) / 8;
+  c.dsl = dl;
+  if (dl.L) hipLaunchKernelGGL(k_split_pack, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, S, c.D, dl);
+  return 0;
+}
+
 void launch_jacobi(Ctx& c) {
-  if (c.U)
+  if (c.fmt != FMT_V)
     hipLaunchKernelGGL(k_jacobi_sym, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.U, c.dinv);
   else
     hipLaunchKernelGGL(k_jacobi, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.V, c.dinv);
@@ -1608,7 +1745,15 @@ void launch_jacobi(Ctx& c) {
 void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
   const int nb = (int)spmv_grid_blocks(c);
   const SpmvTiling tl = spmv_tiling(c.g, c.spmv_subl);
-  if (c.U && c.spmv_kernel >= 1) {
+  if (c.fmt == FMT_SPLIT) {
+    int ztx, zty;
+    split_shape(c, ztx, zty);
+    const ZTiling zt = z_tiling(c.g, ztx, zty, c.spmv_zblocks);
+    if (ztx == 128) launch_symp<128, 4, true>(c, xpad, y, dot, gated, zt, nb);
+    else launch_symp<64, 4, true>(c, xpad, y, dot, gated, zt, nb);
+    return;
+  }
+  if (c.fmt == FMT_U && c.spmv_kernel >= 1) {
     int ztx, zty;
     z_shape(c.spmv_kernel, ztx, zty);
     const ZTiling zt = z_tiling(c.g, ztx, zty, c.spmv_zblocks);
@@ -1626,7 +1771,7 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
     }
     return;
   }
-  if (c.U) {
+  if (c.fmt == FMT_U) {
     if (dot && gated)
       hipLaunchKernelGGL((k_spmv_sym<true, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, c.U, xpad, y, c.partials,
                          c.cg, tl);

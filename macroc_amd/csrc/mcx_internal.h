@@ -29,6 +29,7 @@ struct Geo {
   int nx, ny, nz;          // owned node counts
   int PX, PY, PZ;          // padded box = owned + 1 ghost layer each side
   int UX, UXY;             // sbaij storage pitch: rows of UX = roundup(nx+2, 64) nodes (u_of)
+  int nt_u;                // sbaij SpMV: non-temporal loads of the node's own U stream
   int nown;                // nx*ny*nz
   int ex0, ey0, ez0;       // first element evaluated on this device (global)
   int nex, ney, nez;       // extended element counts (owned + upper ghost layer)
@@ -61,6 +62,19 @@ struct HaloPlan {
 };
 
 struct Ctx;
+
+// Matrix storage of a context.  FMT_V: AIJ stencil blocks (all 27 blocks per node, every row
+// summed in the CPU AIJ order).  FMT_U: MATSBAIJ (upper blocks, lower mirrored).  FMT_SPLIT:
+// the AIJ matrix held exactly as its upper blocks U plus, per owned node, the bf16 correction
+// lower - mirror(upper) of the correction slots that are non-zero somewhere in the matrix
+// (every AIJ value reconstructs bit for bit; rows summed in the z-marching order).
+enum Fmt { FMT_V = 0, FMT_U = 1, FMT_SPLIT = 2 };
+
+// AIJ-split correction slots (slot = nb*9 + r*3 + c of the 13 lower blocks), passed by value
+struct DSlots {
+  int L = 0, Lq = 0;        // active slots, 16-B quads per node (8 bf16 each)
+  unsigned char s[120];     // ascending slot ids
+};
 
 // In-process transport: several contexts (one host thread each) exchanging halos and partial
 // sums by device copies + events.  Used to run the multi-rank path on one GPU (tests) and for
@@ -103,6 +117,11 @@ struct Ctx {
   double* dinv = nullptr;    // Jacobi inverse diagonal
   double* V = nullptr;       // aij stencil-block matrix, AoSoA [ngroups][NPAIR][64] double2
   double* U = nullptr;       // sbaij upper stencil blocks over the padded box [npgroups][UPAIR][64] double2
+  uint16_t* D = nullptr;     // AIJ-split: packed bf16 corrections [node/64][dsl.Lq quads][64] x 8
+  unsigned* d_mask = nullptr;  // AIJ-split assembly: [0..12] slot masks per lower block, [13] inexact
+  int fmt = FMT_V;           // storage the matrix is currently assembled in
+  int aij_split = 1;         // aij: assemble in FMT_SPLIT when every correction is exact in bf16
+  DSlots dsl;
   int64_t npgroups = 0;
   int64_t nupper_local = 0;  // sbaij: stored upper values of the owned rows
   int spmv_subl = 0;         // SpMV sweep: lines per sub-slab of an XCD's slab (0 = whole slab, -1 = linear order)
@@ -171,6 +190,7 @@ void launch_residual(Ctx& c);          // b + partial sums of b.b
 void launch_element_ke(Ctx& c);
 void launch_gather_matrix(Ctx& c);
 void launch_gather_matrix_sym(Ctx& c);
+int build_split(Ctx& c, bool* exact);  // AIJ-split corrections from U + Ke (exact = usable)
 void launch_jacobi(Ctx& c);
 void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated);
 void launch_update_u(Ctx& c);

@@ -59,13 +59,20 @@ def newton_step(x_global_nat):
         its, rn, reason = m.solve_Ax()
         m.update_u()
         return dict(petsc=petsc, nat=nat, b=m.b(), du=m.du(), u=m.u(), res=res, its=its, reason=reason,
-                    rp=rp, ci=ci, v=v, y=y, dir=m.dump_dirichlet(), info=m.info)
+                    rp=rp, ci=ci, v=v, y=y, dir=m.dump_dirichlet(), info=m.get_info())
     return fn
 
 
 @pytest.mark.parametrize("name", ["g1088_r2", "g888_r8", "g522_r3", "g534_r8"])
 def test_multirank_newton_step(name):
-    _multirank(name, sbaij=False)
+    """AIJ blocks in the CPU AIJ order (-mat_aij_split 0): SpMV bit-exact on any rank grid."""
+    _multirank(name, sbaij=False, extra=["-mat_aij_split", 0])
+
+
+@pytest.mark.parametrize("name", ["g1088_r2", "g888_r8", "g534_r8"])
+def test_multirank_aij_split(name):
+    """Default AIJ storage (upper blocks + bf16 corrections): matrix bit-exact, SpMV rounding."""
+    _multirank(name, sbaij=False, split=True)
 
 
 @pytest.mark.parametrize("name", ["g1088_r2", "g888_r8"])
@@ -73,14 +80,14 @@ def test_multirank_sbaij(name):
     _multirank(name, sbaij=True)
 
 
-def _multirank(name, sbaij):
+def _multirank(name, sbaij, extra=(), split=False):
     fx = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     NX, NY, NZ = (int(v) for v in fx["grid"])
     nr = int(fx["nranks"])
     px, py, pz = (int(v) for v in fx["decomp"])
     rtol = float(fx["rtol"])
     argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
-            "-da_processors_z", pz, "-ksp_rtol", repr(rtol)] + (["-dm_mat_type", "sbaij"] if sbaij else [])
+            "-da_processors_z", pz, "-ksp_rtol", repr(rtol)] + (["-dm_mat_type", "sbaij"] if sbaij else []) + list(extra)
     ref = O.Problem(NX, NY, NZ, rtol=rtol)  # one rank: natural order == PETSc order
     x = np.random.default_rng(3).uniform(-1, 1, ref.ndofs)
     out = run_group(argv, nr, newton_step(x))
@@ -107,12 +114,14 @@ def _multirank(name, sbaij):
         b[o["nat"]] = o["b"]
         du[o["nat"]] = o["du"]
         dset.append(o["dir"])
-        if sbaij:  # z-marching default kernel: whole-3-vector mirrored terms, rounding-level
+        if split:
+            assert o["info"]["storage"] == 2
+        if sbaij or split:  # z-marching kernels: whole-3-vector mirrored terms, rounding-level
             absrow = np.add.reduceat(np.abs(v1) * np.abs(x[ci1]), rp1[:-1])
             assert np.all(np.abs(o["y"] - y1[o["nat"]]) <= 1e-14 * absrow[o["nat"]] + 1e-300)
         else:
             assert np.array_equal(o["y"], y1[o["nat"]])  # SpMV bit-exact
-        assert abs(o["its"] - int(fx["its"])) <= 1 + (1 if sbaij else 0)
+        assert abs(o["its"] - int(fx["its"])) <= 1 + (1 if sbaij or split else 0)
         assert o["res"] == out[0]["res"]
         # matrix rows: global PETSc columns, values bit-exact vs the one-rank matrix
         for q in range(len(o["nat"])):

@@ -35,11 +35,12 @@ def du_tol(rtol):
 
 @pytest.mark.parametrize("name", SINGLE)
 def test_newton_step_single_rank(name):
+    """-mat_aij_split 0: AIJ stencil blocks, every row summed in the CPU AIJ order."""
     fx = load(name)
     NX, NY, NZ = (int(v) for v in fx["grid"])
     rtol = float(fx["rtol"])
     P = O.Problem(NX, NY, NZ, rtol=rtol)
-    with M.Macroc(argv_for(NX, NY, NZ, rtol)) as m:
+    with M.Macroc(argv_for(NX, NY, NZ, rtol, ["-mat_aij_split", 0])) as m:
         petsc, nat = m.owned_dofs()
         assert np.array_equal(petsc, fx["dof_map"][nat])
         assert np.array_equal(m.dump_dirichlet(), fx["dirichlet"])
@@ -84,6 +85,39 @@ def test_newton_step_single_rank(name):
             assert np.linalg.norm(du) == 0
         m.update_u()
         assert np.linalg.norm(m.u() - fx["u"]) <= du_tol(rtol) * np.linalg.norm(fx["u"]) + 1e-300
+
+
+@pytest.mark.parametrize("name", SINGLE)
+def test_aij_split_single_rank(name):
+    """Default AIJ storage: upper blocks + bf16 lower corrections.  Every AIJ value is
+    reconstructed bit for bit (matrix dump == oracle), the SpMV rows differ from the CPU order
+    by rounding only (<= 1e-14 of sum |a_ij x_j|), the solve meets the north-star bar."""
+    fx = load(name)
+    NX, NY, NZ = (int(v) for v in fx["grid"])
+    rtol = float(fx["rtol"])
+    P = O.Problem(NX, NY, NZ, rtol=rtol)
+    with M.Macroc(argv_for(NX, NY, NZ, rtol)) as m:
+        for ts in (0, 1):
+            m.apply_bc_on_u(m.get_displacement(ts))
+            P.apply_bc_u(m.get_displacement(ts))
+        m.set_strains(); m.homogenize(); m.assembly_res()
+        P.set_strains(); P.homogenize(); P.assembly_res()
+        m.assembly_jac()
+        P.assembly_jac()
+        info = m.get_info()
+        assert info["storage"] == 2 and 0 <= info["split_slots"] <= 117  # 0: exactly symmetric
+        rp, ci, v = m.dump_csr()
+        assert np.array_equal(v, P.A_values())
+        x = np.random.default_rng(42).uniform(-1, 1, m.n)
+        y, y_ref = m.spmv(x), P.spmv(x)
+        absrow = np.add.reduceat(np.abs(v) * np.abs(x[ci]), rp[:-1])
+        assert np.all(np.abs(y - y_ref) <= 1e-14 * absrow + 1e-300)
+        assert np.array_equal(m.spmv(x), y)
+        its, rn, reason = m.solve_Ax()
+        assert abs(its - int(fx["its"])) <= 1
+        ref = fx["du"]
+        if np.linalg.norm(ref) > 0:
+            assert np.linalg.norm(m.du() - ref) <= du_tol(rtol) * np.linalg.norm(ref)
 
 
 def test_time_loop_matches_oracle_log():
