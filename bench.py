@@ -29,6 +29,16 @@ import macroc_amd as M  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
+# matrix storages: the reference's -dm_mat_type aij (DMSetMatType(da, MATAIJ), src/init.c:92) held
+# as upper blocks + exact bf16 lower corrections (default) or as plain AIJ blocks summed in the
+# CPU AIJ order; -dm_mat_type sbaij through DMSetFromOptions (src/init.c:93)
+STORAGE_ARGS = {"aij": ["-dm_mat_type", "aij"], "aij-blocks": ["-dm_mat_type", "aij", "-mat_aij_split", 0],
+                "sbaij": ["-dm_mat_type", "sbaij"]}
+STORAGE_NAME = {0: "aij-blocks", 1: "sbaij", 2: "aij-split"}
+KERNEL_NAME = {0: "k_spmv (AIJ stencil blocks, CPU AIJ row order)",
+               1: "k_spmv_symz (SBAIJ z-marching tiles)",
+               2: "k_spmv_symp<AIJS> (AIJ-split: upper blocks + bf16 lower corrections, z-marching)"}
+
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
@@ -141,6 +151,7 @@ def measure(argv, rank, world, comm_id, args):
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt[0])
     tm = m.timing()
+    storage = m.get_info()
     spmv_avg_ms = tm["spmv_ms_total"] / max(tm["spmv_launches"], 1)
     spmv_bytes = tm["spmv_bytes_per_launch"]
     check = None
@@ -156,6 +167,8 @@ def measure(argv, rank, world, comm_id, args):
         check = {"true_rel_residual": float(np.sqrt(loc[0] / loc[1])), "ksp_reason": int(reason)}
     m.finish()
     return {"its": its, "tm": tm, "info": info, "check": check, "spmv_avg_ms": spmv_avg_ms, "spmv_bytes": spmv_bytes,
+            "storage": STORAGE_NAME[storage["storage"]], "storage_id": storage["storage"],
+            "split_slots": storage["split_slots"],
             "achieved": spmv_bytes / (spmv_avg_ms * 1e-3) / 1e9, "ms_step": dt / args.steps * 1e3}
 
 
@@ -170,9 +183,9 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16)
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--same-device", action="store_true", help="testing only: every rank on device 0")
-    ap.add_argument("--mat-type", default="aij", choices=["aij", "sbaij"], help="-dm_mat_type of the headline")
+    ap.add_argument("--mat-type", default="aij", choices=list(STORAGE_ARGS), help="matrix storage of the headline")
     ap.add_argument("--variants", default=None,
-                    help="other -dm_mat_type runs reported beside it ('' = none; default sbaij on one GPU only)")
+                    help="other storages reported beside it ('' = none; default aij-blocks,sbaij on one GPU only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -192,11 +205,11 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         comm_id = obj[0]
     def run(mat_type):
-        return measure(argv + ["-dm_mat_type", mat_type], rank, world, comm_id, args)
+        return measure(argv + STORAGE_ARGS[mat_type], rank, world, comm_id, args)
 
     r = run(args.mat_type)
     if args.variants is None:
-        args.variants = "sbaij" if world == 1 else ""
+        args.variants = "aij-blocks,sbaij" if world == 1 else ""
     variants = {}
     if args.variants:
         for v in args.variants.split(","):
@@ -207,10 +220,11 @@ def main():
                     comm_id = obj[0]
                 vr = run(v)
                 variants[v] = {"value": 3 * NX * NY * NZ / (vr["ms_step"] * 1e-3), "ms_per_step": vr["ms_step"],
+                               "storage": vr["storage"], "kernel": KERNEL_NAME[vr["storage_id"]],
                                "cg_its": vr["its"], "ms_per_cg_iter": vr["tm"]["solve_ms"] / max(vr["its"], 1),
                                "dof_cg_iters_per_s": 3 * NX * NY * NZ * vr["its"] / (vr["tm"]["solve_ms"] * 1e-3),
                                "spmv_avg_ms": vr["spmv_avg_ms"], "spmv_bytes_per_launch": vr["spmv_bytes"],
-                               "spmv_achieved_GBs": vr["achieved"], "spmv_traffic": pmc_traffic(v, NX, NY, NZ),
+                               "spmv_achieved_GBs": vr["achieved"], "spmv_traffic": pmc_traffic(vr["storage"], NX, NY, NZ),
                                "check": vr["check"]}
     its, tm, info, check = r["its"], r["tm"], r["info"], r["check"]
     spmv_avg_ms, spmv_bytes, achieved, ms_step = r["spmv_avg_ms"], r["spmv_bytes"], r["achieved"], r["ms_step"]
@@ -238,7 +252,9 @@ def main():
             "data": "synthetic (reference defaults: lx=50 ly=1 lz=50, BC_CIRCLE, E=1e7 nu=0.25, time step 1)",
             "config": {"workload": f"MacroC Newton iteration, time step 1, CG/Jacobi rtol {args.rtol:g}",
                        "grid": [NX, NY, NZ], "grid_per_gpu": [G, G, G], "processors": [px, py, pz],
-                       "dofs": ndofs, "nnz": info["nnz_global"], "parallelism": f"dmda{px}x{py}x{pz}", "mat_type": args.mat_type},
+                       "dofs": ndofs, "nnz": info["nnz_global"], "parallelism": f"dmda{px}x{py}x{pz}",
+                       "mat_type": "aij" if args.mat_type.startswith("aij") else "sbaij", "storage": r["storage"],
+                       "split_slots": r["split_slots"]},
             "cg_its": its,
             "ms_per_cg_iter": tm["solve_ms"] / max(its, 1),
             # CG iterations grow ~linearly with the global grid edge (720 at 64^3, 2814 at 256^3),
@@ -247,8 +263,8 @@ def main():
             "phases_ms": {k: tm[k] for k in ("strains_ms", "homogenize_ms", "residual_ms", "jacobian_ms",
                                              "solve_ms", "update_ms")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                         "frac": achieved / PEAK_HBM_GBS, "traffic": pmc_traffic(args.mat_type, NX, NY, NZ),
-                         "kernel": "k_spmv (stencil-block SpMV inside CG)", "bytes_per_launch": spmv_bytes,
+                         "frac": achieved / PEAK_HBM_GBS, "traffic": pmc_traffic(r["storage"], NX, NY, NZ),
+                         "kernel": KERNEL_NAME[r["storage_id"]], "bytes_per_launch": spmv_bytes,
                          "avg_launch_ms": spmv_avg_ms, "launches_timed": tm["spmv_launches"]},
             "cpu_baseline": cpu,
             "check": check,
