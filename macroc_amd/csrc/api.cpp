@@ -122,8 +122,11 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   if ((rc = dalloc(c, &c.u_pad, npad)) || (rc = dalloc(c, &c.p_pad, npad)) || (rc = dalloc(c, &c.b, nown3)) ||
       (rc = dalloc(c, &c.du, nown3)) || (rc = dalloc(c, &c.r, nown3)) || (rc = dalloc(c, &c.z, nown3)) ||
       (rc = dalloc(c, &c.w, nown3)) || (rc = dalloc(c, &c.dinv, nown3)) || (rc = dalloc(c, &c.tmp, nown3)) ||
-      (c.o.mat_type == MCX_MAT_SBAIJ ? (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))
-                                     : (rc = dalloc(c, &c.V, c.ngroups * NPAIR * 128))) ||
+      (c.o.mat_type == MCX_MAT_SBAIJ
+           ? (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))
+           // AIJ blocks; with AIJ-split also the scratch of its assembly (117 bf16 per padded node)
+           : (rc = dalloc(c, &c.V, std::max<int64_t>(c.ngroups * NPAIR * 128,
+                                                     c.aij_split ? (117 * 64 * c.npgroups + 3) / 4 : 0)))) ||
       (c.aij_split && (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))) ||
       (rc = dalloc(c, &c.eps, 6 * 8 * E)) ||
       (rc = dalloc(c, &c.sig, 6 * 8 * E)) || (rc = dalloc(c, &c.ctan, 36 * 8 * E)) ||
@@ -137,9 +140,9 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
        (rc = dalloc(c, &c.ftrial, 8 * E))))
     return rc;
   if (c.aij_split) {
-    MCX_HIP(hipMalloc(&c.D, sizeof(uint16_t) * 8 * 15 * 64 * c.ngroups));
+    MCX_HIP(hipMalloc(&c.D, sizeof(uint16_t) * 120 * 64 * c.npgroups));
     MCX_HIP(hipMalloc(&c.d_mask, 16 * sizeof(unsigned)));
-    c.device_bytes += sizeof(uint16_t) * 8 * 15 * 64 * c.ngroups;
+    c.device_bytes += sizeof(uint16_t) * 120 * 64 * c.npgroups;
   }
   MCX_HIP(hipHostMalloc((void**)&c.h_cg, sizeof(CgState) * 2, hipHostMallocDefault));
   std::memset(c.h_cg, 0, sizeof(CgState) * 2);
@@ -884,20 +887,21 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
   if (vals) {
     V.resize(up ? c.npgroups * UPAIR * 128 : c.ngroups * NPAIR * 128);
     MCX_HIP(hipMemcpyAsync(V.data(), up ? c.U : c.V, sizeof(double) * V.size(), hipMemcpyDeviceToHost, c.stream));
-    if (c.fmt == FMT_SPLIT && c.dsl.Lq) {
-      Dh.resize((size_t)c.ngroups * c.dsl.Lq * 64 * 8);
+    if (c.fmt == FMT_SPLIT && c.dsl.L) {
+      Dh.resize((size_t)c.npgroups * c.dsl.Lq * 64 * 8);
       MCX_HIP(hipMemcpyAsync(Dh.data(), c.D, sizeof(uint16_t) * Dh.size(), hipMemcpyDeviceToHost, c.stream));
     }
     MCX_HIP(hipStreamSynchronize(c.stream));
   }
-  // AIJ-split: packed position of each correction slot (-1: no correction stored)
+  // AIJ-split: packed position of each correction slot (-1: no correction stored), stored with
+  // the row node (u_of index): nb*9 + r*3 + c
   int dpos[117];
   for (int s = 0; s < 117; s++) dpos[s] = -1;
   for (int p = 0; p < c.dsl.L; p++) dpos[c.dsl.s[p]] = p;
-  auto corr = [&](int64_t n, int s) -> double {
+  auto corr = [&](int64_t u, int s) -> double {
     const int p = dpos[s];
     if (p < 0) return 0.;
-    const uint16_t b = Dh[(((n >> 6) * c.dsl.Lq + (p >> 3)) * 64 + (n & 63)) * 8 + (p & 7)];
+    const uint16_t b = Dh[(((u >> 6) * c.dsl.Lq + (p >> 3)) * 64 + (u & 63)) * 8 + (p & 7)];
     uint32_t f = (uint32_t)b << 16;
     float fv;
     std::memcpy(&fv, &f, 4);
@@ -925,7 +929,7 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
             static const int dsl[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
             if (nb < 13) {
               v = uval(q, 6 + 9 * (12 - nb) + cc * 3 + r);
-              if (c.fmt == FMT_SPLIT) v = v + corr(n, nb * 9 + r * 3 + cc);  // exact AIJ lower value
+              if (c.fmt == FMT_SPLIT) v = v + corr(pc, nb * 9 + r * 3 + cc);  // exact AIJ lower value
             }
             else if (nb == 13) v = uval(pc, dsl[r][cc]);
             else v = uval(pc, 6 + 9 * (nb - 14) + r * 3 + cc);

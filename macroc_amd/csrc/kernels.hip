@@ -605,17 +605,18 @@ __global__ __launch_bounds__(TPB) void k_gather_matrix_sym(Geo g, const double* 
 
 // AIJ-split assembly, pass 1: thread = (owned node n, lower block nb < 13).  The AIJ value
 // A(n,nb)[r][c] (matrix_block, exactly what k_gather_matrix stores) minus the mirrored upper
-// value U(m, 26-nb)[c][r] of the neighbour m, as bf16 bits in S[(nb*9 + r*3 + c) * nown + n].
-// A correction is usable only if it is exact in bf16 and mirror + bf16 == A bit for bit;
-// d_mask[nb] collects the slots that are non-zero anywhere, d_mask[13] any inexact one.
+// value U(m, nbp)[c][r] of the neighbour m = n + off(nb), nbp = 26 - nb, as bf16 bits:
+// S[(nb*9 + r*3 + c) * npu + u_of(n)].  A correction is usable only if it is exact in bf16 and
+// U + bf16 == A bit for bit; d_mask[nb] collects the slots that are non-zero anywhere,
+// d_mask[13] any inexact one.
 __global__ __launch_bounds__(TPB) void k_split_deltas(Geo g, const double* __restrict__ Ke,
                                                       const double* __restrict__ U, uint16_t* __restrict__ S,
-                                                      unsigned* __restrict__ mask) {
+                                                      int64_t npu, unsigned* __restrict__ mask) {
   __shared__ unsigned s_bits, s_bad;
   if (threadIdx.x == 0) s_bits = s_bad = 0;
   __syncthreads();
   const int n = blockIdx.x * TPB + threadIdx.x;
-  const int nb = blockIdx.y;
+  const int nb = blockIdx.y, nbp = 26 - nb;
   if (n < g.nown) {
     int i, j, k;
     node_ijk(g, n, i, j, k);
@@ -624,7 +625,7 @@ __global__ __launch_bounds__(TPB) void k_split_deltas(Geo g, const double* __res
     matrix_block(g, Ke, g.xs + i, g.ys + j, g.zs + k, dx, dy, dz, low);
     const int um = u_of(g, i + dx, j + dy, k + dz);
     const double* Um = U + (int64_t)(um >> 6) * (UPAIR * 128) + 2 * (um & 63);
-    const int base = 6 + 9 * (12 - nb);
+    const int base = 6 + 9 * (nbp - 14), un = u_of(g, i, j, k);
     unsigned bits = 0, bad = 0;
 #pragma unroll
     for (int r = 0; r < 3; r++)
@@ -637,7 +638,7 @@ __global__ __launch_bounds__(TPB) void k_split_deltas(Geo g, const double* __res
         const double db = (double)__uint_as_float(fb);
         if (db != d || mir + db != low[r * 3 + c]) bad = 1;
         if (d != 0.) bits |= 1u << (r * 3 + c);
-        S[(int64_t)(nb * 9 + r * 3 + c) * g.nown + n] = (uint16_t)(fb >> 16);
+        S[(int64_t)(nb * 9 + r * 3 + c) * npu + un] = (uint16_t)(fb >> 16);
       }
     if (bits) atomicOr(&s_bits, bits);
     if (bad) atomicOr(&s_bad, 1u);
@@ -649,16 +650,15 @@ __global__ __launch_bounds__(TPB) void k_split_deltas(Geo g, const double* __res
   }
 }
 
-// AIJ-split assembly, pass 2: pack the active slots of every owned node, 8 bf16 per 16 B,
-// D[((n/64) * Lq + p/8) * 64 + n%64] quad, element p%8
-__global__ __launch_bounds__(TPB) void k_split_pack(Geo g, const uint16_t* __restrict__ S, uint16_t* __restrict__ D,
-                                                    DSlots dl) {
-  const int n = blockIdx.x * TPB + threadIdx.x;
-  if (n >= g.nown) return;
-  for (int p = 0; p < dl.Lq * 8; p++) {
-    const uint16_t v = p < dl.L ? S[(int64_t)dl.s[p] * g.nown + n] : (uint16_t)0;
-    D[(((int64_t)(n >> 6) * dl.Lq + (p >> 3)) * 64 + (n & 63)) * 8 + (p & 7)] = v;
-  }
+// AIJ-split assembly, pass 2: the active slots of every node of the padded box (u_of index),
+// 8 bf16 per 16 B: D[(((u/64) * Lq + p/8) * 64 + u%64) * 8 + p%8]
+__global__ __launch_bounds__(TPB) void k_split_pack(const uint16_t* __restrict__ S, int64_t npu,
+                                                    uint16_t* __restrict__ D, DSlots dl) {
+  const int64_t u = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (u >= npu) return;
+  for (int p = 0; p < dl.Lq * 8; p++)
+    D[(((u >> 6) * dl.Lq + (p >> 3)) * 64 + (u & 63)) * 8 + (p & 7)] =
+        p < dl.L ? S[(int64_t)dl.s[p] * npu + u] : (uint16_t)0;
 }
 
 // PCSetUp_Jacobi: diag, VecReciprocal (non-zeros only), zeros -> 1
@@ -887,7 +887,9 @@ __device__ __forceinline__ void ut_x2(const double* __restrict__ U, const double
     a[2 * q] = w.x;
     a[2 * q + 1] = w.y;
   }
-  const double* b = a + sh;
+  double b[9];
+#pragma unroll
+  for (int t = 0; t < 9; t++) b[t] = sh ? a[t + 1] : a[t];
   const double x0 = x[3 * (int64_t)p], x1 = x[3 * (int64_t)p + 1], x2 = x[3 * (int64_t)p + 2];
   c0 = b[0] * x0;
   c0 += b[3] * x1;
@@ -1091,16 +1093,7 @@ __global__ __launch_bounds__(ZTX * ZTY, (ZTX * ZTY >= 512 ? 1 : 2)) void k_spmv_
 //   (diagonal block, nbp 14..26 ascending).
 // AIJ-split lower corrections: per owned node the 117 lower-block values minus their mirrored
 // upper values, exact in bf16, as 15 x 16-B quads [node/64][15][node%64] (slot nb*9 + r*3 + c)
-constexpr int DQUAD = 15;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ double bf16_slot(const u32x4 (&q)[DQUAD], int t) {
-  const u32x4 w = q[t >> 3];
-  const int h = (t >> 1) & 3;
-  const unsigned v = w[h];
-  const unsigned b = (t & 1) ? (v & 0xffff0000u) : (v << 16);
-  return (double)__uint_as_float(b);
-}
 
 template <bool DOT, bool GATED, int TX, int TY, bool AIJS = false>
 __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* __restrict__ U,
@@ -1152,11 +1145,7 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
       c2 = buf[slot][2][me];
     } else {
       const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
-      if (g.nt_u & 2) {
-        c0 = c1 = c2 = 0.;
-      } else {
-        ut_x2(U, x, ucn + dx + dy * g.UX + dz * g.UXY, pcn + dx + dy * PX + dz * PXY, 26 - nb, c0, c1, c2);
-      }
+      ut_x2(U, x, ucn + dx + dy * g.UX + dz * g.UXY, pcn + dx + dy * PX + dz * PXY, 26 - nb, c0, c1, c2);
     }
   };
   for (int k = k0; k < k1; k++) {
@@ -1165,11 +1154,10 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
     const bool has_next = k + 1 < k1;
     if (k == k0 && active) {  // chunk start: the previous plane is not marched here, pull all nine
       a0 = a1 = a2 = 0.;
-      constexpr int ord[9] = {8, 4, 5, 6, 7, 0, 1, 2, 3};
 #pragma unroll
-      for (int q = 0; q < 9; q++) {
+      for (int q = 0; q < 9; q++) {  // canonical order 8 | 4 5 6 7 | 0 1 2 3
         double c0, c1, c2;
-        term(ord[q], 0, false, pc, uc, c0, c1, c2);
+        term(q == 0 ? 8 : (q <= 4 ? q + 3 : q - 5), 0, false, pc, uc, c0, c1, c2);
         a0 += c0;
         a1 += c1;
         a2 += c2;
@@ -1183,6 +1171,16 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
       x2 = x[3 * (int64_t)pc + 2];
     }
     n0 = n1 = n2 = 0.;
+    // AIJ-split: the first 24 corrections of this node, loaded before the phases (overlapped)
+    u32x4 wpre[3] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+    if constexpr (AIJS) {
+      if (active) {
+        const u32x4* Dn = reinterpret_cast<const u32x4*>(Dq) + (int64_t)(uc >> 6) * dl.Lq * 64 + (uc & 63);
+#pragma unroll
+        for (int t = 0; t < 3; t++)
+          if (t < dl.Lq) wpre[t] = __builtin_nontemporal_load(Dn + t * 64);
+      }
+    }
 #pragma unroll
     for (int ph = 0; ph < 3; ph++) {
       const int lo = ph == 0 ? 14 : (ph == 1 ? 19 : 23), hi = ph == 0 ? 18 : (ph == 1 ? 22 : 26);
@@ -1219,7 +1217,7 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
           double a[9];
 #pragma unroll
           for (int t = 0; t < 9; t++) a[t] = sl(base + t);
-          const int q = (g.nt_u & 4) ? pc : pc + dx + dy * PX + dz * PXY;
+          const int q = pc + dx + dy * PX + dz * PXY;
           const double z0 = x[3 * (int64_t)q], z1 = x[3 * (int64_t)q + 1], z2 = x[3 * (int64_t)q + 2];
           double u0 = a[0] * z0;
           u0 += a[1] * z1;
@@ -1286,26 +1284,32 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
       const int n = i + j * g.nx + k * g.nx * g.ny;
       if constexpr (AIJS) {
         // exact AIJ lower blocks = mirrored upper (summed above) + the bf16 corrections of the
-        // active slots, ascending (nb, c) per row
-        const u32x4* Dn = reinterpret_cast<const u32x4*>(Dq) + (int64_t)(n >> 6) * (dl.Lq * 64) + (n & 63);
-        double d0 = 0., d1 = 0., d2 = 0.;
-#pragma unroll
-        for (int t = 0; t < DQUAD; t++) {
-          if (t >= dl.Lq) break;
-          const u32x4 w = __builtin_nontemporal_load(Dn + t * 64);
-#pragma unroll
-          for (int e = 0; e < 8; e++) {
-            const int p = 8 * t + e;
-            if (p >= dl.L) break;
-            const int s = dl.s[p], nb = s / 9, rc = s - 9 * nb, r = rc / 3, cc = rc - 3 * r;
-            const int qn = pc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
-            const unsigned h = w[e >> 1];
-            const double v = (double)__uint_as_float((e & 1) ? (h & 0xffff0000u) : (h << 16));
-            const double tv = v * x[3 * (int64_t)qn + cc];
-            if (r == 0) d0 += tv;
-            else if (r == 1) d1 += tv;
-            else d2 += tv;
+        // active slots, in slot order (ascending nb, then c, per row).  8 corrections per 16-B
+        // load; the slot walk is uniform, x is reloaded only when the block changes.
+        const u32x4* Dn = reinterpret_cast<const u32x4*>(Dq) + (int64_t)(uc >> 6) * dl.Lq * 64 + (uc & 63);
+        double d0 = 0., d1 = 0., d2 = 0., z0 = 0., z1 = 0., z2 = 0.;
+        u32x4 w = {0u, 0u, 0u, 0u};
+        int prev = -1;
+        for (int p = 0; p < dl.L; p++) {
+          if ((p & 7) == 0) {
+            const int t = p >> 3;
+            w = t == 0 ? wpre[0] : (t == 1 ? wpre[1] : (t == 2 ? wpre[2] : __builtin_nontemporal_load(Dn + t * 64)));
           }
+          const int s = dl.s[p], nb = s / 9, rc = s - 9 * nb, r = rc / 3, cc = rc - 3 * r;
+          if (nb != prev) {
+            const int qn = pc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
+            z0 = x[3 * (int64_t)qn];
+            z1 = x[3 * (int64_t)qn + 1];
+            z2 = x[3 * (int64_t)qn + 2];
+            prev = nb;
+          }
+          const int e = p & 7;
+          const unsigned h = (e >> 1) == 0 ? w[0] : ((e >> 1) == 1 ? w[1] : ((e >> 1) == 2 ? w[2] : w[3]));
+          const double v = (double)__uint_as_float((e & 1) ? (h & 0xffff0000u) : (h << 16));
+          const double t = v * (cc == 0 ? z0 : (cc == 1 ? z1 : z2));
+          if (r == 0) d0 += t;
+          else if (r == 1) d1 += t;
+          else d2 += t;
         }
         a0 += d0;
         a1 += d1;
@@ -1716,22 +1720,28 @@ void launch_gather_matrix_sym(Ctx& c) {
 }
 
 int build_split(Ctx& c, bool* exact) {
-  // pass-1 scratch: 117 bf16 per owned node in the (then unused) AIJ block storage
+  // pass-1 scratch: 117 bf16 per node of the padded box in the (then unused) AIJ block storage
+  const int64_t npu = c.npgroups * 64;
   uint16_t* S = reinterpret_cast<uint16_t*>(c.V);
+  MCX_HIP(hipMemsetAsync(S, 0, sizeof(uint16_t) * 117 * npu, c.stream));
   MCX_HIP(hipMemsetAsync(c.d_mask, 0, 16 * sizeof(unsigned), c.stream));
-  hipLaunchKernelGGL(k_split_deltas, dim3(nblk(c.g.nown), 13), dim3(TPB), 0, c.stream, c.g, c.Ke, c.U, S, c.d_mask);
+  hipLaunchKernelGGL(k_split_deltas, dim3(nblk(c.g.nown), 13), dim3(TPB), 0, c.stream, c.g, c.Ke, c.U, S, npu,
+                     c.d_mask);
   unsigned hm[16];
   MCX_HIP(hipMemcpyAsync(hm, c.d_mask, sizeof(hm), hipMemcpyDeviceToHost, c.stream));
   MCX_HIP(hipStreamSynchronize(c.stream));
   *exact = hm[13] == 0;
   if (!*exact) return 0;
   DSlots dl;
-  for (int nb = 0; nb < 13; nb++)
+  for (int b = 0; b < 13; b++) {
+    dl.m9[b] = (unsigned short)(hm[b] & 511u);
+    dl.pos[b] = (unsigned char)dl.L;
     for (int q = 0; q < 9; q++)
-      if (hm[nb] >> q & 1) dl.s[dl.L++] = (unsigned char)(nb * 9 + q);
+      if (hm[b] >> q & 1) dl.s[dl.L++] = (unsigned char)(b * 9 + q);
+  }
   dl.Lq = (dl.L + 7) / 8;
   c.dsl = dl;
-  if (dl.L) hipLaunchKernelGGL(k_split_pack, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, S, c.D, dl);
+  if (dl.L) hipLaunchKernelGGL(k_split_pack, dim3(nblk(npu)), dim3(TPB), 0, c.stream, S, npu, c.D, dl);
   return 0;
 }
 

@@ -70,10 +70,13 @@ struct Ctx;
 // (every AIJ value reconstructs bit for bit; rows summed in the z-marching order).
 enum Fmt { FMT_V = 0, FMT_U = 1, FMT_SPLIT = 2 };
 
-// AIJ-split correction slots (slot = nb*9 + r*3 + c of the 13 lower blocks), passed by value
+// AIJ-split correction slots, passed by value: slot = nb*9 + r*3 + c of the row node's lower
+// block nb holds A(n, nb)[r][c] - U(m, 26-nb)[c][r], m = n + off(nb)
 struct DSlots {
-  int L = 0, Lq = 0;        // active slots, 16-B quads per node (8 bf16 each)
-  unsigned char s[120];     // ascending slot ids
+  int L = 0, Lq = 0;        // active slots; 16-B quads per node ([u_of/64][Lq][64] x 8 bf16)
+  unsigned char s[120];     // ascending active slot ids
+  unsigned short m9[13];    // per lower block nb: active (r*3+c) bits
+  unsigned char pos[13];    // per lower block: index of its first active slot
 };
 
 // In-process transport: several contexts (one host thread each) exchanging halos and partial
@@ -117,7 +120,7 @@ struct Ctx {
   double* dinv = nullptr;    // Jacobi inverse diagonal
   double* V = nullptr;       // aij stencil-block matrix, AoSoA [ngroups][NPAIR][64] double2
   double* U = nullptr;       // sbaij upper stencil blocks over the padded box [npgroups][UPAIR][64] double2
-  uint16_t* D = nullptr;     // AIJ-split: packed bf16 corrections [node/64][dsl.Lq quads][64] x 8
+  uint16_t* D = nullptr;     // AIJ-split: bf16 corrections of the padded box [u_of/64][dsl.Lq][64] x 8
   unsigned* d_mask = nullptr;  // AIJ-split assembly: [0..12] slot masks per lower block, [13] inexact
   int fmt = FMT_V;           // storage the matrix is currently assembled in
   int aij_split = 1;         // aij: assemble in FMT_SPLIT when every correction is exact in bf16
