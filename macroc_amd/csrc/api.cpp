@@ -75,7 +75,7 @@ static int64_t max_spmv_blocks(Ctx& c) {
   const int keep = c.spmv_kernel, keep_fmt = c.fmt;
   int64_t m = 0;
   for (int f : {FMT_V, FMT_U, FMT_SPLIT})
-    for (int k = 0; k <= 10; k++) {
+    for (int k = 0; k <= 11; k++) {
       c.fmt = f;
       c.spmv_kernel = k;
       m = std::max(m, spmv_grid_blocks(c));
@@ -102,12 +102,13 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   if (rc) return rc;
   int ncu = 0;
   MCX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c.device));
-  // z-marching tiles (sbaij and AIJ-split): one resident round of blocks (two per CU), 128-wide
-  // tiles where the subdomain is wide enough — tools/spmv_ab.py sweeps, DESIGN.md §4
-  c.spmv_zblocks = 2 * std::max(ncu, 1);
+  // z-marching tiles (sbaij and AIJ-split): one resident round of blocks, 256x4 phased tiles
+  // where the subdomain is that wide — tools/spmv_ab.py sweeps, DESIGN.md §4
+  c.ncu = std::max(ncu, 1);
+  c.g.ncu = c.ncu;
   c.aij_split = o->mat_type == MCX_MAT_AIJ && o->mat_aij_split;
   if (o->mat_type == MCX_MAT_SBAIJ) {
-    c.spmv_kernel = c.g.nx >= 128 ? 4 : 1;
+    c.spmv_kernel = c.g.nx >= 256 ? 11 : (c.g.nx >= 128 ? 4 : 1);
     c.fmt = FMT_U;
   }
   MCX_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
@@ -1039,6 +1040,19 @@ int mcx_set_option(void* ctx, const char* name, double value) {
   }
   if (!std::strcmp(name, "spmv_nt_u")) {
     c.g.nt_u = (int)value;
+    return 0;
+  }
+  if (!std::strcmp(name, "split_tx")) {
+    const int v = (int)value;
+    if (v != 0 && v != 64 && v != 128 && v != 256) {
+      set_error("split_tx: 0, 64, 128 or 256");
+      return 2;
+    }
+    c.split_tx = v;
+    if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
+      set_error("split_tx: partials buffer too small");
+      return 2;
+    }
     return 0;
   }
   if (!std::strcmp(name, "aij_split")) {  // takes effect at the next mcx_assembly_jac

@@ -144,6 +144,7 @@ int setup_decomposition(Ctx& c) {
   g.UX = (g.nx + 2 + GROUP - 1) / GROUP * GROUP;
   g.UXY = g.UX * g.PY;
   g.nt_u = 0;
+  g.ncu = 256;
   c.npgroups = (GROUP + (int64_t)g.UXY * g.PZ + GROUP - 1) / GROUP;
   return 0;
 }

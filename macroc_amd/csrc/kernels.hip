@@ -859,6 +859,7 @@ struct ZTiling {
 
 static ZTiling z_tiling(const Geo& g, int ztx, int zty, int want) {
   ZTiling t;
+  if (want <= 0) want = g.ncu * std::max(1, 1024 / (ztx * zty));  // one resident round
   t.ntx = (g.nx + ztx - 1) / ztx;
   t.nty = (g.ny + zty - 1) / zty;
   const int tiles = t.ntx * t.nty;
@@ -1342,6 +1343,7 @@ static void z_shape(int kern, int& ztx, int& zty) {
     case 8: ztx = 64; zty = 4; break;
     case 9: ztx = 64; zty = 8; break;
     case 10: ztx = 256; zty = 2; break;
+    case 11: ztx = 256; zty = 4; break;
     default: ztx = 64; zty = 4; break;
   }
 }
@@ -1658,7 +1660,7 @@ int dirichlet_mask_host(const Geo& g, int gi, int gj, int gk) { return dirichlet
 int64_t node_blocks(const Ctx& c) { return nblk(c.g.nown); }
 // AIJ-split SpMV tile: the phased z-marching kernel, 128x4 where the subdomain is wide enough
 static void split_shape(const Ctx& c, int& ztx, int& zty) {
-  ztx = c.g.nx >= 128 ? 128 : 64;
+  ztx = c.split_tx ? c.split_tx : (c.g.nx >= 256 ? 256 : (c.g.nx >= 128 ? 128 : 64));
   zty = 4;
 }
 
@@ -1759,7 +1761,8 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
     int ztx, zty;
     split_shape(c, ztx, zty);
     const ZTiling zt = z_tiling(c.g, ztx, zty, c.spmv_zblocks);
-    if (ztx == 128) launch_symp<128, 4, true>(c, xpad, y, dot, gated, zt, nb);
+    if (ztx == 256) launch_symp<256, 4, true>(c, xpad, y, dot, gated, zt, nb);
+    else if (ztx == 128) launch_symp<128, 4, true>(c, xpad, y, dot, gated, zt, nb);
     else launch_symp<64, 4, true>(c, xpad, y, dot, gated, zt, nb);
     return;
   }
@@ -1777,6 +1780,7 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
       case 8: launch_symp<64, 4>(c, xpad, y, dot, gated, zt, nb); break;
       case 9: launch_symp<64, 8>(c, xpad, y, dot, gated, zt, nb); break;
       case 10: launch_symp<256, 2>(c, xpad, y, dot, gated, zt, nb); break;
+      case 11: launch_symp<256, 4>(c, xpad, y, dot, gated, zt, nb); break;
       default: launch_symz<64, 4>(c, xpad, y, dot, gated, zt, nb); break;
     }
     return;

@@ -30,6 +30,7 @@ struct Geo {
   int PX, PY, PZ;          // padded box = owned + 1 ghost layer each side
   int UX, UXY;             // sbaij storage pitch: rows of UX = roundup(nx+2, 64) nodes (u_of)
   int nt_u;                // sbaij SpMV: non-temporal loads of the node's own U stream
+  int ncu;                 // compute units (z-marching grid sizing)
   int nown;                // nx*ny*nz
   int ex0, ey0, ez0;       // first element evaluated on this device (global)
   int nex, ney, nez;       // extended element counts (owned + upper ghost layer)
@@ -123,14 +124,16 @@ struct Ctx {
   uint16_t* D = nullptr;     // AIJ-split: bf16 corrections of the padded box [u_of/64][dsl.Lq][64] x 8
   unsigned* d_mask = nullptr;  // AIJ-split assembly: [0..12] slot masks per lower block, [13] inexact
   int fmt = FMT_V;           // storage the matrix is currently assembled in
-  int aij_split = 1;         // aij: assemble in FMT_SPLIT when every correction is exact in bf16
+  int aij_split = 1;
+  int split_tx = 0;          // AIJ-split tile width (0: by subdomain width; option split_tx)         // aij: assemble in FMT_SPLIT when every correction is exact in bf16
   DSlots dsl;
   int64_t npgroups = 0;
   int64_t nupper_local = 0;  // sbaij: stored upper values of the owned rows
   int spmv_subl = 0;         // SpMV sweep: lines per sub-slab of an XCD's slab (0 = whole slab, -1 = linear order)
   int spmv_kernel = 0;       // sbaij: 0 = pull, 1..4 = z-marching push/pull tiles (shapes, see z_shape)
   int cg_nt = 0;             // CG vector kernels: non-temporal stores of x, r, z, p
-  int spmv_zblocks = 1024;   // z-marching: target block count (sets the z-chunk length)
+  int spmv_zblocks = 0;      // z-marching: target block count (0: one resident round, CUs x blocks/CU)
+  int ncu = 0;               // compute units of the device
   int spmv_nt = 2;           // aij: 1 = non-temporal matrix loads, 2 = + non-temporal y stores (-3 %, spmv_ab)
   int64_t partials_cap = 0;
   double* eps = nullptr;     // [6][8][nelem]

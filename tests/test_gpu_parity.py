@@ -215,7 +215,7 @@ def test_64cubed_properties():
 @pytest.mark.parametrize("NX,NY,NZ", [(8, 8, 8), (16, 16, 16), (12, 7, 9), (130, 6, 5)])
 def test_sbaij_single_rank(NX, NY, NZ):
     """-dm_mat_type sbaij: matrix bit-exact vs the oracle's MATSBAIJ emulation; the pull SpMV
-    (spmv_kernel 0) bit-exact too.  The z-marching kernels (1..10, one the default) add the mirrored
+    (spmv_kernel 0) bit-exact too.  The z-marching kernels (1..11, one the default) add the mirrored
     lower blocks as whole 3-vectors, so their rows differ from the oracle's order by rounding
     only: checked to 1e-14 of sum|a||x| per row, and run-to-run identical (no atomics).  The
     solution agrees with the reference's AIJ path within the north-star tolerance."""
@@ -238,7 +238,7 @@ def test_sbaij_single_rank(NX, NY, NZ):
         y_ref = P.spmv(x)
         absrow = np.add.reduceat(np.abs(v) * np.abs(x[ci]), rp[:-1])  # sum |a_ij x_j| per row
         phased = []
-        for kern in range(11):
+        for kern in range(12):
             m.set_option("spmv_kernel", kern)
             y = m.spmv(x)
             if kern == 0:
