@@ -1172,6 +1172,7 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
       x2 = x[3 * (int64_t)pc + 2];
     }
     n0 = n1 = n2 = 0.;
+    double cd0 = 0., cd1 = 0., cd2 = 0.;  // AIJ-split corrections of this plane's node
     // AIJ-split: the first 24 corrections of this node, loaded before the phases (overlapped)
     u32x4 wpre[3] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
     if constexpr (AIJS) {
@@ -1249,6 +1250,41 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
           buf[nbp - lo][2][tgt] = c2;
         }
       }
+      // AIJ-split corrections of this plane's node (independent of the LDS exchange), computed
+      // while the block waits at the phase-2 barrier; exact AIJ lower blocks = mirrored upper
+      // (summed in the gathers) + the bf16 corrections of the active slots, ascending nb then c
+      // per row, added after the lower sum.  8 corrections per 16-B load (prefetched at plane
+      // start); per lower block with corrections one x load, slot positions uniform.
+      if (AIJS && ph == 2 && active) {
+        const u32x4* Dn = reinterpret_cast<const u32x4*>(Dq) + (int64_t)(uc >> 6) * dl.Lq * 64 + (uc & 63);
+        double d0 = 0., d1 = 0., d2 = 0., z0 = 0., z1 = 0., z2 = 0.;
+        int prev = -1;
+        for (int t = 0; t < dl.Lq; t++) {  // uniform: 8 slots per quad, slot ids read 8 at a time
+          const u32x4 w = t == 0 ? wpre[0] : (t == 1 ? wpre[1] : (t == 2 ? wpre[2] : __builtin_nontemporal_load(Dn + t * 64)));
+#pragma unroll
+          for (int e = 0; e < 8; e++) {
+            const int p = 8 * t + e;
+            if (p >= dl.L) break;
+            const int s = dl.s[p], nb = s / 9, rc = s - 9 * nb, r = rc / 3, cc = rc - 3 * r;
+            if (nb != prev) {
+              const int qn = pc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
+              z0 = x[3 * (int64_t)qn];
+              z1 = x[3 * (int64_t)qn + 1];
+              z2 = x[3 * (int64_t)qn + 2];
+              prev = nb;
+            }
+            const unsigned hw = w[e >> 1];
+            const double v = (double)__uint_as_float((e & 1) ? (hw & 0xffff0000u) : (hw << 16));
+            const double tv = v * (cc == 0 ? z0 : (cc == 1 ? z1 : z2));
+            if (r == 0) d0 += tv;
+            else if (r == 1) d1 += tv;
+            else d2 += tv;
+          }
+        }
+        cd0 = d0;
+        cd1 = d1;
+        cd2 = d2;
+      }
       __syncthreads();
       if (active) {
         if (ph == 0) {
@@ -1284,37 +1320,9 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
     if (active) {
       const int n = i + j * g.nx + k * g.nx * g.ny;
       if constexpr (AIJS) {
-        // exact AIJ lower blocks = mirrored upper (summed above) + the bf16 corrections of the
-        // active slots, in slot order (ascending nb, then c, per row).  8 corrections per 16-B
-        // load; the slot walk is uniform, x is reloaded only when the block changes.
-        const u32x4* Dn = reinterpret_cast<const u32x4*>(Dq) + (int64_t)(uc >> 6) * dl.Lq * 64 + (uc & 63);
-        double d0 = 0., d1 = 0., d2 = 0., z0 = 0., z1 = 0., z2 = 0.;
-        u32x4 w = {0u, 0u, 0u, 0u};
-        int prev = -1;
-        for (int p = 0; p < dl.L; p++) {
-          if ((p & 7) == 0) {
-            const int t = p >> 3;
-            w = t == 0 ? wpre[0] : (t == 1 ? wpre[1] : (t == 2 ? wpre[2] : __builtin_nontemporal_load(Dn + t * 64)));
-          }
-          const int s = dl.s[p], nb = s / 9, rc = s - 9 * nb, r = rc / 3, cc = rc - 3 * r;
-          if (nb != prev) {
-            const int qn = pc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
-            z0 = x[3 * (int64_t)qn];
-            z1 = x[3 * (int64_t)qn + 1];
-            z2 = x[3 * (int64_t)qn + 2];
-            prev = nb;
-          }
-          const int e = p & 7;
-          const unsigned h = (e >> 1) == 0 ? w[0] : ((e >> 1) == 1 ? w[1] : ((e >> 1) == 2 ? w[2] : w[3]));
-          const double v = (double)__uint_as_float((e & 1) ? (h & 0xffff0000u) : (h << 16));
-          const double t = v * (cc == 0 ? z0 : (cc == 1 ? z1 : z2));
-          if (r == 0) d0 += t;
-          else if (r == 1) d1 += t;
-          else d2 += t;
-        }
-        a0 += d0;
-        a1 += d1;
-        a2 += d2;
+        a0 += cd0;
+        a1 += cd1;
+        a2 += cd2;
       }
       const double y0 = a0 + s0, y1 = a1 + s1, y2 = a2 + s2;
       __builtin_nontemporal_store(y0, &y[3 * (int64_t)n + 0]);
