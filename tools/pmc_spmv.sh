@@ -9,7 +9,7 @@ G=${2:-256}
 case $MAT in
   aij-split) RE='k_spmv_symp'; BM=aij ;;
   aij-blocks) RE='k_spmv<'; BM=aij-blocks ;;
-  sbaij) RE='k_spmv_symz|k_spmv_sym<'; BM=sbaij ;;
+  sbaij) RE='k_spmv_sym'; BM=sbaij ;;
 esac
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc/$MAT-$G
