@@ -1038,10 +1038,6 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     }
     return 0;
   }
-  if (!std::strcmp(name, "spmv_nt_u")) {
-    c.g.nt_u = (int)value;
-    return 0;
-  }
   if (!std::strcmp(name, "split_tx")) {
     const int v = (int)value;
     if (v != 0 && v != 64 && v != 128 && v != 256) {

@@ -143,7 +143,6 @@ int setup_decomposition(Ctx& c) {
   // 64 + i + (j+1)*UX + (k+1)*UXY (i = -1 lands in the unused last column of the row before)
   g.UX = (g.nx + 2 + GROUP - 1) / GROUP * GROUP;
   g.UXY = g.UX * g.PY;
-  g.nt_u = 0;
   g.ncu = 256;
   c.npgroups = (GROUP + (int64_t)g.UXY * g.PZ + GROUP - 1) / GROUP;
   return 0;

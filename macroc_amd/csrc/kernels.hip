@@ -1190,14 +1190,7 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
         // slot s of this node = half (s & 1) of 16-B pair s >> 1; pairs shared by adjacent
         // blocks are the same load (read-only, merged by the compiler)
         auto sl = [&](int s) {
-          const double2* pp = Ug + (s >> 1) * 64;
-          double2 w;
-          if (g.nt_u & 1) {
-            w.x = __builtin_nontemporal_load(&pp->x);
-            w.y = __builtin_nontemporal_load(&pp->y);
-          } else {
-            w = *pp;
-          }
+          const double2 w = Ug[(s >> 1) * 64];
           return (s & 1) ? w.y : w.x;
         };
         if (ph == 0) {

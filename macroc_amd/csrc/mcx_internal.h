@@ -29,7 +29,6 @@ struct Geo {
   int nx, ny, nz;          // owned node counts
   int PX, PY, PZ;          // padded box = owned + 1 ghost layer each side
   int UX, UXY;             // sbaij storage pitch: rows of UX = roundup(nx+2, 64) nodes (u_of)
-  int nt_u;                // sbaij SpMV: non-temporal loads of the node's own U stream
   int ncu;                 // compute units (z-marching grid sizing)
   int nown;                // nx*ny*nz
   int ex0, ey0, ez0;       // first element evaluated on this device (global)

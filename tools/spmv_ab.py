@@ -17,7 +17,6 @@ ap.add_argument("--nt", default="0", help="aij non-temporal matrix loads: 0,1")
 ap.add_argument("--zblocks", default="0", help="z-marching grid (0 = one resident round)")
 ap.add_argument("--split", type=int, default=1, help="aij: -mat_aij_split")
 ap.add_argument("--splittx", default="0", help="aij-split tile widths to compare (0 = default)")
-ap.add_argument("--ntu", default="0", help="sbaij: non-temporal U loads (phased kernel)")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--iters", type=int, default=20)
 a = ap.parse_args()
@@ -32,7 +31,7 @@ import numpy as np  # noqa: E402
 
 variants = [(int(s), int(kk), int(nt), int(zb), int(nu), int(tx)) for s in a.subl.split(",")
             for kk in a.kernels.split(",") for nt in a.nt.split(",") for zb in a.zblocks.split(",")
-            for nu in a.ntu.split(",") for tx in a.splittx.split(",")]
+            for nu in ("0",) for tx in a.splittx.split(",")]
 res = {v: [] for v in variants}
 x = np.random.default_rng(1).uniform(-1, 1, m.n)
 ys = {}
@@ -41,7 +40,6 @@ for v in variants:
     m.set_option("spmv_kernel", v[1])
     m.set_option("spmv_nt", v[2])
     m.set_option("spmv_zblocks", v[3])
-    m.set_option("spmv_nt_u", v[4])
     if a.mat == "aij" and a.split:
         m.set_option("split_tx", v[5])
     ys[v] = m.spmv(x)
@@ -52,14 +50,13 @@ for r in range(a.rounds):
         m.set_option("spmv_kernel", v[1])
         m.set_option("spmv_nt", v[2])
         m.set_option("spmv_zblocks", v[3])
-        m.set_option("spmv_nt_u", v[4])
-        if a.mat == "aij" and a.split:
+            if a.mat == "aij" and a.split:
             m.set_option("split_tx", v[5])
         res[v].append(m.time_spmv(a.iters))
 tb = m.timing()["spmv_bytes_per_launch"]
 for v in variants:
     med = statistics.median(res[v])
     rel = np.linalg.norm(ys[v] - y0) / np.linalg.norm(y0)
-    print(f"{a.mat} grid {N}^3 subl={v[0]:3d} kernel={v[1]} nt={v[2]} zb={v[3]} ntu={v[4]} tx={v[5]}: median {med:.4f} ms  min {min(res[v]):.4f}  -> "
+    print(f"{a.mat} grid {N}^3 subl={v[0]:3d} kernel={v[1]} nt={v[2]} zb={v[3]} tx={v[5]}: median {med:.4f} ms  min {min(res[v]):.4f}  -> "
           f"{tb / med / 1e6:.0f} GB/s (algorithmic {tb / 1e9:.2f} GB)  |y-y0|/|y0|={rel:.2e}")
 m.finish()
