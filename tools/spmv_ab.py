@@ -50,7 +50,7 @@ for r in range(a.rounds):
         m.set_option("spmv_kernel", v[1])
         m.set_option("spmv_nt", v[2])
         m.set_option("spmv_zblocks", v[3])
-            if a.mat == "aij" and a.split:
+        if a.mat == "aij" and a.split:
             m.set_option("split_tx", v[5])
         res[v].append(m.time_spmv(a.iters))
 tb = m.timing()["spmv_bytes_per_launch"]
