@@ -168,7 +168,7 @@ def measure(argv, rank, world, comm_id, args):
     m.finish()
     return {"its": its, "tm": tm, "info": info, "check": check, "spmv_avg_ms": spmv_avg_ms, "spmv_bytes": spmv_bytes,
             "storage": STORAGE_NAME[storage["storage"]], "storage_id": storage["storage"],
-            "split_slots": storage["split_slots"],
+            "split_slots": storage["split_slots"], "split_bits": storage["split_bits"],
             "achieved": spmv_bytes / (spmv_avg_ms * 1e-3) / 1e9, "ms_step": dt / args.steps * 1e3}
 
 
@@ -254,7 +254,7 @@ def main():
                        "grid": [NX, NY, NZ], "grid_per_gpu": [G, G, G], "processors": [px, py, pz],
                        "dofs": ndofs, "nnz": info["nnz_global"], "parallelism": f"dmda{px}x{py}x{pz}",
                        "mat_type": "aij" if args.mat_type.startswith("aij") else "sbaij", "storage": r["storage"],
-                       "split_slots": r["split_slots"]},
+                       "split_slots": r["split_slots"], "split_bits": r["split_bits"]},
             "cg_its": its,
             "ms_per_cg_iter": tm["solve_ms"] / max(its, 1),
             # CG iterations grow ~linearly with the global grid edge (720 at 64^3, 2814 at 256^3),

@@ -107,6 +107,7 @@ typedef struct {
   int storage;                  /* matrix as last assembled: 0 AIJ blocks, 1 SBAIJ upper blocks,
                                    2 AIJ-split (upper blocks + bf16 lower corrections) */
   int split_slots;              /* AIJ-split: correction slots stored per node (of 117) */
+  int split_bits;               /* AIJ-split: bits per correction (16 = bf16, 32 = f32) */
 } mcx_info;
 
 typedef struct {

@@ -67,6 +67,7 @@ class Info(C.Structure):
         ("nnz_local", C.c_int64), ("nnz_global", C.c_int64), ("nelem_local", C.c_int64), ("nelem_ext", C.c_int64),
         ("dx", C.c_double), ("dy", C.c_double), ("dz", C.c_double), ("wg", C.c_double),
         ("device_bytes", C.c_int64), ("device", C.c_int), ("storage", C.c_int), ("split_slots", C.c_int),
+        ("split_bits", C.c_int),
     ]
 
     def as_dict(self):

@@ -127,7 +127,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
            ? (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))
            // AIJ blocks; with AIJ-split also the scratch of its assembly (117 bf16 per padded node)
            : (rc = dalloc(c, &c.V, std::max<int64_t>(c.ngroups * NPAIR * 128,
-                                                     c.aij_split ? (117 * 64 * c.npgroups + 3) / 4 : 0)))) ||
+                                                     c.aij_split ? (126 * 64 * c.npgroups + 1) / 2 : 0)))) ||
       (c.aij_split && (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))) ||
       (rc = dalloc(c, &c.eps, 6 * 8 * E)) ||
       (rc = dalloc(c, &c.sig, 6 * 8 * E)) || (rc = dalloc(c, &c.ctan, 36 * 8 * E)) ||
@@ -141,9 +141,9 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
        (rc = dalloc(c, &c.ftrial, 8 * E))))
     return rc;
   if (c.aij_split) {
-    MCX_HIP(hipMalloc(&c.D, sizeof(uint16_t) * 120 * 64 * c.npgroups));
+    MCX_HIP(hipMalloc(&c.D, sizeof(unsigned) * 120 * 64 * c.npgroups));  // f32 worst case
     MCX_HIP(hipMalloc(&c.d_mask, 16 * sizeof(unsigned)));
-    c.device_bytes += sizeof(uint16_t) * 120 * 64 * c.npgroups;
+    c.device_bytes += sizeof(unsigned) * 120 * 64 * c.npgroups;
   }
   MCX_HIP(hipHostMalloc((void**)&c.h_cg, sizeof(CgState) * 2, hipHostMallocDefault));
   std::memset(c.h_cg, 0, sizeof(CgState) * 2);
@@ -455,6 +455,7 @@ static void fill_info(const Ctx& c, mcx_info* in) {
   in->device = c.device;
   in->storage = c.fmt;
   in->split_slots = c.fmt == FMT_SPLIT ? c.dsl.L : 0;
+  in->split_bits = c.fmt == FMT_SPLIT ? (c.dsl.wide ? 32 : 16) : 0;
 }
 
 
@@ -896,14 +897,16 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
   }
   // AIJ-split: packed position of each correction slot (-1: no correction stored), stored with
   // the row node (u_of index): nb*9 + r*3 + c
-  int dpos[117];
-  for (int s = 0; s < 117; s++) dpos[s] = -1;
+  int dpos[126];
+  for (int s = 0; s < 126; s++) dpos[s] = -1;
   for (int p = 0; p < c.dsl.L; p++) dpos[c.dsl.s[p]] = p;
   auto corr = [&](int64_t u, int s) -> double {
     const int p = dpos[s];
     if (p < 0) return 0.;
-    const uint16_t b = Dh[(((u >> 6) * c.dsl.Lq + (p >> 3)) * 64 + (u & 63)) * 8 + (p & 7)];
-    uint32_t f = (uint32_t)b << 16;
+    const int per = c.dsl.wide ? 4 : 8;
+    const int64_t q = ((u >> 6) * c.dsl.Lq + p / per) * 64 + (u & 63);
+    uint32_t f = c.dsl.wide ? (uint32_t)Dh[q * 8 + 2 * (p % 4)] | ((uint32_t)Dh[q * 8 + 2 * (p % 4) + 1] << 16)
+                            : (uint32_t)Dh[q * 8 + p % 8] << 16;
     float fv;
     std::memcpy(&fv, &f, 4);
     return (double)fv;
@@ -932,7 +935,10 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
               v = uval(q, 6 + 9 * (12 - nb) + cc * 3 + r);
               if (c.fmt == FMT_SPLIT) v = v + corr(pc, nb * 9 + r * 3 + cc);  // exact AIJ lower value
             }
-            else if (nb == 13) v = uval(pc, dsl[r][cc]);
+            else if (nb == 13) {
+              v = uval(pc, dsl[r][cc]);
+              if (c.fmt == FMT_SPLIT && r > cc) v = v + corr(pc, 13 * 9 + r * 3 + cc);  // lower triangle
+            }
             else v = uval(pc, 6 + 9 * (nb - 14) + r * 3 + cc);
           } else if (vals) {
             int s = nb * 9 + r * 3 + cc;
@@ -1036,6 +1042,14 @@ int mcx_set_option(void* ctx, const char* name, double value) {
       set_error("spmv_zblocks: partials buffer too small");
       return 2;
     }
+    return 0;
+  }
+  if (!std::strcmp(name, "split_wide")) {  // testing: f32 corrections even when bf16 is exact
+    c.split_wide = value != 0.;
+    return 0;
+  }
+  if (!std::strcmp(name, "split_maxq")) {  // takes effect at the next mcx_assembly_jac
+    c.split_maxq = std::max(0, std::min(30, (int)value));
     return 0;
   }
   if (!std::strcmp(name, "split_tx")) {

@@ -605,19 +605,43 @@ __global__ __launch_bounds__(TPB) void k_gather_matrix_sym(Geo g, const double* 
 
 // AIJ-split assembly, pass 1: thread = (owned node n, lower block nb < 13).  The AIJ value
 // A(n,nb)[r][c] (matrix_block, exactly what k_gather_matrix stores) minus the mirrored upper
-// value U(m, nbp)[c][r] of the neighbour m = n + off(nb), nbp = 26 - nb, as bf16 bits:
-// S[(nb*9 + r*3 + c) * npu + u_of(n)].  A correction is usable only if it is exact in bf16 and
-// U + bf16 == A bit for bit; d_mask[nb] collects the slots that are non-zero anywhere,
-// d_mask[13] any inexact one.
+// value U(m, nbp)[c][r] of the neighbour m = n + off(nb), nbp = 26 - nb, as f32 bits:
+// S[(nb*9 + r*3 + c) * npu + u_of(n)].  A width is usable only if every correction is exact in
+// it and U + correction == A bit for bit; d_mask[nb] collects the slots that are non-zero
+// anywhere, d_mask[14] bit 0 = some correction inexact in bf16, bit 1 = inexact in f32.
+// blockIdx.y = 13: the diagonal block's strictly-lower entries against their mirrors.
 __global__ __launch_bounds__(TPB) void k_split_deltas(Geo g, const double* __restrict__ Ke,
-                                                      const double* __restrict__ U, uint16_t* __restrict__ S,
+                                                      const double* __restrict__ U, unsigned* __restrict__ S,
                                                       int64_t npu, unsigned* __restrict__ mask) {
   __shared__ unsigned s_bits, s_bad;
   if (threadIdx.x == 0) s_bits = s_bad = 0;
   __syncthreads();
   const int n = blockIdx.x * TPB + threadIdx.x;
   const int nb = blockIdx.y, nbp = 26 - nb;
-  if (n < g.nown) {
+  if (n < g.nown && nb == 13) {
+    // diagonal block: stored as its upper triangle; the strictly-lower AIJ entries (1,0), (2,0),
+    // (2,1) are corrected against their mirrors
+    int i, j, k;
+    node_ijk(g, n, i, j, k);
+    double blk[9];
+    matrix_block(g, Ke, g.xs + i, g.ys + j, g.zs + k, 0, 0, 0, blk);
+    const int un = u_of(g, i, j, k);
+    unsigned bits = 0, bad = 0;
+#pragma unroll
+    for (int r = 1; r < 3; r++)
+#pragma unroll
+      for (int c = 0; c < r; c++) {
+        const double mir = blk[c * 3 + r], d = blk[r * 3 + c] - mir;
+        const unsigned f32 = __float_as_uint((float)d), fb = f32 & 0xffff0000u;
+        const double df = (double)__uint_as_float(f32), db = (double)__uint_as_float(fb);
+        if (db != d || mir + db != blk[r * 3 + c]) bad |= 1;
+        if (df != d || mir + df != blk[r * 3 + c]) bad |= 2;
+        if (d != 0.) bits |= 1u << (r * 3 + c);
+        S[(int64_t)(13 * 9 + r * 3 + c) * npu + un] = f32;
+      }
+    if (bits) atomicOr(&s_bits, bits);
+    if (bad) atomicOr(&s_bad, bad);
+  } else if (n < g.nown) {
     int i, j, k;
     node_ijk(g, n, i, j, k);
     const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
@@ -634,31 +658,36 @@ __global__ __launch_bounds__(TPB) void k_split_deltas(Geo g, const double* __res
         const int s = base + c * 3 + r;
         const double mir = Um[(s >> 1) * 128 + (s & 1)];
         const double d = low[r * 3 + c] - mir;
-        const unsigned fb = __float_as_uint((float)d) & 0xffff0000u;
-        const double db = (double)__uint_as_float(fb);
-        if (db != d || mir + db != low[r * 3 + c]) bad = 1;
+        const unsigned f32 = __float_as_uint((float)d), fb = f32 & 0xffff0000u;
+        const double df = (double)__uint_as_float(f32), db = (double)__uint_as_float(fb);
+        if (db != d || mir + db != low[r * 3 + c]) bad |= 1;  // not exact in bf16
+        if (df != d || mir + df != low[r * 3 + c]) bad |= 2;  // not exact in f32
         if (d != 0.) bits |= 1u << (r * 3 + c);
-        S[(int64_t)(nb * 9 + r * 3 + c) * npu + un] = (uint16_t)(fb >> 16);
+        S[(int64_t)(nb * 9 + r * 3 + c) * npu + un] = f32;
       }
     if (bits) atomicOr(&s_bits, bits);
-    if (bad) atomicOr(&s_bad, 1u);
+    if (bad) atomicOr(&s_bad, bad);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     if (s_bits) atomicOr(&mask[nb], s_bits);
-    if (s_bad) atomicOr(&mask[13], 1u);
+    if (s_bad) atomicOr(&mask[14], s_bad);
   }
 }
 
 // AIJ-split assembly, pass 2: the active slots of every node of the padded box (u_of index),
-// 8 bf16 per 16 B: D[(((u/64) * Lq + p/8) * 64 + u%64) * 8 + p%8]
-__global__ __launch_bounds__(TPB) void k_split_pack(const uint16_t* __restrict__ S, int64_t npu,
+// 16 B per quad: 8 bf16 (D[(((u/64) * Lq + p/8) * 64 + u%64) * 8 + p%8]) or 4 f32
+__global__ __launch_bounds__(TPB) void k_split_pack(const unsigned* __restrict__ S, int64_t npu,
                                                     uint16_t* __restrict__ D, DSlots dl) {
   const int64_t u = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (u >= npu) return;
-  for (int p = 0; p < dl.Lq * 8; p++)
-    D[(((u >> 6) * dl.Lq + (p >> 3)) * 64 + (u & 63)) * 8 + (p & 7)] =
-        p < dl.L ? S[(int64_t)dl.s[p] * npu + u] : (uint16_t)0;
+  const int per = dl.wide ? 4 : 8;
+  for (int p = 0; p < dl.Lq * per; p++) {
+    const unsigned v = p < dl.L ? S[(int64_t)dl.s[p] * npu + u] : 0u;
+    const int64_t q = (((u >> 6) * dl.Lq + p / per) * 64 + (u & 63));
+    if (dl.wide) reinterpret_cast<unsigned*>(D)[q * 4 + p % 4] = v;
+    else D[q * 8 + p % 8] = (uint16_t)(v >> 16);
+  }
 }
 
 // PCSetUp_Jacobi: diag, VecReciprocal (non-zeros only), zeros -> 1
@@ -1252,11 +1281,13 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
         const u32x4* Dn = reinterpret_cast<const u32x4*>(Dq) + (int64_t)(uc >> 6) * dl.Lq * 64 + (uc & 63);
         double d0 = 0., d1 = 0., d2 = 0., z0 = 0., z1 = 0., z2 = 0.;
         int prev = -1;
-        for (int t = 0; t < dl.Lq; t++) {  // uniform: 8 slots per quad, slot ids read 8 at a time
+        const int per = dl.wide ? 4 : 8;
+        for (int t = 0; t < dl.Lq; t++) {  // uniform: 8 (bf16) or 4 (f32) slots per quad
           const u32x4 w = t == 0 ? wpre[0] : (t == 1 ? wpre[1] : (t == 2 ? wpre[2] : __builtin_nontemporal_load(Dn + t * 64)));
 #pragma unroll
           for (int e = 0; e < 8; e++) {
-            const int p = 8 * t + e;
+            if (e >= per) break;
+            const int p = per * t + e;
             if (p >= dl.L) break;
             const int s = dl.s[p], nb = s / 9, rc = s - 9 * nb, r = rc / 3, cc = rc - 3 * r;
             if (nb != prev) {
@@ -1266,8 +1297,13 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
               z2 = x[3 * (int64_t)qn + 2];
               prev = nb;
             }
-            const unsigned hw = w[e >> 1];
-            const double v = (double)__uint_as_float((e & 1) ? (hw & 0xffff0000u) : (hw << 16));
+            double v;
+            if (dl.wide) {
+              v = (double)__uint_as_float(w[e & 3]);
+            } else {
+              const unsigned hw = w[e >> 1];
+              v = (double)__uint_as_float((e & 1) ? (hw & 0xffff0000u) : (hw << 16));
+            }
             const double tv = v * (cc == 0 ? z0 : (cc == 1 ? z1 : z2));
             if (r == 0) d0 += tv;
             else if (r == 1) d1 += tv;
@@ -1722,27 +1758,34 @@ void launch_gather_matrix_sym(Ctx& c) {
   hipLaunchKernelGGL(k_gather_matrix_sym, dim3(nblk(npad), 14), dim3(TPB), 0, c.stream, c.g, c.Ke, c.U, npad);
 }
 
+// exact = the split storage is used (every correction exact and at most split_maxq quads)
 int build_split(Ctx& c, bool* exact) {
-  // pass-1 scratch: 117 bf16 per node of the padded box in the (then unused) AIJ block storage
+  // pass-1 scratch: 126 f32 slots (13 lower blocks + the diagonal) per node of the padded box, in
+  // the (then unused) AIJ block storage
   const int64_t npu = c.npgroups * 64;
-  uint16_t* S = reinterpret_cast<uint16_t*>(c.V);
-  MCX_HIP(hipMemsetAsync(S, 0, sizeof(uint16_t) * 117 * npu, c.stream));
+  unsigned* S = reinterpret_cast<unsigned*>(c.V);
+  MCX_HIP(hipMemsetAsync(S, 0, sizeof(unsigned) * 126 * npu, c.stream));
   MCX_HIP(hipMemsetAsync(c.d_mask, 0, 16 * sizeof(unsigned), c.stream));
-  hipLaunchKernelGGL(k_split_deltas, dim3(nblk(c.g.nown), 13), dim3(TPB), 0, c.stream, c.g, c.Ke, c.U, S, npu,
+  hipLaunchKernelGGL(k_split_deltas, dim3(nblk(c.g.nown), 14), dim3(TPB), 0, c.stream, c.g, c.Ke, c.U, S, npu,
                      c.d_mask);
   unsigned hm[16];
   MCX_HIP(hipMemcpyAsync(hm, c.d_mask, sizeof(hm), hipMemcpyDeviceToHost, c.stream));
   MCX_HIP(hipStreamSynchronize(c.stream));
-  *exact = hm[13] == 0;
+  *exact = (hm[14] & 2u) == 0;  // f32 always suffices when bf16 does
   if (!*exact) return 0;
   DSlots dl;
-  for (int b = 0; b < 13; b++) {
+  dl.wide = (hm[14] & 1u) || c.split_wide ? 1 : 0;
+  for (int b = 0; b < 14; b++) {
     dl.m9[b] = (unsigned short)(hm[b] & 511u);
     dl.pos[b] = (unsigned char)dl.L;
     for (int q = 0; q < 9; q++)
       if (hm[b] >> q & 1) dl.s[dl.L++] = (unsigned char)(b * 9 + q);
   }
-  dl.Lq = (dl.L + 7) / 8;
+  dl.Lq = dl.wide ? (dl.L + 3) / 4 : (dl.L + 7) / 8;
+  if (dl.Lq > c.split_maxq) {  // dense corrections: the AIJ blocks stream is faster
+    *exact = false;
+    return 0;
+  }
   c.dsl = dl;
   if (dl.L) hipLaunchKernelGGL(k_split_pack, dim3(nblk(npu)), dim3(TPB), 0, c.stream, S, npu, c.D, dl);
   return 0;

@@ -71,12 +71,14 @@ struct Ctx;
 enum Fmt { FMT_V = 0, FMT_U = 1, FMT_SPLIT = 2 };
 
 // AIJ-split correction slots, passed by value: slot = nb*9 + r*3 + c of the row node's lower
-// block nb holds A(n, nb)[r][c] - U(m, 26-nb)[c][r], m = n + off(nb)
+// block nb < 13 holds A(n, nb)[r][c] - U(m, 26-nb)[c][r], m = n + off(nb); nb = 13 (the
+// diagonal block, stored as its upper triangle) holds A(n,n)[r][c] - A(n,n)[c][r] for r > c
 struct DSlots {
-  int L = 0, Lq = 0;        // active slots; 16-B quads per node ([u_of/64][Lq][64] x 8 bf16)
-  unsigned char s[120];     // ascending active slot ids
-  unsigned short m9[13];    // per lower block nb: active (r*3+c) bits
-  unsigned char pos[13];    // per lower block: index of its first active slot
+  int L = 0, Lq = 0;        // active slots; 16-B quads per node ([u_of/64][Lq][64])
+  int wide = 0;             // 0: 8 bf16 per quad; 1: 4 f32 per quad (some correction not exact in bf16)
+  unsigned char s[120];     // ascending active slot ids (at most 117 + 3)
+  unsigned short m9[14];    // per lower block nb (13: diagonal): active (r*3+c) bits
+  unsigned char pos[14];    // per block: index of its first active slot
 };
 
 // In-process transport: several contexts (one host thread each) exchanging halos and partial
@@ -121,9 +123,11 @@ struct Ctx {
   double* V = nullptr;       // aij stencil-block matrix, AoSoA [ngroups][NPAIR][64] double2
   double* U = nullptr;       // sbaij upper stencil blocks over the padded box [npgroups][UPAIR][64] double2
   uint16_t* D = nullptr;     // AIJ-split: bf16 corrections of the padded box [u_of/64][dsl.Lq][64] x 8
-  unsigned* d_mask = nullptr;  // AIJ-split assembly: [0..12] slot masks per lower block, [13] inexact
+  unsigned* d_mask = nullptr;  // AIJ-split assembly: [0..13] slot masks per lower block, [14] inexact
   int fmt = FMT_V;           // storage the matrix is currently assembled in
   int aij_split = 1;
+  int split_maxq = 4;
+  int split_wide = 0;        // force f32 corrections (testing the wide path)        // AIJ-split only while the corrections fit this many 16-B quads per node
   int split_tx = 0;          // AIJ-split tile width (0: by subdomain width; option split_tx)         // aij: assemble in FMT_SPLIT when every correction is exact in bf16
   DSlots dsl;
   int64_t npgroups = 0;

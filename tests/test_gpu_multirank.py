@@ -45,8 +45,10 @@ def run_group(argv, nranks, fn, timeout=300):
     return results
 
 
-def newton_step(x_global_nat):
+def newton_step(x_global_nat, options=()):
     def fn(m):
+        for k, v in options:
+            m.set_option(k, v)
         petsc, nat = m.owned_dofs()
         m.apply_bc_on_u(m.get_displacement(0))
         m.apply_bc_on_u(m.get_displacement(1))
@@ -90,7 +92,7 @@ def _multirank(name, sbaij, extra=(), split=False):
             "-da_processors_z", pz, "-ksp_rtol", repr(rtol)] + (["-dm_mat_type", "sbaij"] if sbaij else []) + list(extra)
     ref = O.Problem(NX, NY, NZ, rtol=rtol)  # one rank: natural order == PETSc order
     x = np.random.default_rng(3).uniform(-1, 1, ref.ndofs)
-    out = run_group(argv, nr, newton_step(x))
+    out = run_group(argv, nr, newton_step(x, [("split_maxq", 30)] if split else []))
     aij_du = None
     if sbaij:  # the sbaij classification is by natural index: decomposition independent
         ref.apply_bc_u(ref.get_displacement(0))

@@ -97,6 +97,7 @@ def test_aij_split_single_rank(name):
     rtol = float(fx["rtol"])
     P = O.Problem(NX, NY, NZ, rtol=rtol)
     with M.Macroc(argv_for(NX, NY, NZ, rtol)) as m:
+        m.set_option("split_maxq", 30)  # tiny grids are boundary-dominated: dense corrections
         for ts in (0, 1):
             m.apply_bc_on_u(m.get_displacement(ts))
             P.apply_bc_u(m.get_displacement(ts))
@@ -118,6 +119,38 @@ def test_aij_split_single_rank(name):
         ref = fx["du"]
         if np.linalg.norm(ref) > 0:
             assert np.linalg.norm(m.du() - ref) <= du_tol(rtol) * np.linalg.norm(ref)
+
+
+@pytest.mark.parametrize("maxq,wide,storage", [(4, 0, 0), (30, 0, 2), (30, 1, 2)])
+def test_aij_split_dense_plastic(maxq, wide, storage):
+    """A plastic tangent fills all 117 correction slots: by default (at most 4 quads per node)
+    the AIJ blocks are used; allowed more quads, the split storage holds them in bf16 or f32
+    (forced) — the matrix is bit-exact either way, the SpMV within rounding."""
+    NX, NY, NZ, dt = 12, 10, 12, 0.05
+    P = O.Problem(NX, NY, NZ, rtol=1e-10, law=1, dt=dt, bc_type=0)
+    P.apply_bc_u(P.get_displacement(1))
+    P.set_strains(); P.homogenize(); P.assembly_res(); P.assembly_jac(); P.solve(); P.update_u()
+    u = P.u()
+    P.set_strains(); P.homogenize(); P.assembly_jac()
+    assert P.nonlinear_gps()[0] > 0
+    argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-dt", dt, "-mat_law", "plastic", "-bc_type", 0]
+    with M.Macroc(argv) as m:
+        m.set_option("split_maxq", maxq)
+        m.set_option("split_wide", wide)
+        m.apply_bc_on_u(m.get_displacement(1))
+        m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac(); m.solve_Ax(); m.update_u()
+        m.set_u(u)
+        m.set_strains(); m.homogenize(); m.assembly_jac()
+        info = m.get_info()
+        assert info["storage"] == storage
+        if storage == 2:
+            assert info["split_slots"] > 32 and info["split_bits"] == (32 if wide else 16)
+        rp, ci, v = m.dump_csr()
+        assert np.array_equal(v, P.A_values())
+        x = np.random.default_rng(9).uniform(-1, 1, m.n)
+        y, y_ref = m.spmv(x), P.spmv(x)
+        absrow = np.add.reduceat(np.abs(v) * np.abs(x[ci]), rp[:-1])
+        assert np.all(np.abs(y - y_ref) <= 1e-14 * absrow + 1e-300)
 
 
 def test_time_loop_matches_oracle_log():

@@ -17,12 +17,13 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--grid", type=int, default=128)
 ap.add_argument("--ts", type=int, default=3, help="time steps (step 0 has zero load)")
 ap.add_argument("--mat-type", default="aij")
+ap.add_argument("--split", type=int, default=1, help="aij: -mat_aij_split (1: upper blocks + bf16 corrections)")
 ap.add_argument("--rtol", type=float, default=1e-8)
 ap.add_argument("--dt", type=float, default=0.01, help="load step (U = -ts*dt); 0.01 drives the circle plastic")
 a = ap.parse_args()
 N = a.grid
 m = M.Macroc(["-da_grid_x", N, "-da_grid_y", N, "-da_grid_z", N, "-mat_law", "plastic", "-ksp_rtol", repr(a.rtol),
-              "-dm_mat_type", a.mat_type, "-ts", a.ts, "-dt", a.dt])
+              "-dm_mat_type", a.mat_type, "-mat_aij_split", a.split, "-ts", a.ts, "-dt", a.dt])
 m.set_timing(True)
 steps = []
 t_all = time.perf_counter()
@@ -36,8 +37,10 @@ for ts in range(a.ts):
     print(json.dumps(steps[-1]), file=sys.stderr, flush=True)
 tot = time.perf_counter() - t_all
 nits = sum(s["newton_its"] for s in steps)
+info = m.get_info()
 print(json.dumps({"workload": f"config 5 path: {N}^3 non-linear Newton (J2 callback), {a.ts} time steps, dt {a.dt}",
-                  "mat_type": a.mat_type, "newton_its": nits, "cg_its": sum(sum(s["ksp_its"]) for s in steps),
+                  "mat_type": a.mat_type, "storage": {0: "aij-blocks", 1: "sbaij", 2: "aij-split"}[info["storage"]],
+                  "split_slots": info["split_slots"], "split_bits": info["split_bits"], "newton_its": nits, "cg_its": sum(sum(s["ksp_its"]) for s in steps),
                   "seconds": tot, "ms_per_newton_iter": tot / max(nits, 1) * 1e3,
                   "dof_per_s": 3 * N ** 3 * nits / tot, "steps": steps}))
 m.finish()
