@@ -1,62 +1,63 @@
-"""Interleaved in-process A/B of SpMV variants (DESIGN rule: compare variants on one device,
-one process, alternating rounds).  Usage: python tools/spmv_ab.py --grid 256 --mat aij --subl 0,8,16"""
+"""Interleaved in-process A/B of SpMV variants (DESIGN rule: compare variants on one device, one
+process, alternating rounds).  A variant is a set of mcx_set_option values, e.g.
+
+    python tools/spmv_ab.py --grid 256 --mat aij --variants "split_tx=0;split_tx=128;spmv_zblocks=512"
+
+Options not named by a variant are reset to --base before it runs."""
 import argparse
+import os
 import statistics
 import sys
-import os
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+
 import macroc_amd as M  # noqa: E402
 
 ap = argparse.ArgumentParser()
-ap.add_argument("--grid", type=int, default=256)
-ap.add_argument("--mat", default="aij")
-ap.add_argument("--subl", default="0")
-ap.add_argument("--kernels", default="0", help="sbaij kernels to compare: 0 pull, 1 z-marching")
-ap.add_argument("--nt", default="0", help="aij non-temporal matrix loads: 0,1")
-ap.add_argument("--zblocks", default="0", help="z-marching grid (0 = one resident round)")
+ap.add_argument("--grid", default="256", help="N or NX,NY,NZ")
+ap.add_argument("--mat", default="aij", choices=["aij", "sbaij"])
 ap.add_argument("--split", type=int, default=1, help="aij: -mat_aij_split")
-ap.add_argument("--splittx", default="0", help="aij-split tile widths to compare (0 = default)")
+ap.add_argument("--variants", default="split_tx=0", help="';'-separated option sets 'name=value,name=value'")
+ap.add_argument("--base", default="split_tx=0,spmv_zblocks=0", help="options every variant starts from")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--iters", type=int, default=20)
 a = ap.parse_args()
-N = a.grid
-m = M.Macroc(["-da_grid_x", N, "-da_grid_y", N, "-da_grid_z", N, "-dm_mat_type", a.mat, "-mat_aij_split", a.split])
+
+
+def parse(spec):
+    return [(kv.split("=")[0], float(kv.split("=")[1])) for kv in spec.split(",") if kv]
+
+
+g = [int(v) for v in a.grid.split(",")]
+NX, NY, NZ = g if len(g) == 3 else g * 3
+m = M.Macroc(["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-dm_mat_type", a.mat, "-mat_aij_split", a.split])
 m.apply_bc_on_u(m.get_displacement(1))
 m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
-m.spmv(m.b())  # p := b (padded), a realistic operand
-t = m.timing()
-nbytes = None
-import numpy as np  # noqa: E402
+base = parse(a.base)
+variants = [parse(v) for v in a.variants.split(";")]
 
-variants = [(int(s), int(kk), int(nt), int(zb), int(nu), int(tx)) for s in a.subl.split(",")
-            for kk in a.kernels.split(",") for nt in a.nt.split(",") for zb in a.zblocks.split(",")
-            for nu in ("0",) for tx in a.splittx.split(",")]
-res = {v: [] for v in variants}
+
+def select(v):
+    for k, val in base + v:
+        m.set_option(k, val)
+
+
 x = np.random.default_rng(1).uniform(-1, 1, m.n)
-ys = {}
+ys = []
 for v in variants:
-    m.set_option("spmv_subl", v[0])
-    m.set_option("spmv_kernel", v[1])
-    m.set_option("spmv_nt", v[2])
-    m.set_option("spmv_zblocks", v[3])
-    if a.mat == "aij" and a.split:
-        m.set_option("split_tx", v[5])
-    ys[v] = m.spmv(x)
-y0 = ys[variants[0]]
+    select(v)
+    ys.append(m.spmv(x))
+res = [[] for _ in variants]
 for r in range(a.rounds):
-    for v in variants:
-        m.set_option("spmv_subl", v[0])
-        m.set_option("spmv_kernel", v[1])
-        m.set_option("spmv_nt", v[2])
-        m.set_option("spmv_zblocks", v[3])
-        if a.mat == "aij" and a.split:
-            m.set_option("split_tx", v[5])
-        res[v].append(m.time_spmv(a.iters))
+    for q, v in enumerate(variants):
+        select(v)
+        res[q].append(m.time_spmv(a.iters))
 tb = m.timing()["spmv_bytes_per_launch"]
-for v in variants:
-    med = statistics.median(res[v])
-    rel = np.linalg.norm(ys[v] - y0) / np.linalg.norm(y0)
-    print(f"{a.mat} grid {N}^3 subl={v[0]:3d} kernel={v[1]} nt={v[2]} zb={v[3]} tx={v[5]}: median {med:.4f} ms  min {min(res[v]):.4f}  -> "
-          f"{tb / med / 1e6:.0f} GB/s (algorithmic {tb / 1e9:.2f} GB)  |y-y0|/|y0|={rel:.2e}")
+print(f"{a.mat} grid {NX}x{NY}x{NZ} storage {m.get_info()['storage']} algorithmic {tb / 1e9:.3f} GB per launch")
+for q, v in enumerate(variants):
+    med = statistics.median(res[q])
+    rel = np.linalg.norm(ys[q] - ys[0]) / np.linalg.norm(ys[0])
+    name = ",".join(f"{k}={val:g}" for k, val in v) or "(base)"
+    print(f"  {name:40s} median {med:.4f} ms  min {min(res[q]):.4f}  -> {tb / med / 1e6:.0f} GB/s  |y-y0|/|y0|={rel:.2e}")
 m.finish()
