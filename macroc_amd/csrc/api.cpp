@@ -1052,6 +1052,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.split_maxq = std::max(0, std::min(30, (int)value));
     return 0;
   }
+  if (!std::strcmp(name, "split_dbg")) {
+    c.split_dbg = std::max(0, std::min(2, (int)value));
+    return 0;
+  }
   if (!std::strcmp(name, "split_tx")) {
     const int v = (int)value;
     if (v != 0 && v != 64 && v != 128 && v != 256) {

@@ -1279,36 +1279,52 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
       // start); per lower block with corrections one x load, slot positions uniform.
       if (AIJS && ph == 2 && active) {
         const u32x4* Dn = reinterpret_cast<const u32x4*>(Dq) + (int64_t)(uc >> 6) * dl.Lq * 64 + (uc & 63);
-        double d0 = 0., d1 = 0., d2 = 0., z0 = 0., z1 = 0., z2 = 0.;
-        int prev = -1;
+        double d0 = 0., d1 = 0., d2 = 0.;
         const int per = dl.wide ? 4 : 8;
-        for (int t = 0; t < dl.Lq; t++) {  // uniform: 8 (bf16) or 4 (f32) slots per quad
-          const u32x4 w = t == 0 ? wpre[0] : (t == 1 ? wpre[1] : (t == 2 ? wpre[2] : __builtin_nontemporal_load(Dn + t * 64)));
+        // the slots held in wpre (24 bf16 / 12 f32) at unrolled positions: one 8-B x load per slot,
+        // all issued before the first use (one round trip, not one per block)
+        const int nfast = min(dl.L, 3 * per);
+        double xv[24];
 #pragma unroll
-          for (int e = 0; e < 8; e++) {
-            if (e >= per) break;
-            const int p = per * t + e;
-            if (p >= dl.L) break;
-            const int s = dl.s[p], nb = s / 9, rc = s - 9 * nb, r = rc / 3, cc = rc - 3 * r;
-            if (nb != prev) {
-              const int qn = pc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
-              z0 = x[3 * (int64_t)qn];
-              z1 = x[3 * (int64_t)qn + 1];
-              z2 = x[3 * (int64_t)qn + 2];
-              prev = nb;
-            }
-            double v;
-            if (dl.wide) {
-              v = (double)__uint_as_float(w[e & 3]);
-            } else {
-              const unsigned hw = w[e >> 1];
-              v = (double)__uint_as_float((e & 1) ? (hw & 0xffff0000u) : (hw << 16));
-            }
-            const double tv = v * (cc == 0 ? z0 : (cc == 1 ? z1 : z2));
-            if (r == 0) d0 += tv;
-            else if (r == 1) d1 += tv;
-            else d2 += tv;
+        for (int p = 0; p < 24; p++) {
+          xv[p] = 0.;
+          if (p < nfast) {
+            const int s = dl.s[p], nb = s / 9, cc = (s - 9 * nb) % 3;
+            const int qn = pc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
+            xv[p] = x[3 * (int64_t)qn + cc];
           }
+        }
+#pragma unroll
+        for (int p = 0; p < 24; p++) {
+          if (p >= nfast) continue;
+          const int r = (dl.s[p] % 9) / 3;
+          double v;
+          if (dl.wide) {
+            v = (double)__uint_as_float(wpre[p >> 2][p & 3]);
+          } else {
+            const unsigned hw = wpre[p >> 3][(p & 7) >> 1];
+            v = (double)__uint_as_float((p & 1) ? (hw & 0xffff0000u) : (hw << 16));
+          }
+          const double tv = v * xv[p];
+          if (r == 0) d0 += tv;
+          else if (r == 1) d1 += tv;
+          else d2 += tv;
+        }
+        for (int p = nfast; p < dl.L; p++) {  // beyond wpre (dense corrections): one slot at a time
+          const u32x4 w = __builtin_nontemporal_load(Dn + (p / per) * 64);
+          const int s = dl.s[p], nb = s / 9, rc = s - 9 * nb, r = rc / 3, cc = rc - 3 * r, e = p % per;
+          const int qn = pc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
+          double v;
+          if (dl.wide) {
+            v = (double)__uint_as_float(w[e & 3]);
+          } else {
+            const unsigned hw = w[e >> 1];
+            v = (double)__uint_as_float((e & 1) ? (hw & 0xffff0000u) : (hw << 16));
+          }
+          const double tv = v * x[3 * (int64_t)qn + cc];
+          if (r == 0) d0 += tv;
+          else if (r == 1) d1 += tv;
+          else d2 += tv;
         }
         cd0 = d0;
         cd1 = d1;
@@ -1388,15 +1404,20 @@ static void z_shape(int kern, int& ztx, int& zty) {
 template <int ZTX, int ZTY, bool AIJS = false>
 static void launch_symp(Ctx& c, const double* xpad, double* y, bool dot, bool gated, const ZTiling& zt, int nb) {
   const uint16_t* Dq = c.D;
+  DSlots dl = c.dsl;
+  if (c.split_dbg) {  // timing-only diagnostics (wrong products): 1 = loads, no corrections; 2 = neither
+    dl.L = 0;
+    if (c.split_dbg == 2) dl.Lq = 0;
+  }
   if (dot && gated)
     hipLaunchKernelGGL((k_spmv_symp<true, true, ZTX, ZTY, AIJS>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g, c.U,
-                       xpad, y, c.partials, c.cg, zt, Dq, c.dsl);
+                       xpad, y, c.partials, c.cg, zt, Dq, dl);
   else if (dot)
     hipLaunchKernelGGL((k_spmv_symp<true, false, ZTX, ZTY, AIJS>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g, c.U,
-                       xpad, y, c.partials, c.cg, zt, Dq, c.dsl);
+                       xpad, y, c.partials, c.cg, zt, Dq, dl);
   else
     hipLaunchKernelGGL((k_spmv_symp<false, false, ZTX, ZTY, AIJS>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g, c.U,
-                       xpad, y, c.partials, c.cg, zt, Dq, c.dsl);
+                       xpad, y, c.partials, c.cg, zt, Dq, dl);
 }
 
 template <int ZTX, int ZTY>

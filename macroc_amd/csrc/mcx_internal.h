@@ -127,6 +127,7 @@ struct Ctx {
   int fmt = FMT_V;           // storage the matrix is currently assembled in
   int aij_split = 1;
   int split_maxq = 4;
+  int split_dbg = 0;         // timing-only diagnostics of the split SpMV (option split_dbg)
   int split_wide = 0;        // force f32 corrections (testing the wide path)        // AIJ-split only while the corrections fit this many 16-B quads per node
   int split_tx = 0;          // AIJ-split tile width (0: by subdomain width; option split_tx)         // aij: assemble in FMT_SPLIT when every correction is exact in bf16
   DSlots dsl;
