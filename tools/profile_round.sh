@@ -1,0 +1,12 @@
+#!/bin/bash
+# tools/profile_round.sh TAG — the measurements behind the bench line, on the GPU box:
+# the default bench, the same command under rocprofv3 --kernel-trace --stats, and the PMC HBM
+# traffic passes of the headline SpMV (tools/pmc_spmv.sh).  Everything lands in gpurun_out/.
+set -euo pipefail
+TAG=${1:-r01}
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 420 python3 bench.py > gpurun_out/${TAG}_bench_default.json 2> gpurun_out/${TAG}_bench_default.log
+timeout -k 10 480 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- \
+  python3 bench.py > gpurun_out/${TAG}_bench_default_under_rocprof.json 2> gpurun_out/${TAG}_bench_rocprof.log
+bash tools/pmc_spmv.sh aij-split 256
