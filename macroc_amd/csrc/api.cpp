@@ -209,6 +209,7 @@ static int cg_solve(Ctx& c, int* its, double* rnorm, int* reason) {
     slot ^= 1;
     if (issued > cap) break;
   }
+  launch_cg_xfinal(c);  // the last iteration's VecAXPY(x, alpha, p), deferred by k_cg_pupdate
   MCX_HIP(hipStreamSynchronize(c.stream));
   CgState fin;
   MCX_HIP(hipMemcpy(&fin, c.cg, sizeof(CgState), hipMemcpyDeviceToHost));

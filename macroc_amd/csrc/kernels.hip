@@ -1471,7 +1471,10 @@ __global__ __launch_bounds__(TPB) void k_cg_init(Geo g, const double* __restrict
   }
 }
 
-// p <- z (i == 0) or z + (beta/betaold) p   (VecCopy / VecAYPX)
+// p <- z (i == 0) or z + (beta/betaold) p   (VecCopy / VecAYPX).  The previous iteration's
+// VecAXPY(x, alpha, p) is applied here, where p is read anyway (same operation and rounding as
+// in KSPSolve_CG, one iteration later; k_cg_xfinal applies the last one): the update kernel
+// then reads neither x nor p.
 template <bool NT>
 __device__ __forceinline__ void st(double* p, double v) {
   if constexpr (NT) __builtin_nontemporal_store(v, p);
@@ -1480,7 +1483,7 @@ __device__ __forceinline__ void st(double* p, double v) {
 
 template <bool NT>
 __global__ void k_cg_pupdate(Geo g, const double* __restrict__ z, double* __restrict__ ppad,
-                             const CgState* __restrict__ cg) {
+                             double* __restrict__ x, const CgState* __restrict__ cg) {
   if (cg->reason) return;
   int n = blockIdx.x * TPB + threadIdx.x;
   if (n >= g.nown) return;
@@ -1491,32 +1494,47 @@ __global__ void k_cg_pupdate(Geo g, const double* __restrict__ z, double* __rest
 #pragma unroll
     for (int d = 0; d < 3; d++) st<NT>(&ppad[3 * pc + d], z[3 * n + d]);
   } else {
-    const double bc = cg->bcoef;
+    const double bc = cg->bcoef, a = cg->alpha;
 #pragma unroll
-    for (int d = 0; d < 3; d++) st<NT>(&ppad[3 * pc + d], z[3 * n + d] + bc * ppad[3 * pc + d]);
+    for (int d = 0; d < 3; d++) {
+      const int q = 3 * n + d;
+      const double pv = ppad[3 * pc + d];
+      st<NT>(&x[q], x[q] + a * pv);
+      st<NT>(&ppad[3 * pc + d], z[q] + bc * pv);
+    }
   }
 }
 
-// x += a p; r += (-a) w; z = D^-1 r; partials z.z, z.r
+// the last iteration's x += alpha p (when that iteration reached its update)
+__global__ void k_cg_xfinal(Geo g, const double* __restrict__ ppad, double* __restrict__ x,
+                            const CgState* __restrict__ cg) {
+  if (!cg->xpend) return;
+  int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  const int pc = pad_of(g, i, j, k);
+  const double a = cg->alpha;
+#pragma unroll
+  for (int d = 0; d < 3; d++) x[3 * n + d] = x[3 * n + d] + a * ppad[3 * pc + d];
+}
+
+// r += (-a) w; z = D^-1 r; partials z.z, z.r   (x += a p: deferred to k_cg_pupdate)
 template <bool NT>
-__global__ __launch_bounds__(TPB) void k_cg_update(Geo g, const double* __restrict__ ppad, const double* __restrict__ w,
-                                                   const double* __restrict__ dinv, double* __restrict__ x,
+__global__ __launch_bounds__(TPB) void k_cg_update(Geo g, const double* __restrict__ w,
+                                                   const double* __restrict__ dinv,
                                                    double* __restrict__ r, double* __restrict__ z,
                                                    double* __restrict__ part, int nparts,
                                                    const CgState* __restrict__ cg) {
   __shared__ double sh[TPB / 64];
   if (cg->reason) return;
-  const double a = cg->alpha, ma = -a;
+  const double ma = -cg->alpha;
   int n = blockIdx.x * TPB + threadIdx.x;
   double zz = 0., zr = 0.;
   if (n < g.nown) {
-    int i, j, k;
-    node_ijk(g, n, i, j, k);
-    const int pc = pad_of(g, i, j, k);
 #pragma unroll
     for (int d = 0; d < 3; d++) {
       const int q = 3 * n + d;
-      st<NT>(&x[q], x[q] + a * ppad[3 * pc + d]);
       const double rv = r[q] + ma * w[q];
       st<NT>(&r[q], rv);
       const double zv = rv * dinv[q];
@@ -1544,6 +1562,7 @@ __device__ void cg_logic_init(CgState* s, double zz, double zr, double* hist) {
   s->its = 0;
   s->dpi = 0.;
   s->betaold = 0.;
+  s->xpend = 0;
   s->reason = converged_default(s, dp);
   if (s->reason) return;
   s->beta = zr;
@@ -1558,10 +1577,12 @@ __device__ void cg_logic_alpha(CgState* s, double dpi) {
   s->dpi = dpi;
   s->betaold = s->beta;
   if (dpi == 0.0 || (s->i > 0 && dpi * dpiold <= 0.0)) {
-    s->reason = MCX_KSP_DIVERGED_INDEFINITE_MAT;
+    s->reason = MCX_KSP_DIVERGED_INDEFINITE_MAT;  // before VecAXPY: the pending x update is none
+    s->xpend = 0;
     return;
   }
   s->alpha = s->beta / dpi;
+  s->xpend = 1;
 }
 
 __device__ void cg_logic_beta(CgState* s, double zz, double zr, double* hist) {
@@ -1964,13 +1985,17 @@ int cg_finish_init(Ctx& c) {
   return reduce_and_logic(c, 2, nb, RED_INIT, false);
 }
 
+void launch_cg_xfinal(Ctx& c) {
+  hipLaunchKernelGGL(k_cg_xfinal, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.p_pad, c.du, c.cg);
+}
+
 int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1) {
   const int nbn = (int)nblk(c.g.nown);
   const int nbs = (int)spmv_grid_blocks(c);
   if (c.cg_nt)
-    hipLaunchKernelGGL(k_cg_pupdate<true>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.cg);
+    hipLaunchKernelGGL(k_cg_pupdate<true>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg);
   else
-    hipLaunchKernelGGL(k_cg_pupdate<false>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.cg);
+    hipLaunchKernelGGL(k_cg_pupdate<false>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg);
   int rc = halo_exchange(c, c.p_pad);
   if (rc) return rc;
   if (ev0) MCX_HIP(hipEventRecord(ev0, c.stream));
@@ -1979,10 +2004,10 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1) {
   rc = reduce_and_logic(c, 1, nbs, RED_ALPHA, true);
   if (rc) return rc;
   if (c.cg_nt)
-    hipLaunchKernelGGL(k_cg_update<true>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.p_pad, c.w, c.dinv, c.du, c.r, c.z,
+    hipLaunchKernelGGL(k_cg_update<true>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.w, c.dinv, c.r, c.z,
                      c.partials, nbn, c.cg);
   else
-    hipLaunchKernelGGL(k_cg_update<false>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.p_pad, c.w, c.dinv, c.du, c.r, c.z,
+    hipLaunchKernelGGL(k_cg_update<false>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.w, c.dinv, c.r, c.z,
                      c.partials, nbn, c.cg);
   rc = reduce_and_logic(c, 2, nbn, RED_BETA, true);
   return rc;

@@ -42,7 +42,8 @@ struct Geo {
 struct CgState {
   double beta, betaold, dpi, dpiold, alpha, dp, ttol, rnorm0, bcoef;
   double rtol, abstol, dtol;
-  int i, its, reason, maxits, hist_on, pad;
+  int i, its, reason, maxits, hist_on;
+  int xpend;  // x += alpha p of the last iteration not yet applied (k_cg_pupdate / k_cg_xfinal apply it)
 };
 
 struct Material {
@@ -204,6 +205,7 @@ int build_split(Ctx& c, bool* exact);  // AIJ-split corrections from U + Ke (exa
 void launch_jacobi(Ctx& c);
 void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated);
 void launch_update_u(Ctx& c);
+void launch_cg_xfinal(Ctx& c);
 void launch_reduce(Ctx& c, int nvals, int nparts, double* out);
 void launch_cg_init(Ctx& c);
 int cg_iteration(Ctx& c, hipEvent_t spmv_start, hipEvent_t spmv_stop);
