@@ -20,11 +20,14 @@ ap.add_argument("--mat-type", default="aij")
 ap.add_argument("--split", type=int, default=1, help="aij: -mat_aij_split (1: upper blocks + bf16 corrections)")
 ap.add_argument("--rtol", type=float, default=1e-8)
 ap.add_argument("--dt", type=float, default=0.01, help="load step (U = -ts*dt); 0.01 drives the circle plastic")
+ap.add_argument("--maxq", type=int, default=None, help="aij-split: split_maxq (correction quads per node allowed)")
 a = ap.parse_args()
 N = a.grid
 m = M.Macroc(["-da_grid_x", N, "-da_grid_y", N, "-da_grid_z", N, "-mat_law", "plastic", "-ksp_rtol", repr(a.rtol),
               "-dm_mat_type", a.mat_type, "-mat_aij_split", a.split, "-ts", a.ts, "-dt", a.dt])
 m.set_timing(True)
+if a.maxq is not None:
+    m.set_option("split_maxq", a.maxq)
 steps = []
 t_all = time.perf_counter()
 for ts in range(a.ts):
