@@ -1167,15 +1167,21 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
   double dot = 0.;
   double a0 = 0., a1 = 0., a2 = 0.;  // this plane's node: lower sum so far
   double n0 = 0., n1 = 0., n2 = 0.;  // next plane's node: lower dz=-1 sum so far
-  // lower term nb of the node at padded index pc: from LDS slot or pulled
-  auto term = [&](int nb, int slot, bool from_lds, int pcn, int ucn, double& c0, double& c1, double& c2) {
+  // lower term nb of the node (i, j, kt) at padded index pcn: from LDS slot or pulled.  A source
+  // outside the global domain is a zero ghost (x = 0 there): its term is +0 without the loads
+  auto term = [&](int nb, int slot, bool from_lds, int pcn, int ucn, int kt, double& c0, double& c1, double& c2) {
     if (from_lds) {
       c0 = buf[slot][0][me];
       c1 = buf[slot][1][me];
       c2 = buf[slot][2][me];
     } else {
       const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
-      ut_x2(U, x, ucn + dx + dy * g.UX + dz * g.UXY, pcn + dx + dy * PX + dz * PXY, 26 - nb, c0, c1, c2);
+      const unsigned gx = g.xs + i + dx, gy = g.ys + j + dy, gz = g.zs + kt + dz;
+      if (gx >= (unsigned)g.NX || gy >= (unsigned)g.NY || gz >= (unsigned)g.NZ) {
+        c0 = c1 = c2 = 0.;
+      } else {
+        ut_x2(U, x, ucn + dx + dy * g.UX + dz * g.UXY, pcn + dx + dy * PX + dz * PXY, 26 - nb, c0, c1, c2);
+      }
     }
   };
   for (int k = k0; k < k1; k++) {
@@ -1187,7 +1193,7 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
 #pragma unroll
       for (int q = 0; q < 9; q++) {  // canonical order 8 | 4 5 6 7 | 0 1 2 3
         double c0, c1, c2;
-        term(q == 0 ? 8 : (q <= 4 ? q + 3 : q - 5), 0, false, pc, uc, c0, c1, c2);
+        term(q == 0 ? 8 : (q <= 4 ? q + 3 : q - 5), 0, false, pc, uc, k, c0, c1, c2);
         a0 += c0;
         a1 += c1;
         a2 += c2;
@@ -1338,7 +1344,7 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
           for (int nb = 9; nb <= 12; nb++) {
             const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1;
             double c0, c1, c2;
-            term(nb, (26 - nb) - lo, in_tile(dx, dy), pc, uc, c0, c1, c2);
+            term(nb, (26 - nb) - lo, in_tile(dx, dy), pc, uc, k, c0, c1, c2);
             a0 += c0;
             a1 += c1;
             a2 += c2;
@@ -1353,7 +1359,7 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
             if (nb < nb_lo || nb > nb_hi) continue;
             const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1;
             double c0, c1, c2;
-            term(nb, (26 - nb) - lo, in_tile(dx, dy), pc + PXY, uc + g.UXY, c0, c1, c2);
+            term(nb, (26 - nb) - lo, in_tile(dx, dy), pc + PXY, uc + g.UXY, k + 1, c0, c1, c2);
             n0 += c0;
             n1 += c1;
             n2 += c2;
