@@ -1132,7 +1132,10 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
                                                         ZTiling zt, const uint16_t* __restrict__ Dq = nullptr,
                                                         DSlots dl = DSlots()) {
   constexpr int T = TX * TY;
+  // y-edge terms computed by helper threads (TY >= 4: at most 4 TX = T of them per phase)
+  constexpr bool HELP = TY >= 4;
   __shared__ double buf[5][3][T];
+  __shared__ double edge[HELP ? 3 : 1][HELP ? T : 1];
   __shared__ double sh[T / 64];
   if (GATED && cg->reason) return;
   const int b = blockIdx.x;
@@ -1208,16 +1211,6 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
     }
     n0 = n1 = n2 = 0.;
     double cd0 = 0., cd1 = 0., cd2 = 0.;  // AIJ-split corrections of this plane's node
-    // AIJ-split: the first 24 corrections of this node, loaded before the phases (overlapped)
-    u32x4 wpre[3] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
-    if constexpr (AIJS) {
-      if (active) {
-        const u32x4* Dn = reinterpret_cast<const u32x4*>(Dq) + (int64_t)(uc >> 6) * dl.Lq * 64 + (uc & 63);
-#pragma unroll
-        for (int t = 0; t < 3; t++)
-          if (t < dl.Lq) wpre[t] = __builtin_nontemporal_load(Dn + t * 64);
-      }
-    }
 #pragma unroll
     for (int ph = 0; ph < 3; ph++) {
       const int lo = ph == 0 ? 14 : (ph == 1 ? 19 : 23), hi = ph == 0 ? 18 : (ph == 1 ? 22 : 26);
@@ -1290,20 +1283,21 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
         // the slots held in wpre (24 bf16 / 12 f32) at unrolled positions: one 8-B x load per slot,
         // all issued before the first use (one round trip, not one per block)
         const int nfast = min(dl.L, 3 * per);
+        // the first 24 corrections of this node (3 quads), loaded with the x gathers below
+        u32x4 wpre[3] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
+#pragma unroll
+        for (int t = 0; t < 3; t++)
+          if (t < dl.Lq) wpre[t] = __builtin_nontemporal_load(Dn + t * 64);
         double xv[24];
 #pragma unroll
         for (int p = 0; p < 24; p++) {
           xv[p] = 0.;
-          if (p < nfast) {
-            const int s = dl.s[p], nb = s / 9, cc = (s - 9 * nb) % 3;
-            const int qn = pc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
-            xv[p] = x[3 * (int64_t)qn + cc];
-          }
+          if (p < nfast) xv[p] = x[3 * (int64_t)pc + (dl.xc[p] >> 2)];
         }
 #pragma unroll
         for (int p = 0; p < 24; p++) {
           if (p >= nfast) continue;
-          const int r = (dl.s[p] % 9) / 3;
+          const int r = dl.xc[p] & 3;
           double v;
           if (dl.wide) {
             v = (double)__uint_as_float(wpre[p >> 2][p & 3]);
@@ -1336,15 +1330,52 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
         cd1 = d1;
         cd2 = d2;
       }
+      // Edge terms: the lower terms the tile's y-edge rows would pull after the barrier (row 0:
+      // sources at dy = -1, row TY-1: dy = +1), computed now by one helper thread each into
+      // edge[][h] (the same expression as the pull), so no wave waits on a chain of pulls there.
+      //   ph 0: h < 3 TX: row 0, this plane, nb 9 + h / TX;  3 TX <= h < 4 TX: row TY-1, next plane, nb 8
+      //   ph 1: h < 2 TX: row TY-1, next plane, nb 6 + h / TX;  ph 2: h < 3 TX: row 0, next plane, nb h / TX
+      if constexpr (HELP) {
+        const int grp = me / TX, it = txi * TX + me % TX;  // group: wave-uniform (TX % 64 == 0)
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          const int nbh = ph == 0 ? (q < 3 ? 9 + q : 8) : (ph == 1 ? (q < 2 ? 6 + q : -1) : (q < 3 ? q : -1));
+          if (nbh < 0 || grp != q) continue;
+          const bool nxt = !(ph == 0 && q < 3);
+          const int jt = tyi * TY + ((ph == 0 && q == 3) || ph == 1 ? TY - 1 : 0);
+          if (it < g.nx && jt < g.ny && (!nxt || has_next)) {
+            const int kt = k + (nxt ? 1 : 0);
+            const int dx = nbh % 3 - 1, dy = (nbh / 3) % 3 - 1, dz = nbh / 9 - 1;
+            const unsigned gx = g.xs + it + dx, gy = g.ys + jt + dy, gz = g.zs + kt + dz;
+            double c0 = 0., c1 = 0., c2 = 0.;
+            if (gx < (unsigned)g.NX && gy < (unsigned)g.NY && gz < (unsigned)g.NZ)
+              ut_x2(U, x, u_of(g, it, jt, kt) + dx + dy * g.UX + dz * g.UXY,
+                    (it + 1 + dx) + (jt + 1 + dy) * PX + (kt + 1 + dz) * PXY, 26 - nbh, c0, c1, c2);
+            edge[0][me] = c0;
+            edge[1][me] = c1;
+            edge[2][me] = c2;
+          }
+        }
+      }
       __syncthreads();
       if (active) {
+        // lower term nb: from the helpers' edge[] (y-edge rows), the LDS exchange or pulled now
+        auto term2 = [&](int nb, int eidx, int pcn, int ucn, int kt, double& c0, double& c1, double& c2) {
+          const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1;
+          if (HELP && dy != 0 && (ly + dy < 0 || ly + dy >= TY)) {
+            c0 = edge[0][eidx];
+            c1 = edge[1][eidx];
+            c2 = edge[2][eidx];
+          } else {
+            term(nb, (26 - nb) - lo, in_tile(dx, dy), pcn, ucn, kt, c0, c1, c2);
+          }
+        };
         if (ph == 0) {
           // this plane's node: dz = 0 lower terms nb 9..12 (sources pushed nbp 17..14)
 #pragma unroll
           for (int nb = 9; nb <= 12; nb++) {
-            const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1;
             double c0, c1, c2;
-            term(nb, (26 - nb) - lo, in_tile(dx, dy), pc, uc, k, c0, c1, c2);
+            term2(nb, (nb - 9) * TX + lx, pc, uc, k, c0, c1, c2);
             a0 += c0;
             a1 += c1;
             a2 += c2;
@@ -1357,9 +1388,9 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
 #pragma unroll
           for (int nb = 0; nb <= 8; nb++) {
             if (nb < nb_lo || nb > nb_hi) continue;
-            const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1;
+            const int eidx = (ph == 0 ? 3 * TX : 0) + (ph == 1 ? nb - 6 : (ph == 2 ? nb : 0)) * TX + lx;
             double c0, c1, c2;
-            term(nb, (26 - nb) - lo, in_tile(dx, dy), pc + PXY, uc + g.UXY, k + 1, c0, c1, c2);
+            term2(nb, eidx, pc + PXY, uc + g.UXY, k + 1, c0, c1, c2);
             n0 += c0;
             n1 += c1;
             n2 += c2;
@@ -1830,6 +1861,11 @@ int build_split(Ctx& c, bool* exact) {
       if (hm[b] >> q & 1) dl.s[dl.L++] = (unsigned char)(b * 9 + q);
   }
   dl.Lq = dl.wide ? (dl.L + 3) / 4 : (dl.L + 7) / 8;
+  for (int p = 0; p < std::min(dl.L, 24); p++) {  // the walk's x gather offsets (k_spmv_symp)
+    const int s = dl.s[p], nb = s / 9, rc = s - 9 * nb;
+    const int off = (nb % 3 - 1) + ((nb / 3) % 3 - 1) * c.g.PX + (nb / 9 - 1) * c.g.PX * c.g.PY;
+    dl.xc[p] = (3 * off + rc % 3) * 4 + rc / 3;
+  }
   if (dl.Lq > c.split_maxq) {  // dense corrections: the AIJ blocks stream is faster
     *exact = false;
     return 0;

@@ -80,6 +80,7 @@ struct DSlots {
   unsigned char s[120];     // ascending active slot ids (at most 117 + 3)
   unsigned short m9[14];    // per lower block nb (13: diagonal): active (r*3+c) bits
   unsigned char pos[14];    // per block: index of its first active slot
+  int xc[24];               // slot p < 24: (x offset from 3 * padded index of the row node) * 4 + row
 };
 
 // In-process transport: several contexts (one host thread each) exchanging halos and partial
