@@ -193,6 +193,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
+        if torch.cuda.is_available() and not args.same_device:
+            torch.cuda.set_device(local)  # torch's own synchronize() then targets this rank's GPU
     px, py, pz = rank_grid(world)
     G = args.grid
     NX, NY, NZ = G * px, G * py, G * pz
