@@ -36,7 +36,7 @@ STORAGE_ARGS = {"aij": ["-dm_mat_type", "aij"], "aij-blocks": ["-dm_mat_type", "
                 "sbaij": ["-dm_mat_type", "sbaij"]}
 STORAGE_NAME = {0: "aij-blocks", 1: "sbaij", 2: "aij-split"}
 KERNEL_NAME = {0: "k_spmv (AIJ stencil blocks, CPU AIJ row order)",
-               1: "k_spmv_symz (SBAIJ z-marching tiles)",
+               1: "k_spmv_symp (SBAIJ phased z-marching tiles)",
                2: "k_spmv_symp<AIJS> (AIJ-split: upper blocks + bf16 lower corrections, z-marching)"}
 
 

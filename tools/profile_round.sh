@@ -10,3 +10,4 @@ timeout -k 10 420 python3 bench.py > gpurun_out/${TAG}_bench_default.json 2> gpu
 timeout -k 10 480 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- \
   python3 bench.py > gpurun_out/${TAG}_bench_default_under_rocprof.json 2> gpurun_out/${TAG}_bench_rocprof.log
 bash tools/pmc_spmv.sh aij-split 256
+bash tools/pmc_spmv.sh sbaij 256
