@@ -212,6 +212,26 @@ def test_ksp_edge_cases():
         assert its == 0 and reason in (2, 3)
 
 
+@pytest.mark.parametrize("maxits", [1, 2, 5])
+def test_ksp_maxits_iterate(maxits):
+    """DIVERGED_ITS after 1, 2, 5 iterations returns the iterate of the last one: KSPSolve_CG
+    applies x += alpha p before its stopping test, and the device loop defers that update into
+    the next p update (k_cg_xfinal applies the last one)."""
+    N, rtol = 8, 1e-12
+    P = O.Problem(N, N, N, rtol=rtol, maxits=maxits)
+    P.apply_bc_u(P.get_displacement(1))
+    P.set_strains(); P.homogenize(); P.assembly_res(); P.assembly_jac()
+    out = P.solve()
+    with M.Macroc(argv_for(N, N, N, rtol, ["-ksp_max_it", maxits])) as m:
+        m.apply_bc_on_u(m.get_displacement(1))
+        m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
+        its, rn, reason = m.solve_Ax()
+        assert (its, reason) == (out["its"], out["reason"]) == (maxits, -3)
+        du = m.du()
+    assert np.linalg.norm(du) > 0
+    assert np.linalg.norm(du - P.du()) <= 1e-12 * np.linalg.norm(P.du())
+
+
 def _solve_big(N, rtol):
     m = M.Macroc(argv_for(N, N, N, rtol))
     m.apply_bc_on_u(m.get_displacement(1))
