@@ -888,10 +888,15 @@ struct ZTiling {
 
 static ZTiling z_tiling(const Geo& g, int ztx, int zty, int want) {
   ZTiling t;
-  if (want <= 0) want = g.ncu * std::max(1, 1024 / (ztx * zty));  // one resident round
   t.ntx = (g.nx + ztx - 1) / ztx;
   t.nty = (g.ny + zty - 1) / zty;
   const int tiles = t.ntx * t.nty;
+  if (want <= 0) {
+    // one resident round, but at least two planes per chunk: a one-plane chunk pulls all of
+    // its lower terms (64^3: 0.083 ms at one plane, 0.071 ms at two, tools/spmv_ab.py)
+    want = g.ncu * std::max(1, 1024 / (ztx * zty));
+    want = std::min(want, tiles * std::max(1, g.nz / 2));
+  }
   t.nzc = std::max(1, std::min(g.nz, (want + tiles - 1) / tiles));
   t.kc = (g.nz + t.nzc - 1) / t.nzc;
   t.nzc = (g.nz + t.kc - 1) / t.kc;
