@@ -145,3 +145,38 @@ def _multirank(name, sbaij, extra=(), split=False):
         assert np.linalg.norm(du - duref) <= tol * np.linalg.norm(duref)
     else:
         assert not du.any()
+
+
+@pytest.mark.parametrize("mat", ["aij", "sbaij", "sbaij-phased"])
+@pytest.mark.parametrize("grid,procs", [((140, 10, 8), (2, 1, 1)), ((132, 12, 12), (2, 2, 2))])
+def test_multirank_full_tiles(grid, procs, mat):
+    """Subdomains wide enough for full z-marching tiles (64 x 4) next to partial ones: internal
+    subdomain faces at a tile's lane 0 and row 0 (helper-computed edge terms pulling real
+    ghosts), at partial tiles' last lanes and rows (pulled by the target), and the global
+    boundary (skipped ghosts).  Rows within rounding of the one-rank oracle's product, the
+    solve within the north-star tolerance."""
+    NX, NY, NZ = grid
+    px, py, pz = procs
+    nr, rtol = px * py * pz, 1e-10
+    argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
+            "-da_processors_z", pz, "-ksp_rtol", repr(rtol), "-dm_mat_type", mat.split("-")[0]]
+    opts = {"aij": [("split_maxq", 30)], "sbaij": [], "sbaij-phased": [("spmv_kernel", 8)]}[mat]  # 8: phased 64x4
+    ref = O.Problem(NX, NY, NZ, rtol=rtol)
+    ref.apply_bc_u(ref.get_displacement(0))
+    ref.apply_bc_u(ref.get_displacement(1))
+    ref.set_strains(); ref.homogenize(); ref.assembly_res(); ref.assembly_jac()
+    if mat.startswith("sbaij"):
+        ref.sbaij_mirror()
+    rp1, ci1 = ref.csr()
+    v1 = ref.A_values()
+    x = np.random.default_rng(11).uniform(-1, 1, ref.ndofs)
+    y1 = ref.spmv(x)
+    absrow = np.add.reduceat(np.abs(v1) * np.abs(x[ci1]), rp1[:-1])
+    ref.solve()
+    duref = ref.du()
+    out = run_group(argv, nr, newton_step(x, opts))
+    du = np.zeros(ref.ndofs)
+    for o in out:
+        assert np.all(np.abs(o["y"] - y1[o["nat"]]) <= 1e-14 * absrow[o["nat"]] + 1e-300)
+        du[o["nat"]] = o["du"]
+    assert np.linalg.norm(du - duref) <= 1e-8 * np.linalg.norm(duref)
