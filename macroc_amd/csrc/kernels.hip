@@ -1562,16 +1562,19 @@ __global__ void k_cg_xfinal(Geo g, const double* __restrict__ ppad, double* __re
 }
 
 // r += (-a) w; z = D^-1 r; partials z.z, z.r   (x += a p: deferred to k_cg_pupdate)
+// 1024-thread blocks: a quarter of the partials for k_reduce (one block reads them all)
+static constexpr int UTPB = 1024;
+
 template <bool NT>
-__global__ __launch_bounds__(TPB) void k_cg_update(Geo g, const double* __restrict__ w,
+__global__ __launch_bounds__(UTPB) void k_cg_update(Geo g, const double* __restrict__ w,
                                                    const double* __restrict__ dinv,
                                                    double* __restrict__ r, double* __restrict__ z,
                                                    double* __restrict__ part, int nparts,
                                                    const CgState* __restrict__ cg) {
-  __shared__ double sh[TPB / 64];
+  __shared__ double sh[UTPB / 64];
   if (cg->reason) return;
   const double ma = -cg->alpha;
-  int n = blockIdx.x * TPB + threadIdx.x;
+  int n = blockIdx.x * UTPB + threadIdx.x;
   double zz = 0., zr = 0.;
   if (n < g.nown) {
 #pragma unroll
@@ -1585,8 +1588,8 @@ __global__ __launch_bounds__(TPB) void k_cg_update(Geo g, const double* __restri
       zr += zv * rv;
     }
   }
-  double s0 = block_sum<TPB>(zz, sh);
-  double s1 = block_sum<TPB>(zr, sh);
+  double s0 = block_sum<UTPB>(zz, sh);
+  double s1 = block_sum<UTPB>(zr, sh);
   if (threadIdx.x == 0) {
     part[blockIdx.x] = s0;
     part[nparts + blockIdx.x] = s1;
@@ -2039,6 +2042,7 @@ void launch_cg_xfinal(Ctx& c) {
 int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1) {
   const int nbn = (int)nblk(c.g.nown);
   const int nbs = (int)spmv_grid_blocks(c);
+  const int nbu = (int)((c.g.nown + UTPB - 1) / UTPB);
   if (c.cg_nt)
     hipLaunchKernelGGL(k_cg_pupdate<true>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg);
   else
@@ -2051,12 +2055,12 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1) {
   rc = reduce_and_logic(c, 1, nbs, RED_ALPHA, true);
   if (rc) return rc;
   if (c.cg_nt)
-    hipLaunchKernelGGL(k_cg_update<true>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.w, c.dinv, c.r, c.z,
-                     c.partials, nbn, c.cg);
+    hipLaunchKernelGGL(k_cg_update<true>, dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, c.dinv, c.r, c.z,
+                     c.partials, nbu, c.cg);
   else
-    hipLaunchKernelGGL(k_cg_update<false>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.w, c.dinv, c.r, c.z,
-                     c.partials, nbn, c.cg);
-  rc = reduce_and_logic(c, 2, nbn, RED_BETA, true);
+    hipLaunchKernelGGL(k_cg_update<false>, dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, c.dinv, c.r, c.z,
+                     c.partials, nbu, c.cg);
+  rc = reduce_and_logic(c, 2, nbu, RED_BETA, true);
   return rc;
 }
 
