@@ -1279,8 +1279,8 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
       // AIJ-split corrections of this plane's node (independent of the LDS exchange), computed
       // while the block waits at the phase-2 barrier; exact AIJ lower blocks = mirrored upper
       // (summed in the gathers) + the bf16 corrections of the active slots, ascending nb then c
-      // per row, added after the lower sum.  8 corrections per 16-B load (prefetched at plane
-      // start); per lower block with corrections one x load, slot positions uniform.
+      // per row, added after the lower sum.  8 corrections per 16-B quad (prefetched at plane
+      // start); one 8-B x gather per slot, all issued before the first product (see below).
       if (AIJS && ph == 2 && active) {
         const u32x4* Dn = reinterpret_cast<const u32x4*>(Dq) + (int64_t)(uc >> 6) * dl.Lq * 64 + (uc & 63);
         double d0 = 0., d1 = 0., d2 = 0.;
