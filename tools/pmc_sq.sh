@@ -11,12 +11,12 @@ PASSES=(
   "TCP_TCC_READ_REQ_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum"
 )
 for mat in aij sbaij; do
-  K=0; [ $mat = sbaij ] && K=0,4,7
+  V="split_dbg=0"; [ $mat = sbaij ] && V="spmv_kernel=11"
   p=0
   for C in "${PASSES[@]}"; do
     p=$((p+1))
     timeout -k 10 300 rocprofv3 --pmc $C --kernel-include-regex 'k_spmv' -d $OUT/$mat-$p -o run --output-format csv -- \
-      python3 tools/spmv_ab.py --mat $mat --kernels $K --rounds 1 --iters 5 --grid 256 > $OUT/$mat-$p.log 2>&1
+      python3 tools/spmv_ab.py --mat $mat --variants "$V" --base "" --rounds 1 --iters 5 --grid 256 > $OUT/$mat-$p.log 2>&1
   done
 done
 python3 - <<'PY'
