@@ -1151,11 +1151,11 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
   const int per = max(nty_here, 0) * zt.ntx * zt.nzc;
   const bool blk_ok = t8 < per;
   int tyi = 0, txi = 0, zc = 0;
-  if (blk_ok) {
-    zc = t8 % zt.nzc;
-    const int r = t8 / zt.nzc;
-    txi = r % zt.ntx;
-    tyi = ty0 + r / zt.ntx;
+  if (blk_ok) {  // x fastest, then the slab's tile rows, then z-chunks
+    txi = t8 % zt.ntx;
+    const int r = t8 / zt.ntx;
+    tyi = ty0 + r % nty_here;
+    zc = r / nty_here;
   }
   if (!blk_ok) {  // whole block idle (uniform): still write the partial
     if (DOT && threadIdx.x == 0) part[blockIdx.x] = 0.;
