@@ -10,13 +10,19 @@ the same state, nothing is cached across steps.  Workload: 256^3 nodes per GPU
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Rank 0 prints ONE JSON line (see the contract in the task statement / DESIGN.md §6).
+Rank 0 prints ONE JSON line (see the contract in the task statement / DESIGN.md §6) as soon as
+the headline and the CPU baseline are measured; `--variants aij-blocks,sbaij` then measures other
+storages (1 warmup + 1 step each, on stderr) while the `--budget` wall time lasts.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
+
+T_START = time.perf_counter()  # wall-clock budget of the whole invocation (variants are guarded by it)
 
 # torch first: the library then binds to the HIP runtime torch already loaded (one runtime per
 # process); torch is only plumbing here (process group for barriers / max-over-ranks).
@@ -62,15 +68,45 @@ def pmc_traffic(mat_type, NX, NY, NZ):
         return None
 
 
-def cpu_baseline(N, threads, gpu_its, rtol, ndofs_target, nelem_target, nnz_target, cg_cap=200):
+def host_cores():
+    """CPUs this process may really use: the affinity mask, capped by a cgroup v2 CPU quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def oracle_timing_build():
+    """-O3 -march=native build of the oracle for this host (timing only; -ffp-contract=off kept,
+    so it computes the same numbers as the checker build).  Falls back to the in-tree -O2 build."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = os.path.join(tempfile.mkdtemp(prefix="mcx_oracle_"), "liboracle_native.so")
+    cmd = ["gcc", "-O3", "-march=native", "-fPIC", "-ffp-contract=off", "-fopenmp", "-std=gnu11", "-shared", "-o",
+           out, os.path.join(here, "oracle", "oracle.c"), "-lm"]
+    try:
+        subprocess.run(cmd, check=True, timeout=120, capture_output=True)
+        return out, "gcc -O3 -march=native -ffp-contract=off"
+    except (OSError, subprocess.SubprocessError):
+        return None, "gcc -O2 (in-tree build; the -march=native build failed)"
+
+
+def cpu_baseline(N, threads, gpu_its, rtol, ndofs_target, nelem_target, nnz_target, cg_cap):
     """The oracle — the C restatement of the reference path, its MPI ranks run as OpenMP threads
-    (one emulated rank per thread, PETSc stash / per-rank dot semantics) — on an N^3 sample of
+    (one emulated rank per host core, PETSc stash / per-rank dot semantics) — on an N^3 sample of
     the same workload: full assembly + homogenize + residual, then `cg_cap` CG iterations.  Its
     per-element assembly time and per-(CG iteration x nonzero) time are scaled to the target
     grid with the GPU run's CG iteration count."""
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from oracle import oracle as O
 
+    path, build = oracle_timing_build()
+    if path:
+        O.use_library(path)
     used = O.set_threads(threads)
     P = O.Problem(N, N, N, nranks=used, rtol=rtol, maxits=cg_cap)
     P.apply_bc_u(P.get_displacement(0))
@@ -98,22 +134,24 @@ def cpu_baseline(N, threads, gpu_its, rtol, ndofs_target, nelem_target, nnz_targ
         "unit": "DOF/s",
         "cores": used,
         "kind": "port",
-        "sample": (f"oracle/ (C restatement of the reference path, gcc -O2, {used} OpenMP threads = {used} emulated "
-                   f"MPI ranks) on {N}^3: assembly {t2 - t0:.1f} s, {out['its']} CG its {t3 - t2:.1f} s; "
-                   f"per-element and per-(CG-iteration x nonzero) times scaled to the GPU workload with its "
-                   f"{gpu_its} CG iterations"),
+        "sample": (f"oracle/ (C restatement of the reference path, {build}, {used} OpenMP threads = {used} emulated "
+                   f"MPI ranks, one per usable host core) on {N}^3: assembly {t2 - t0:.1f} s, {out['its']} CG its "
+                   f"{t3 - t2:.1f} s; per-element and per-(CG-iteration x nonzero) times scaled to the GPU workload "
+                   f"with its {gpu_its} CG iterations"),
         "sample_seconds": t4 - t0,
         "extrapolated_step_seconds": t_target,
     }
 
 
-def measure(argv, rank, world, comm_id, args):
-    """Setup + warmup + timed steps of one configuration; returns the timings of this rank."""
+def measure(argv, rank, world, comm_id, args, steps, warmup):
+    """Setup + warmup + timed steps of one configuration; returns the timings of this rank.
+    Timing mode only records HIP events on the compute stream (no host waits): one event pair
+    per phase and per SpMV launch of the first 256 CG iterations of each solve."""
     t_setup = time.perf_counter()
     m = M.Macroc(argv, rank=rank, nranks=world, comm_id=comm_id)
     m.set_timing(True)
     info = m.info
-    log(f"[rank {rank}] {argv[-1]}: setup {time.perf_counter() - t_setup:.1f}s, device GB "
+    log(f"[rank {rank}] {' '.join(map(str, argv))}: setup {time.perf_counter() - t_setup:.1f}s, device GB "
         f"{info['device_bytes'] / 1e9:.1f}, local {info['nx']}x{info['ny']}x{info['nz']}")
     U = m.get_displacement(1)
 
@@ -135,17 +173,21 @@ def measure(argv, rank, world, comm_id, args):
         if world > 1:
             dist.barrier()
 
-    for w in range(args.warmup):
+    t_warm = []
+    for w in range(warmup):
         t = time.perf_counter()
         r = step()
-        log(f"[rank {rank}] warmup {w}: {time.perf_counter() - t:.2f}s its={r[1]}")
+        m.synchronize()
+        t_warm.append(time.perf_counter() - t)
+        log(f"[rank {rank}] warmup {w}: {t_warm[-1]:.2f}s its={r[1]}")
     barrier_sync()
     t0 = time.perf_counter()
-    for s in range(args.steps):
-        res, its, rn, reason = step()
+    for s in range(steps):
+        res, its, rn, reason = step()  # the solve's result readback already waited for the stream
         log(f"[rank {rank}] step {s}: its={its} reason={reason} |RES|={res:.6e} rnorm={rn:.3e}")
     barrier_sync()
     dt = time.perf_counter() - t0
+    log(f"[rank {rank}] {steps} steps: {dt:.2f}s, its={its} reason={reason} |RES|={res:.6e} rnorm={rn:.3e}")
     if world > 1:
         tt = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -166,10 +208,14 @@ def measure(argv, rank, world, comm_id, args):
             loc = tt.numpy()
         check = {"true_rel_residual": float(np.sqrt(loc[0] / loc[1])), "ksp_reason": int(reason)}
     m.finish()
+    nloc = info["ndofs_local"]
+    # PETSc AIJ bytes of the same SpMV (int32 col, int64 rowptr, x once, y once): SURVEY §8(d)
+    csr_bytes = info["nnz_local"] * 12 + (nloc + 1) * 8 + 2 * nloc * 8
     return {"its": its, "tm": tm, "info": info, "check": check, "spmv_avg_ms": spmv_avg_ms, "spmv_bytes": spmv_bytes,
-            "storage": STORAGE_NAME[storage["storage"]], "storage_id": storage["storage"],
+            "csr_bytes": csr_bytes, "storage": STORAGE_NAME[storage["storage"]], "storage_id": storage["storage"],
             "split_slots": storage["split_slots"], "split_bits": storage["split_bits"],
-            "achieved": spmv_bytes / (spmv_avg_ms * 1e-3) / 1e9, "ms_step": dt / args.steps * 1e3}
+            "achieved": spmv_bytes / (spmv_avg_ms * 1e-3) / 1e9, "ms_step": dt / max(steps, 1) * 1e3,
+            "warmup_s": t_warm}
 
 
 def main():
@@ -179,13 +225,15 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--grid", type=int, default=256, help="nodes per direction per GPU")
     ap.add_argument("--rtol", type=float, default=1e-8)
-    ap.add_argument("--cpu-sample", type=int, default=96, help="oracle sample grid (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16)
+    ap.add_argument("--cpu-sample", type=int, default=128, help="oracle sample grid (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0 = every usable host core)")
+    ap.add_argument("--cpu-cg-its", type=int, default=60, help="CG iterations of the oracle sample")
     ap.add_argument("--no-check", action="store_true")
-    ap.add_argument("--same-device", action="store_true", help="testing only: every rank on device 0")
     ap.add_argument("--mat-type", default="aij", choices=list(STORAGE_ARGS), help="matrix storage of the headline")
-    ap.add_argument("--variants", default=None,
-                    help="other storages reported beside it ('' = none; default aij-blocks,sbaij on one GPU only)")
+    ap.add_argument("--variants", default="",
+                    help="other storages measured after the headline line is printed (comma list, 1 warmup + "
+                         "1 step each, reported on stderr, skipped once --budget is spent)")
+    ap.add_argument("--budget", type=float, default=480.0, help="wall seconds the optional variants may use up to")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -193,41 +241,22 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        if torch.cuda.is_available() and not args.same_device:
+        if torch.cuda.is_available():
             torch.cuda.set_device(local)  # torch's own synchronize() then targets this rank's GPU
     px, py, pz = rank_grid(world)
     G = args.grid
     NX, NY, NZ = G * px, G * py, G * pz
     argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
-            "-da_processors_z", pz, "-ts", 2, "-ksp_rtol", repr(args.rtol),
-            "-device", 0 if args.same_device else local]
-    comm_id = None
-    if world > 1:
+            "-da_processors_z", pz, "-ts", 2, "-ksp_rtol", repr(args.rtol), "-device", local]
+
+    def new_comm_id():
+        if world == 1:
+            return None
         obj = [M.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
-        comm_id = obj[0]
-    def run(mat_type):
-        return measure(argv + STORAGE_ARGS[mat_type], rank, world, comm_id, args)
+        return obj[0]
 
-    r = run(args.mat_type)
-    if args.variants is None:
-        args.variants = "aij-blocks,sbaij" if world == 1 else ""
-    variants = {}
-    if args.variants:
-        for v in args.variants.split(","):
-            if v and v != args.mat_type:
-                if world > 1:
-                    obj = [M.comm_unique_id() if rank == 0 else None]
-                    dist.broadcast_object_list(obj, src=0)
-                    comm_id = obj[0]
-                vr = run(v)
-                variants[v] = {"value": 3 * NX * NY * NZ / (vr["ms_step"] * 1e-3), "ms_per_step": vr["ms_step"],
-                               "storage": vr["storage"], "kernel": KERNEL_NAME[vr["storage_id"]],
-                               "cg_its": vr["its"], "ms_per_cg_iter": vr["tm"]["solve_ms"] / max(vr["its"], 1),
-                               "dof_cg_iters_per_s": 3 * NX * NY * NZ * vr["its"] / (vr["tm"]["solve_ms"] * 1e-3),
-                               "spmv_avg_ms": vr["spmv_avg_ms"], "spmv_bytes_per_launch": vr["spmv_bytes"],
-                               "spmv_achieved_GBs": vr["achieved"], "spmv_traffic": pmc_traffic(vr["storage"], NX, NY, NZ),
-                               "check": vr["check"]}
+    r = measure(argv + STORAGE_ARGS[args.mat_type], rank, world, new_comm_id(), args, args.steps, args.warmup)
     its, tm, info, check = r["its"], r["tm"], r["info"], r["check"]
     spmv_avg_ms, spmv_bytes, achieved, ms_step = r["spmv_avg_ms"], r["spmv_bytes"], r["achieved"], r["ms_step"]
     ndofs = 3 * NX * NY * NZ
@@ -235,10 +264,12 @@ def main():
         cpu = None
         if world == 1 and args.cpu_sample > 0:
             try:
-                cpu = cpu_baseline(args.cpu_sample, args.cpu_threads, its, args.rtol, ndofs,
-                                   (NX - 1) * (NY - 1) * (NZ - 1), info["nnz_global"])
+                threads = args.cpu_threads or host_cores()
+                cpu = cpu_baseline(args.cpu_sample, threads, its, args.rtol, ndofs, (NX - 1) * (NY - 1) * (NZ - 1),
+                                   info["nnz_global"], args.cpu_cg_its)
             except Exception as e:  # the baseline is reported, never the product path
                 cpu = {"error": repr(e)}
+        csr_achieved = r["csr_bytes"] / (spmv_avg_ms * 1e-3) / 1e9
         line = {
             "metric": "Newton-iter DOF/s (assembly+CG) at 256^3 grid per GPU; SpMV achieved HBM GB/s",
             "value": ndofs / (ms_step * 1e-3),
@@ -264,15 +295,32 @@ def main():
             "dof_cg_iters_per_s": ndofs * its / (tm["solve_ms"] * 1e-3),
             "phases_ms": {k: tm[k] for k in ("strains_ms", "homogenize_ms", "residual_ms", "jacobian_ms",
                                              "solve_ms", "update_ms")},
+            "device_gb": info["device_bytes"] / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": pmc_traffic(r["storage"], NX, NY, NZ),
                          "kernel": KERNEL_NAME[r["storage_id"]], "bytes_per_launch": spmv_bytes,
-                         "avg_launch_ms": spmv_avg_ms, "launches_timed": tm["spmv_launches"]},
+                         "avg_launch_ms": spmv_avg_ms, "launches_timed": tm["spmv_launches"],
+                         # the same launch priced at PETSc AIJ bytes (what the reference's MatMult streams)
+                         "csr_bytes_per_launch": r["csr_bytes"], "csr_achieved": csr_achieved,
+                         "csr_frac": csr_achieved / PEAK_HBM_GBS},
             "cpu_baseline": cpu,
             "check": check,
-            "variants": variants,
         }
         print(json.dumps(line), flush=True)
+    # optional storages: after the line, 1 warmup + 1 step each, while the budget lasts
+    per_step = max(r["warmup_s"] or [ms_step * 1e-3])
+    for v in [v for v in args.variants.split(",") if v and v != args.mat_type]:
+        if time.perf_counter() - T_START + 3 * per_step > args.budget:
+            log(f"variant {v}: skipped (budget {args.budget:.0f}s)")
+            continue
+        vr = measure(argv + STORAGE_ARGS[v], rank, world, new_comm_id(), args, 1, 1)
+        if rank == 0:
+            log("variant " + json.dumps({
+                "mat_type": v, "value": ndofs / (vr["ms_step"] * 1e-3), "ms_per_step": vr["ms_step"],
+                "storage": vr["storage"], "kernel": KERNEL_NAME[vr["storage_id"]], "cg_its": vr["its"],
+                "ms_per_cg_iter": vr["tm"]["solve_ms"] / max(vr["its"], 1), "spmv_avg_ms": vr["spmv_avg_ms"],
+                "spmv_bytes_per_launch": vr["spmv_bytes"], "spmv_achieved_GBs": vr["achieved"],
+                "spmv_traffic": pmc_traffic(vr["storage"], NX, NY, NZ), "check": vr["check"]}))
     if world > 1:
         dist.destroy_process_group()
 

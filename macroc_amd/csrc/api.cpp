@@ -33,19 +33,19 @@ static void elastic_C(double E, double nu, double C[36]) {
   for (int a = 3; a < 6; a++) C[a * 6 + a] = mu;
 }
 
+// phase timer: an event pair on the compute stream, recorded without any host wait (the
+// timed steps are not serialised by the instrumentation); mcx_get_timing resolves the last pair
+enum { PH_STRAINS, PH_HOMOG, PH_RES, PH_JAC, PH_SOLVE, PH_UPDATE };
 struct PhaseTimer {
   Ctx& c;
-  double* out;
-  PhaseTimer(Ctx& cc, double* o) : c(cc), out(o) {
-    if (c.timing) (void)hipEventRecord(c.ev_a, c.stream);
+  int k;
+  PhaseTimer(Ctx& cc, int kk) : c(cc), k(kk) {
+    if (c.timing && c.ev_phase[k][0]) (void)hipEventRecord(c.ev_phase[k][0], c.stream);
   }
   ~PhaseTimer() {
-    if (!c.timing) return;
-    (void)hipEventRecord(c.ev_b, c.stream);
-    (void)hipEventSynchronize(c.ev_b);
-    float ms = 0.f;
-    (void)hipEventElapsedTime(&ms, c.ev_a, c.ev_b);
-    *out = ms;
+    if (!c.timing || !c.ev_phase[k][1]) return;
+    (void)hipEventRecord(c.ev_phase[k][1], c.stream);
+    c.phase_rec[k] = true;
   }
 };
 
@@ -62,6 +62,9 @@ static int free_ctx(Ctx* c) {
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->ev_a) (void)hipEventDestroy(c->ev_a);
   if (c->ev_b) (void)hipEventDestroy(c->ev_b);
+  for (auto& pr : c->ev_phase)
+    for (hipEvent_t e : pr)
+      if (e) (void)hipEventDestroy(e);
   for (int q = 0; q < 2; q++)
     if (c->ev_chunk[q]) (void)hipEventDestroy(c->ev_chunk[q]);
   comm_destroy(*c);
@@ -114,6 +117,8 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   MCX_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
   MCX_HIP(hipEventCreate(&c.ev_a));
   MCX_HIP(hipEventCreate(&c.ev_b));
+  for (auto& pr : c.ev_phase)
+    for (hipEvent_t& e : pr) MCX_HIP(hipEventCreate(&e));
   for (int q = 0; q < 2; q++) MCX_HIP(hipEventCreateWithFlags(&c.ev_chunk[q], hipEventDisableTiming));
   if ((rc = comm_init(c, comm_id))) return rc;
   if ((rc = build_halo_plan(c))) return rc;
@@ -559,7 +564,7 @@ int mcx_apply_bc_u(void* ctx, double U) {
 int mcx_set_strains(void* ctx) {
   GUARD(ctx);
   CTX(ctx);
-  PhaseTimer t(c, &c.t.strains_ms);
+  PhaseTimer t(c, PH_STRAINS);
   int rc = halo_exchange(c, c.u_pad);  // DMGlobalToLocal (src/assembly.c:40-41)
   if (rc) return rc;
   launch_strains(c);
@@ -570,7 +575,7 @@ int mcx_set_strains(void* ctx) {
 int mcx_homogenize(void* ctx) {
   GUARD(ctx);
   CTX(ctx);
-  PhaseTimer t(c, &c.t.homogenize_ms);
+  PhaseTimer t(c, PH_HOMOG);
   launch_homogenize(c);
   MCX_HIP(hipGetLastError());
   return 0;
@@ -580,7 +585,7 @@ int mcx_assembly_res(void* ctx, double* norm2) {
   GUARD(ctx);
   CTX(ctx);
   {
-    PhaseTimer t(c, &c.t.residual_ms);
+    PhaseTimer t(c, PH_RES);
     launch_residual(c);
     launch_reduce(c, 1, (int)node_blocks(c), c.red);
     MCX_HIP(hipGetLastError());
@@ -596,7 +601,7 @@ int mcx_assembly_res(void* ctx, double* norm2) {
 int mcx_assembly_jac(void* ctx) {
   GUARD(ctx);
   CTX(ctx);
-  PhaseTimer t(c, &c.t.jacobian_ms);
+  PhaseTimer t(c, PH_JAC);
   launch_element_ke(c);
   if (c.o.mat_type == MCX_MAT_SBAIJ) {
     launch_gather_matrix_sym(c);
@@ -623,7 +628,7 @@ int mcx_solve(void* ctx, int* its, double* rnorm, int* reason) {
   double n0 = 0.;
   int rc;
   {
-    PhaseTimer t(c, &c.t.solve_ms);
+    PhaseTimer t(c, PH_SOLVE);
     rc = cg_solve(c, &i0, &n0, &r0);
   }
   if (rc) return rc;
@@ -637,7 +642,7 @@ int mcx_solve(void* ctx, int* its, double* rnorm, int* reason) {
 int mcx_update_u(void* ctx) {
   GUARD(ctx);
   CTX(ctx);
-  PhaseTimer t(c, &c.t.update_ms);
+  PhaseTimer t(c, PH_UPDATE);
   launch_update_u(c);
   MCX_HIP(hipGetLastError());
   return 0;
@@ -1018,6 +1023,15 @@ int mcx_set_timing(void* ctx, int on) {
 int mcx_get_timing(void* ctx, mcx_timing* t) {
   GUARD(ctx);
   CTX(ctx);
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  double* ph[6] = {&c.t.strains_ms, &c.t.homogenize_ms, &c.t.residual_ms, &c.t.jacobian_ms, &c.t.solve_ms,
+                   &c.t.update_ms};
+  for (int k = 0; k < 6; k++)
+    if (c.phase_rec[k]) {
+      float ms = 0.f;
+      MCX_HIP(hipEventElapsedTime(&ms, c.ev_phase[k][0], c.ev_phase[k][1]));
+      *ph[k] = ms;
+    }
   *t = c.t;
   // algorithmic bytes of one SpMV in this format: the stencil-block values actually present
   // (AIJ nonzeros of the owned rows x 8 B), x read once, y written once

@@ -127,11 +127,11 @@ struct Ctx {
   uint16_t* D = nullptr;     // AIJ-split: bf16 corrections of the padded box [u_of/64][dsl.Lq][64] x 8
   unsigned* d_mask = nullptr;  // AIJ-split assembly: [0..13] slot masks per lower block, [14] inexact
   int fmt = FMT_V;           // storage the matrix is currently assembled in
-  int aij_split = 1;
-  int split_maxq = 4;
+  int aij_split = 1;         // aij: assemble in FMT_SPLIT when every correction is exact in bf16
+  int split_maxq = 4;        // AIJ-split only while the corrections fit this many 16-B quads per node
   int split_dbg = 0;         // timing-only diagnostics of the split SpMV (option split_dbg)
-  int split_wide = 0;        // force f32 corrections (testing the wide path)        // AIJ-split only while the corrections fit this many 16-B quads per node
-  int split_tx = 0;          // AIJ-split tile width (0: by subdomain width; option split_tx)         // aij: assemble in FMT_SPLIT when every correction is exact in bf16
+  int split_wide = 0;        // force f32 corrections (testing the wide path)
+  int split_tx = 0;          // AIJ-split tile width (0: by subdomain width; option split_tx)
   DSlots dsl;
   int64_t npgroups = 0;
   int64_t nupper_local = 0;  // sbaij: stored upper values of the owned rows
@@ -166,6 +166,10 @@ struct Ctx {
   mcx_timing t{};
   std::vector<hipEvent_t> ev_pool;
   hipEvent_t ev_a = nullptr, ev_b = nullptr;
+  // per-phase event pairs (strains, homogenize, residual, jacobian, solve, update): recorded
+  // without a host wait, resolved by mcx_get_timing
+  hipEvent_t ev_phase[6][2] = {};
+  bool phase_rec[6] = {};
   hipEvent_t ev_chunk[2] = {nullptr, nullptr};
   int last_its = 0;
   std::vector<double> last_hist;

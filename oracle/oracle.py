@@ -33,10 +33,19 @@ def build():
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
 
 
-def lib():
+def use_library(path):
+    """Load the oracle from another build of oracle.c (bench.py's -O3 -march=native timing
+    build); must be called before the first lib()."""
+    global _LIB
+    if _LIB is not None:
+        raise RuntimeError("oracle library already loaded")
+    lib(path)
+
+
+def lib(path=None):
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "liboracle.so")
+        path = path or os.path.join(_HERE, "liboracle.so")
         if not os.path.exists(path):
             build()
         L = C.CDLL(path)
