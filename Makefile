@@ -9,7 +9,11 @@ HDR = macroc_amd/csrc/mcx_internal.h include/macroc_amd.h
 LIB = macroc_amd/libmacroc_amd.so
 OBJ = $(patsubst macroc_amd/csrc/%,build/%.o,$(SRC))
 
-all: $(LIB) oracle driver
+MPI_DIR ?= /opt/conda
+MPI_FLAGS = -I$(MPI_DIR)/include -Wl,-rpath-link,/usr/lib/x86_64-linux-gnu $(MPI_DIR)/lib/libmpi.so -Wl,-rpath,$(MPI_DIR)/lib
+TESTLAW = tests/libmcx_testlaw.so
+
+all: $(LIB) oracle driver driver-mpi testlaw
 
 build/%.o: macroc_amd/csrc/% $(HDR)
 	@mkdir -p build
@@ -22,11 +26,28 @@ driver: macroc_amd/driver/macroc_amd
 macroc_amd/driver/macroc_amd: macroc_amd/driver/main.c include/macroc_amd.h $(LIB)
 	gcc -O2 -std=gnu11 -Iinclude -o $@ macroc_amd/driver/main.c -Lmacroc_amd -lmacroc_amd -Wl,-rpath,'$$ORIGIN/..'
 
+# MPI build of the driver (one rank per GPU, like `mpirun -np N macroc`); skipped without MPICH
+driver-mpi: macroc_amd/driver/macroc_amd_mpi
+macroc_amd/driver/macroc_amd_mpi: macroc_amd/driver/main.c include/macroc_amd.h $(LIB)
+	@if [ -f $(MPI_DIR)/include/mpi.h ]; then \
+	  gcc -O2 -std=gnu11 -DMCX_WITH_MPI -Iinclude -o $@ macroc_amd/driver/main.c -Lmacroc_amd -lmacroc_amd \
+	    -Wl,-rpath,'$$ORIGIN/..' $(MPI_FLAGS); \
+	else echo "no MPI under $(MPI_DIR): driver-mpi skipped"; fi
+
+# test fixture: an external constitutive law (device law + MicroPP-shaped host library) and the
+# driver linked against it as against MicroPP (tests/test_gpu_callback.py)
+testlaw: $(TESTLAW) tests/macroc_amd_micropp
+$(TESTLAW): tests/csrc/testlaw.hip include/macroc_amd.h
+	$(HIPCC) -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=$(ARCH) -shared -o $@ $<
+tests/macroc_amd_micropp: macroc_amd/driver/main.c include/macroc_amd.h $(LIB) $(TESTLAW)
+	gcc -O2 -std=gnu11 -DMCX_WITH_MICROPP -Iinclude -o $@ macroc_amd/driver/main.c -Lmacroc_amd -lmacroc_amd \
+	  -Ltests -lmcx_testlaw -Wl,-rpath,'$$ORIGIN/../macroc_amd' -Wl,-rpath,'$$ORIGIN'
+
 oracle:
 	$(MAKE) -s -C oracle
 
 clean:
-	rm -rf build $(LIB) macroc_amd/driver/macroc_amd
+	rm -rf build $(LIB) macroc_amd/driver/macroc_amd macroc_amd/driver/macroc_amd_mpi $(TESTLAW) tests/macroc_amd_micropp
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle driver clean
+.PHONY: all oracle driver driver-mpi testlaw clean

@@ -26,6 +26,14 @@
  *   mcx_solve                         <- solve_Ax -> KSPSolve(CG, Jacobi)  src/assembly.c:179-192
  *   mcx_update_u                      <- VecAXPY(u, 1., du)  src/main.c:79
  *   mcx_material_set                  <- micropp_C_material_set  src/init.c:196-201
+ *   mcx_set_micropp / mcx_set_device_law / mcx_set_gp_stress / mcx_set_gp_ctan
+ *                                     <- the MicroPP C-wrapper boundary itself: micropp_C_set_strain3
+ *                                        src/assembly.c:59, micropp_C_homogenize src/main.c:62,
+ *                                        micropp_C_get_stress3 src/assembly.c:149,
+ *                                        micropp_C_get_ctan3 src/assembly.c:92,
+ *                                        micropp_C_update_vars src/main.c:83,
+ *                                        micropp_C_get_non_linear_gps / _get_f_trial_max
+ *                                        src/util.c:71,96 (-mat_law external)
  */
 #ifndef MACROC_AMD_H
 #define MACROC_AMD_H
@@ -58,8 +66,10 @@ enum {
    lower triangle mirrored from it) */
 enum { MCX_MAT_AIJ = 0, MCX_MAT_SBAIJ = 1 };
 
-/* constitutive laws behind the Gauss-point callback (-mat_law elastic|plastic) */
-enum { MCX_LAW_ELASTIC = 0, MCX_LAW_PLASTIC = 1 };
+/* constitutive laws behind the Gauss-point callback (-mat_law elastic|plastic|external):
+   device isotropic elastic, device J2 plasticity (MicroPP material type 1), or an external law
+   registered through mcx_set_micropp / mcx_set_device_law / mcx_set_gp_stress+ctan */
+enum { MCX_LAW_ELASTIC = 0, MCX_LAW_PLASTIC = 1, MCX_LAW_EXTERNAL = 2 };
 
 typedef struct {
   int64_t NX, NY, NZ;          /* -da_grid_x/y/z          (default 40 3 40, include/macroc.h:44-46) */
@@ -108,6 +118,11 @@ typedef struct {
                                    2 AIJ-split (upper blocks + bf16 lower corrections) */
   int split_slots;              /* AIJ-split: correction slots stored per node (of 117) */
   int split_bits;               /* AIJ-split: bits per correction (16 = bf16, 32 = f32) */
+  /* Gauss-point box of the constitutive callback: the elements this context evaluates, x
+     fastest from element (ex0, ey0, ez0) (global element = lower-left node), nelem_ext =
+     nex*ney*nez; Gauss point gpi = ie*8 + gp.  One rank: DMDAGetElements' own order.  Several
+     ranks: the rank's PETSc elements plus the upper ghost layer (owner computes). */
+  int64_t ex0, ey0, ez0, nex, ney, nez;
 } mcx_info;
 
 typedef struct {
@@ -151,6 +166,56 @@ int mcx_get_info(void* ctx, mcx_info* info);
 
 /* Gauss-point constitutive model (micropp_C_material_set(id,E,nu,Sy,Ka,type)) */
 int mcx_material_set(void* ctx, int id, double E, double nu, double Sy, double Ka, int type);
+
+/* ---- the MicroPP Gauss-point callback boundary (-mat_law external) ----
+ * The reference hands every Gauss point's strain to MicroPP's C wrapper and reads stress and
+ * tangent back per Gauss point (src/assembly.c:59,92,149, src/main.c:62,83).  With -mat_law
+ * external the device laws are replaced by one of:
+ *  (1) host callbacks with the wrapper's call shapes (a real MicroPP links straight in:
+ *      api.set_strain3 = micropp_C_set_strain3, ...).  mcx_homogenize then copies the strains to
+ *      the host, calls set_strain3(gpi, strain) for every Gauss point (gpi = ie*8 + gp over
+ *      mcx_info's Gauss-point box, ascending), homogenize() once, get_stress3(gpi, stress) and
+ *      get_ctan3(gpi, ctan) for every Gauss point, and copies stress and tangent back.
+ *      mcx_update_vars calls update_vars(); the non-linear statistics come from
+ *      get_non_linear_gps / get_f_trial_max when given.
+ *  (2) a device law: law->homogenize(law->user, &batch) runs on the context's stream with
+ *      device pointers to strain, stress and tangent (the same contract as the built-in laws).
+ *  (3) batched injection: mcx_set_gp_stress / mcx_set_gp_ctan copy caller-computed values
+ *      (host, [ngp][6] / [ngp][36], gpi order) into the device arrays; mcx_get_gp_strain reads
+ *      the strains of the same box.
+ * Stress and tangent are Voigt (xx, yy, zz, xy, xz, yz; engineering shear), the tangent row
+ * major (ctan[k*6+l], src/assembly.c:99).  Pass NULL to unregister. */
+typedef struct {
+  void (*set_strain3)(int gpi, double* strain);  /* micropp_C_set_strain3   src/assembly.c:59 */
+  void (*homogenize)(void);                      /* micropp_C_homogenize    src/main.c:62 */
+  void (*get_stress3)(int gpi, double* stress);  /* micropp_C_get_stress3   src/assembly.c:149 */
+  void (*get_ctan3)(int gpi, double* ctan);      /* micropp_C_get_ctan3     src/assembly.c:92 */
+  void (*update_vars)(void);                     /* micropp_C_update_vars   src/main.c:83 (may be NULL) */
+  int (*get_non_linear_gps)(void);               /* src/util.c:71 (may be NULL) */
+  double (*get_f_trial_max)(void);               /* src/util.c:96 (may be NULL) */
+} mcx_micropp_api;
+
+typedef struct {
+  int64_t nelem;      /* elements of the Gauss-point box (mcx_info.nelem_ext) */
+  int64_t ngp;        /* 8 * nelem */
+  const double* eps;  /* device [6][8][nelem]: component k of GP gp of element e at k*ngp + gp*nelem + e */
+  double* sig;        /* device, same layout */
+  double* ctan;       /* device [36][8][nelem]: ctan[k*6+l] of GP gp of element e at (k*6+l)*ngp + gp*nelem + e */
+  void* stream;       /* the context's HIP stream: launch on it, or finish before returning */
+} mcx_gp_batch;
+
+typedef struct {
+  int (*homogenize)(void* user, const mcx_gp_batch* batch);            /* required; 0 = OK */
+  int (*update_vars)(void* user);                                      /* may be NULL */
+  int (*nonlinear_stats)(void* user, int64_t* n_nonlinear, double* f_trial_max); /* may be NULL */
+  void* user;
+} mcx_device_law;
+
+int mcx_set_micropp(void* ctx, const mcx_micropp_api* api);
+int mcx_set_device_law(void* ctx, const mcx_device_law* law);
+int mcx_set_gp_stress(void* ctx, const double* host /* [ngp][6] */);
+int mcx_set_gp_ctan(void* ctx, const double* host /* [ngp][36] */);
+int mcx_get_gp_strain(void* ctx, double* host /* [ngp][6] */);
 
 double mcx_get_displacement(void* ctx, int time_s);
 int mcx_zero_u(void* ctx);                 /* VecZeroEntries(u)  src/init.c:103 */

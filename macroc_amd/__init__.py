@@ -38,7 +38,10 @@ EXPORTS = [
     "mcx_time_step", "mcx_get_u", "mcx_set_u", "mcx_get_b", "mcx_get_du", "mcx_get_strain", "mcx_get_stress",
     "mcx_owned_dofs", "mcx_dump_csr", "mcx_dump_dirichlet", "mcx_spmv", "mcx_get_ksp_history",
     "mcx_set_timing", "mcx_get_timing", "mcx_synchronize", "mcx_set_option", "mcx_time_spmv",
+    "mcx_set_micropp", "mcx_set_device_law", "mcx_set_gp_stress", "mcx_set_gp_ctan", "mcx_get_gp_strain",
 ]
+
+LAWS = {"elastic": 0, "plastic": 1, "external": 2}
 
 
 class Opts(C.Structure):
@@ -68,10 +71,35 @@ class Info(C.Structure):
         ("dx", C.c_double), ("dy", C.c_double), ("dz", C.c_double), ("wg", C.c_double),
         ("device_bytes", C.c_int64), ("device", C.c_int), ("storage", C.c_int), ("split_slots", C.c_int),
         ("split_bits", C.c_int),
+        ("ex0", C.c_int64), ("ey0", C.c_int64), ("ez0", C.c_int64), ("nex", C.c_int64), ("ney", C.c_int64),
+        ("nez", C.c_int64),
     ]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# MicroPP C-wrapper call shapes (micropp_c_wrapper.h, called at src/assembly.c:59,92,149,
+# src/main.c:62,83, src/util.c:71,96)
+SET_STRAIN3 = C.CFUNCTYPE(None, C.c_int, C.POINTER(C.c_double))
+HOMOGENIZE = C.CFUNCTYPE(None)
+GET_STRESS3 = C.CFUNCTYPE(None, C.c_int, C.POINTER(C.c_double))
+GET_CTAN3 = C.CFUNCTYPE(None, C.c_int, C.POINTER(C.c_double))
+UPDATE_VARS = C.CFUNCTYPE(None)
+GET_NON_LINEAR_GPS = C.CFUNCTYPE(C.c_int)
+GET_F_TRIAL_MAX = C.CFUNCTYPE(C.c_double)
+
+
+class MicroppApi(C.Structure):
+    _fields_ = [("set_strain3", SET_STRAIN3), ("homogenize", HOMOGENIZE), ("get_stress3", GET_STRESS3),
+                ("get_ctan3", GET_CTAN3), ("update_vars", UPDATE_VARS), ("get_non_linear_gps", GET_NON_LINEAR_GPS),
+                ("get_f_trial_max", GET_F_TRIAL_MAX)]
+
+
+class DeviceLaw(C.Structure):
+    """mcx_device_law: function pointers of a device constitutive law (built in C/HIP)."""
+    _fields_ = [("homogenize", C.c_void_p), ("update_vars", C.c_void_p), ("nonlinear_stats", C.c_void_p),
+                ("user", C.c_void_p)]
 
 
 class Timing(C.Structure):
@@ -140,6 +168,10 @@ def lib():
     L.mcx_get_timing.argtypes = [vp, C.POINTER(Timing)]
     L.mcx_set_option.argtypes = [vp, C.c_char_p, C.c_double]
     L.mcx_time_spmv.argtypes = [vp, C.c_int, d]
+    L.mcx_set_micropp.argtypes = [vp, C.POINTER(MicroppApi)]
+    L.mcx_set_device_law.argtypes = [vp, C.POINTER(DeviceLaw)]
+    for fn in ("mcx_set_gp_stress", "mcx_set_gp_ctan", "mcx_get_gp_strain"):
+        getattr(L, fn).argtypes = [vp, d]
     _LIB = L
     return L
 
@@ -335,6 +367,44 @@ class Macroc:
 
     def synchronize(self):
         _check(lib().mcx_synchronize(self._ctx), "synchronize")
+
+    # ---- the MicroPP Gauss-point callback boundary (-mat_law external)
+    @property
+    def ngp(self):
+        """Gauss points of the callback box (mcx_info nelem_ext * 8), gpi = ie*8 + gp."""
+        return 8 * self.info["nelem_ext"]
+
+    def set_micropp(self, set_strain3=None, homogenize=None, get_stress3=None, get_ctan3=None, update_vars=None,
+                    get_non_linear_gps=None, get_f_trial_max=None):
+        """Register host callbacks with micropp_C_* call shapes (Python callables taking
+        (gpi, ctypes double pointer) etc.); no arguments unregisters."""
+        if set_strain3 is None:
+            _check(lib().mcx_set_micropp(self._ctx, None), "mcx_set_micropp")
+            self._mpp = None
+            return
+        api = MicroppApi(SET_STRAIN3(set_strain3), HOMOGENIZE(homogenize), GET_STRESS3(get_stress3),
+                         GET_CTAN3(get_ctan3), UPDATE_VARS(update_vars) if update_vars else UPDATE_VARS(),
+                         GET_NON_LINEAR_GPS(get_non_linear_gps) if get_non_linear_gps else GET_NON_LINEAR_GPS(),
+                         GET_F_TRIAL_MAX(get_f_trial_max) if get_f_trial_max else GET_F_TRIAL_MAX())
+        self._mpp = api  # the library keeps the function pointers: keep the thunks alive
+        _check(lib().mcx_set_micropp(self._ctx, C.byref(api)), "mcx_set_micropp")
+
+    def set_device_law(self, law):
+        """Register an mcx_device_law (DeviceLaw structure filled by a C/HIP library); None unregisters."""
+        self._dlaw = law
+        _check(lib().mcx_set_device_law(self._ctx, C.byref(law) if law is not None else None), "mcx_set_device_law")
+
+    def set_gp_stress(self, sig):
+        sig = np.ascontiguousarray(sig, dtype=np.float64).reshape(self.ngp, 6)
+        _check(lib().mcx_set_gp_stress(self._ctx, _dp(sig)), "mcx_set_gp_stress")
+
+    def set_gp_ctan(self, ctan):
+        ctan = np.ascontiguousarray(ctan, dtype=np.float64).reshape(self.ngp, 36)
+        _check(lib().mcx_set_gp_ctan(self._ctx, _dp(ctan)), "mcx_set_gp_ctan")
+
+    def gp_strain(self):
+        """strains of the callback box, [ngp][6] in gpi order."""
+        return self._get("mcx_get_gp_strain", self.ngp * 6).reshape(-1, 6)
 
     # ---- data access (owned rows, PETSc-local order)
     def _get(self, fn, n):

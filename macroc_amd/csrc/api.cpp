@@ -54,7 +54,7 @@ static int free_ctx(Ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->V, c->U, c->D, c->d_mask, c->eps, c->sig, c->ctan,
-                  c->Ke, c->be, c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
+                  c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
@@ -125,33 +125,34 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   if ((rc = upload_constants(c))) return rc;
   const Geo& g = c.g;
   const int64_t npad = (int64_t)g.PX * g.PY * g.PZ * 3, nown3 = 3 * (int64_t)g.nown, E = g.nelem;
+  // matrix storage: AIJ blocks V only for -mat_aij_split 0 (the AIJ-split path allocates it
+  // lazily if a correction is not exact, mcx_assembly_jac); U for sbaij and AIJ-split; the
+  // AIJ-split corrections D are sized by build_split to the active slots
   if ((rc = dalloc(c, &c.u_pad, npad)) || (rc = dalloc(c, &c.p_pad, npad)) || (rc = dalloc(c, &c.b, nown3)) ||
       (rc = dalloc(c, &c.du, nown3)) || (rc = dalloc(c, &c.r, nown3)) || (rc = dalloc(c, &c.z, nown3)) ||
       (rc = dalloc(c, &c.w, nown3)) || (rc = dalloc(c, &c.dinv, nown3)) || (rc = dalloc(c, &c.tmp, nown3)) ||
-      (c.o.mat_type == MCX_MAT_SBAIJ
-           ? (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))
-           // AIJ blocks; with AIJ-split also the scratch of its assembly (117 bf16 per padded node)
-           : (rc = dalloc(c, &c.V, std::max<int64_t>(c.ngroups * NPAIR * 128,
-                                                     c.aij_split ? (126 * 64 * c.npgroups + 1) / 2 : 0)))) ||
-      (c.aij_split && (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))) ||
-      (rc = dalloc(c, &c.eps, 6 * 8 * E)) ||
-      (rc = dalloc(c, &c.sig, 6 * 8 * E)) || (rc = dalloc(c, &c.ctan, 36 * 8 * E)) ||
-      (rc = dalloc(c, &c.Ke, (int64_t)NKE * E)) || (rc = dalloc(c, &c.be, 24 * E)) ||
+      ((c.o.mat_type == MCX_MAT_SBAIJ || c.aij_split) && (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))) ||
+      (c.o.mat_type == MCX_MAT_AIJ && !c.aij_split && (rc = dalloc(c, &c.V, c.ngroups * NPAIR * 128))) ||
+      (rc = dalloc(c, &c.eps, 6 * 8 * E)) || (rc = dalloc(c, &c.sig, 6 * 8 * E)) ||
       (rc = dalloc(c, &c.partials, c.partials_cap = 4 * std::max(max_spmv_blocks(c), node_blocks(c)) + 64)) ||
       (rc = dalloc(c, &c.red, 16)) || (rc = dalloc(c, &c.red_loc, 16)) || (rc = dalloc(c, &c.cg, 1)) ||
       (rc = dalloc(c, &c.hist, (int64_t)o->ksp_max_it + 2)))
     return rc;
+  // per-GP tangent: only laws that hand one over (the isotropic elastic C is a kernel argument)
+  if (o->mat_law != MCX_LAW_ELASTIC && (rc = dalloc(c, &c.ctan, 36 * 8 * E))) return rc;
   if (o->mat_law == MCX_LAW_PLASTIC &&
       ((rc = dalloc(c, &c.hist_old, 7 * 8 * E)) || (rc = dalloc(c, &c.hist_new, 7 * 8 * E)) ||
        (rc = dalloc(c, &c.ftrial, 8 * E))))
     return rc;
-  if (c.aij_split) {
-    MCX_HIP(hipMalloc(&c.D, sizeof(unsigned) * 120 * 64 * c.npgroups));  // f32 worst case
-    MCX_HIP(hipMalloc(&c.d_mask, 16 * sizeof(unsigned)));
-    c.device_bytes += sizeof(unsigned) * 120 * 64 * c.npgroups;
-  }
+  if (c.aij_split) MCX_HIP(hipMalloc(&c.d_mask, 16 * sizeof(unsigned)));
   MCX_HIP(hipHostMalloc((void**)&c.h_cg, sizeof(CgState) * 2, hipHostMallocDefault));
   std::memset(c.h_cg, 0, sizeof(CgState) * 2);
+  if (o->micro_n != 2 && o->mat_law != MCX_LAW_EXTERNAL && rank == 0)
+    std::fprintf(stderr,
+                 "WARNING! -micro_n %d has no effect: the device Gauss-point laws have no micro-scale FE problem "
+                 "(MicroPP's FE2 solver is out of scope); it sizes an external MicroPP (-mat_law external, "
+                 "micropp_C_create3, src/init.c:210-213)\n",
+                 o->micro_n);
   c.mat.law = o->mat_law;
   c.mat.E = o->micro_mat_1[0];
   c.mat.nu = o->micro_mat_1[1];
@@ -344,11 +345,12 @@ int mcx_parse_args(mcx_opts* o, int argc, const char* const* argv) {
     }
     if (!std::strcmp(k, "-mat_ignore_lower_triangular")) continue;
     if (!std::strcmp(k, "-mat_law")) {
-      if (!v || (std::strcmp(v, "elastic") && std::strcmp(v, "plastic"))) {
-        set_error(std::string("-mat_law: elastic or plastic, got ") + (v ? v : "(none)"));
+      if (!v || (std::strcmp(v, "elastic") && std::strcmp(v, "plastic") && std::strcmp(v, "external"))) {
+        set_error(std::string("-mat_law: elastic, plastic or external, got ") + (v ? v : "(none)"));
         return 2;
       }
-      o->mat_law = std::strcmp(v, "plastic") ? MCX_LAW_ELASTIC : MCX_LAW_PLASTIC;
+      o->mat_law = !std::strcmp(v, "plastic") ? MCX_LAW_PLASTIC
+                   : !std::strcmp(v, "external") ? MCX_LAW_EXTERNAL : MCX_LAW_ELASTIC;
       a++;
       continue;
     }
@@ -462,6 +464,12 @@ static void fill_info(const Ctx& c, mcx_info* in) {
   in->storage = c.fmt;
   in->split_slots = c.fmt == FMT_SPLIT ? c.dsl.L : 0;
   in->split_bits = c.fmt == FMT_SPLIT ? (c.dsl.wide ? 32 : 16) : 0;
+  in->ex0 = g.ex0;
+  in->ey0 = g.ey0;
+  in->ez0 = g.ez0;
+  in->nex = g.nex;
+  in->ney = g.ney;
+  in->nez = g.nez;
 }
 
 
@@ -572,12 +580,131 @@ int mcx_set_strains(void* ctx) {
   return 0;
 }
 
+// -mat_law external: the registered law fills sig and ctan from eps (see macroc_amd.h)
+static int external_homogenize(Ctx& c) {
+  const int64_t E = c.g.nelem, ngp = 8 * E;
+  if (c.has_dlaw) {
+    mcx_gp_batch b{E, ngp, c.eps, c.sig, c.ctan, (void*)c.stream};
+    const int rc = c.dlaw.homogenize(c.dlaw.user, &b);
+    if (rc) {
+      set_error("external device law: homogenize returned " + std::to_string(rc));
+      return 6;
+    }
+    MCX_HIP(hipGetLastError());
+    return 0;
+  }
+  if (!c.has_mpp) return 0;  // values injected with mcx_set_gp_stress / mcx_set_gp_ctan
+  // host MicroPP: strains out, per-GP calls in gpi = ie*8 + gp order, stress + tangent back
+  c.h_gp.resize((size_t)ngp * 36);
+  double* h = c.h_gp.data();
+  MCX_HIP(hipMemcpyAsync(h, c.eps, sizeof(double) * 6 * ngp, hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  std::vector<double> soa((size_t)ngp * 6);
+  for (int64_t e = 0; e < E; e++)
+    for (int gp = 0; gp < 8; gp++) {
+      double eps6[6];
+      for (int k = 0; k < 6; k++) eps6[k] = h[(int64_t)k * ngp + gp * E + e];
+      c.mpp.set_strain3((int)(e * 8 + gp), eps6);
+    }
+  c.mpp.homogenize();
+  for (int64_t e = 0; e < E; e++)
+    for (int gp = 0; gp < 8; gp++) {
+      double s6[6];
+      c.mpp.get_stress3((int)(e * 8 + gp), s6);
+      for (int k = 0; k < 6; k++) soa[(size_t)k * ngp + gp * E + e] = s6[k];
+    }
+  MCX_HIP(hipMemcpyAsync(c.sig, soa.data(), sizeof(double) * 6 * ngp, hipMemcpyHostToDevice, c.stream));
+  for (int64_t e = 0; e < E; e++)
+    for (int gp = 0; gp < 8; gp++) {
+      double c36[36];
+      c.mpp.get_ctan3((int)(e * 8 + gp), c36);
+      for (int kl = 0; kl < 36; kl++) h[(size_t)kl * ngp + gp * E + e] = c36[kl];
+    }
+  MCX_HIP(hipMemcpyAsync(c.ctan, h, sizeof(double) * 36 * ngp, hipMemcpyHostToDevice, c.stream));
+  MCX_HIP(hipStreamSynchronize(c.stream));  // the staging buffers are reused
+  return 0;
+}
+
 int mcx_homogenize(void* ctx) {
   GUARD(ctx);
   CTX(ctx);
   PhaseTimer t(c, PH_HOMOG);
+  if (c.mat.law == MCX_LAW_EXTERNAL) return external_homogenize(c);
   launch_homogenize(c);
   MCX_HIP(hipGetLastError());
+  return 0;
+}
+
+static int need_external(Ctx& c, const char* fn) {
+  if (c.mat.law == MCX_LAW_EXTERNAL) return 0;
+  set_error(std::string(fn) + ": the context was created without -mat_law external");
+  return 7;
+}
+
+int mcx_set_micropp(void* ctx, const mcx_micropp_api* api) {
+  GUARD(ctx);
+  CTX(ctx);
+  if (int rc = need_external(c, "mcx_set_micropp")) return rc;
+  if (api && (!api->set_strain3 || !api->homogenize || !api->get_stress3 || !api->get_ctan3)) {
+    set_error("mcx_set_micropp: set_strain3, homogenize, get_stress3 and get_ctan3 are required");
+    return 2;
+  }
+  c.has_mpp = api != nullptr;
+  if (api) c.mpp = *api;
+  if (api) c.has_dlaw = false;
+  return 0;
+}
+
+int mcx_set_device_law(void* ctx, const mcx_device_law* law) {
+  GUARD(ctx);
+  CTX(ctx);
+  if (int rc = need_external(c, "mcx_set_device_law")) return rc;
+  if (law && !law->homogenize) {
+    set_error("mcx_set_device_law: homogenize is required");
+    return 2;
+  }
+  c.has_dlaw = law != nullptr;
+  if (law) c.dlaw = *law;
+  if (law) c.has_mpp = false;
+  return 0;
+}
+
+// host [ngp][ncomp] (gpi order) <-> device [ncomp][8][nelem]
+static int gp_upload(Ctx& c, const double* host, double* dev, int ncomp) {
+  const int64_t E = c.g.nelem, ngp = 8 * E;
+  std::vector<double> soa((size_t)ngp * ncomp);
+  for (int64_t e = 0; e < E; e++)
+    for (int gp = 0; gp < 8; gp++)
+      for (int k = 0; k < ncomp; k++) soa[(size_t)k * ngp + gp * E + e] = host[(e * 8 + gp) * ncomp + k];
+  MCX_HIP(hipMemcpyAsync(dev, soa.data(), sizeof(double) * soa.size(), hipMemcpyHostToDevice, c.stream));
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  return 0;
+}
+
+int mcx_set_gp_stress(void* ctx, const double* host) {
+  GUARD(ctx);
+  CTX(ctx);
+  if (int rc = need_external(c, "mcx_set_gp_stress")) return rc;
+  return gp_upload(c, host, c.sig, 6);
+}
+
+int mcx_set_gp_ctan(void* ctx, const double* host) {
+  GUARD(ctx);
+  CTX(ctx);
+  if (int rc = need_external(c, "mcx_set_gp_ctan")) return rc;
+  return gp_upload(c, host, c.ctan, 36);
+}
+
+int mcx_get_gp_strain(void* ctx, double* host) {
+  GUARD(ctx);
+  CTX(ctx);
+  const int64_t E = c.g.nelem, ngp = 8 * E;
+  std::vector<double> soa((size_t)ngp * 6);
+  MCX_HIP(hipMemcpyAsync(soa.data(), c.eps, sizeof(double) * soa.size(), hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  for (int64_t e = 0; e < E; e++)
+    for (int gp = 0; gp < 8; gp++)
+      for (int k = 0; k < 6; k++) host[(e * 8 + gp) * 6 + k] = soa[(size_t)k * ngp + gp * E + e];
   return 0;
 }
 
@@ -598,25 +725,35 @@ int mcx_assembly_res(void* ctx, double* norm2) {
   return 0;
 }
 
+// the AIJ stencil-block storage, allocated on first use when the context started with AIJ-split
+static int ensure_V(Ctx& c) {
+  if (c.V) return 0;
+  return dalloc(c, &c.V, c.ngroups * NPAIR * 128);
+}
+
 int mcx_assembly_jac(void* ctx) {
   GUARD(ctx);
   CTX(ctx);
   PhaseTimer t(c, PH_JAC);
-  launch_element_ke(c);
+  int rc;
   if (c.o.mat_type == MCX_MAT_SBAIJ) {
     launch_gather_matrix_sym(c);
     c.fmt = FMT_U;
   } else if (c.aij_split) {
     launch_gather_matrix_sym(c);
     bool exact = false;
-    int rc = build_split(c, &exact);
-    if (rc) return rc;
+    if ((rc = build_split(c, &exact))) return rc;
     c.fmt = exact ? FMT_SPLIT : FMT_V;
-    if (!exact) launch_gather_matrix(c);  // a correction is not exact in bf16: plain AIJ blocks
+    if (!exact) {  // a correction is not exact in bf16 / f32: plain AIJ blocks
+      if ((rc = ensure_V(c))) return rc;
+      launch_gather_matrix(c);
+    }
   } else {
+    if ((rc = ensure_V(c))) return rc;
     launch_gather_matrix(c);
     c.fmt = FMT_V;
   }
+  c.assembled = true;
   MCX_HIP(hipGetLastError());
   return 0;
 }
@@ -624,6 +761,10 @@ int mcx_assembly_jac(void* ctx) {
 int mcx_solve(void* ctx, int* its, double* rnorm, int* reason) {
   GUARD(ctx);
   CTX(ctx);
+  if (!c.assembled) {
+    set_error("mcx_solve: no matrix assembled (call mcx_assembly_jac first)");
+    return 5;
+  }
   int i0 = 0, r0 = 0;
   double n0 = 0.;
   int rc;
@@ -652,6 +793,14 @@ int mcx_update_vars(void* ctx) {
   GUARD(ctx);
   CTX(ctx);
   if (c.hist_old) std::swap(c.hist_old, c.hist_new);
+  if (c.has_mpp && c.mpp.update_vars) c.mpp.update_vars();
+  if (c.has_dlaw && c.dlaw.update_vars) {
+    MCX_HIP(hipStreamSynchronize(c.stream));
+    if (int rc = c.dlaw.update_vars(c.dlaw.user)) {
+      set_error("external device law: update_vars returned " + std::to_string(rc));
+      return 6;
+    }
+  }
   return 0;
 }
 
@@ -660,7 +809,18 @@ int mcx_get_nonlinear_stats(void* ctx, int64_t* n_nonlinear, double* f_trial_max
   CTX(ctx);
   int64_t n = 0;
   double fm = 0.;
-  if (c.ftrial) {
+  if (c.has_mpp) {  // the external MicroPP's own counts (over its Gauss points)
+    if (c.mpp.get_non_linear_gps) n = c.mpp.get_non_linear_gps();
+    if (c.mpp.get_f_trial_max) fm = c.mpp.get_f_trial_max();
+  } else if (c.has_dlaw) {
+    if (c.dlaw.nonlinear_stats) {
+      MCX_HIP(hipStreamSynchronize(c.stream));
+      if (int rc = c.dlaw.nonlinear_stats(c.dlaw.user, &n, &fm)) {
+        set_error("external device law: nonlinear_stats returned " + std::to_string(rc));
+        return 6;
+      }
+    }
+  } else if (c.ftrial) {
     const Geo& g = c.g;
     std::vector<double> ft(8 * g.nelem);
     MCX_HIP(hipMemcpyAsync(ft.data(), c.ftrial, sizeof(double) * ft.size(), hipMemcpyDeviceToHost, c.stream));
@@ -888,6 +1048,10 @@ int mcx_owned_dofs(void* ctx, int64_t* petsc, int64_t* natural) {
 int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
   GUARD(ctx);
   CTX(ctx);
+  if (vals && !c.assembled) {
+    set_error("mcx_dump_csr: no matrix assembled (call mcx_assembly_jac first)");
+    return 5;
+  }
   const Geo& g = c.g;
   const bool up = c.fmt != FMT_V;  // FMT_U / FMT_SPLIT: values from the upper blocks
   std::vector<double> V;
@@ -992,6 +1156,10 @@ int mcx_dump_dirichlet(void* ctx, int64_t* idx, int64_t* n) {
 int mcx_spmv(void* ctx, const double* x_host, double* y_host) {
   GUARD(ctx);
   CTX(ctx);
+  if (!c.assembled) {
+    set_error("mcx_spmv: no matrix assembled (call mcx_assembly_jac first)");
+    return 5;
+  }
   MCX_HIP(hipMemcpyAsync(c.tmp, x_host, sizeof(double) * 3 * c.g.nown, hipMemcpyHostToDevice, c.stream));
   launch_copy_owned_to_pad(c, c.tmp, c.p_pad);
   int rc = halo_exchange(c, c.p_pad);
@@ -1085,7 +1253,7 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     return 0;
   }
   if (!std::strcmp(name, "aij_split")) {  // takes effect at the next mcx_assembly_jac
-    if (value != 0. && !c.D) {
+    if (value != 0. && (!c.U || !c.d_mask)) {
       set_error("aij_split: context created with -mat_aij_split 0 (no split storage)");
       return 2;
     }
@@ -1115,6 +1283,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
 int mcx_time_spmv(void* ctx, int iters, double* avg_ms) {
   GUARD(ctx);
   CTX(ctx);
+  if (!c.assembled) {
+    set_error("mcx_time_spmv: no matrix assembled");
+    return 5;
+  }
   launch_spmv(c, c.p_pad, c.w, true, false);  // warm
   MCX_HIP(hipEventRecord(c.ev_a, c.stream));
   for (int q = 0; q < iters; q++) launch_spmv(c, c.p_pad, c.w, true, false);

@@ -263,10 +263,11 @@ __global__ void k_vtu_cells(Geo g, const double* __restrict__ u, const double* _
 }
 
 // ---------------------------------------------------------------------------- material
-// Gauss-point callback, isotropic linear elastic (MicroPP surrogate): sigma = C eps,
-// ctan = C, per Gauss point (micropp_C_homogenize / get_stress3 / get_ctan3).
+// Gauss-point callback, isotropic linear elastic (MicroPP surrogate): sigma = C eps per Gauss
+// point (micropp_C_homogenize / get_stress3).  The tangent is the constant C (get_ctan3): the
+// Jacobian evaluates it from the kernel argument, so no per-GP tangent array exists.
 __global__ void k_homogenize_elastic(int64_t ngp, Material mat, const double* __restrict__ eps,
-                                     double* __restrict__ sig, double* __restrict__ ctan) {
+                                     double* __restrict__ sig) {
   int64_t q = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (q >= ngp) return;
   double e[6];
@@ -279,8 +280,6 @@ __global__ void k_homogenize_elastic(int64_t ngp, Material mat, const double* __
     for (int l = 0; l < 6; l++) s += mat.C[k * 6 + l] * e[l];
     sig[k * ngp + q] = s;
   }
-#pragma unroll
-  for (int kl = 0; kl < 36; kl++) ctan[kl * ngp + q] = mat.C[kl];
 }
 
 // small-strain J2 plasticity with linear isotropic hardening (MicroPP material type 1: E, nu,
@@ -362,60 +361,60 @@ __global__ void k_homogenize_plastic(int64_t ngp, Material mat, const double* __
 }
 
 // ---------------------------------------------------------------------------- residual
-// assembly_res (src/assembly.c:142-154): be[i] += B[j][i] * sigma[j] * wg, gp outer, j inner
-__global__ void k_element_res(Geo g, const double* __restrict__ sig, double* __restrict__ be) {
-  int64_t le = (int64_t)blockIdx.x * TPB + threadIdx.x;
-  if (le >= g.nelem) return;
-  const int64_t E = g.nelem, NG = 8 * E;
-  double acc[24];
-#pragma unroll
-  for (int i = 0; i < 24; i++) acc[i] = 0.;
-#pragma unroll
-  for (int gp = 0; gp < 8; gp++) {
-    double s[6];
-#pragma unroll
-    for (int jj = 0; jj < 6; jj++) s[jj] = sig[jj * NG + gp * E + le];
-#pragma unroll
-    for (int i = 0; i < 24; i++) {
-      const int d = i % 3;
-#pragma unroll
-      for (int jj = 0; jj < 6; jj++) {
-        const bool nz = (jj < 3) ? (d == jj) : (jj == 3 ? d != 2 : (jj == 4 ? d != 1 : d != 0));
-        if (nz) acc[i] += cB[gp][jj][i] * s[jj] * g.wg;
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < 24; i++) be[i * E + le] = acc[i];
+// rows k of B with B[k][3a+r] != 0, ascending: K(0) = {0,3,4}, K(1) = {1,3,5}, K(2) = {2,4,5}
+__device__ __forceinline__ constexpr int krow(int r, int q) { return q == 0 ? r : (r == 1 ? (q == 1 ? 3 : 5) : 3 + q - (r == 0)); }
+// position of row k in K(r) (k in K(r))
+__device__ __forceinline__ constexpr int kpos(int r, int k) { return k == r ? 0 : ((k == 3 || (k == 4 && r == 2)) ? 1 : 2); }
+__device__ __forceinline__ constexpr bool kin(int r, int k) {
+  return k == r || (r == 0 && (k == 3 || k == 4)) || (r == 1 && (k == 3 || k == 5)) || (r == 2 && (k == 4 || k == 5));
 }
 
-// b_node = sum over adjacent elements in ascending element order (the order the reference's
-// element loop adds into b_loc, :156-161), Dirichlet rows zeroed (apply_bc_on_res), then
-// VecScale(b,-1) (:171-173).  Emits per-block partial sums of b.b for VecNorm.
-__global__ __launch_bounds__(TPB) void k_gather_res(Geo g, const double* __restrict__ be, double* __restrict__ b,
-                                                    double* __restrict__ part) {
+// assembly_res (src/assembly.c:120-176) node by node, without an element-vector array: the
+// node's rows are 0 + be_e1 + be_e2 + ... over its elements in ascending element order (the
+// order the reference's element loop adds into b_loc, :156-161), each be[3a+r] = sum_gp sum_j
+// B[j][3a+r] * sigma_j * wg evaluated on the fly (gp outer, j ascending, :145-154; zero B terms
+// skipped, exact); Dirichlet rows zeroed (apply_bc_on_res), then VecScale(b,-1) (:171-173).
+// The element loop runs over the node's local offset (ox, oy, oz) in the element, descending =
+// ascending element index, so the local node number a is wave-uniform (scalar B loads).
+// Emits per-block partial sums of b.b for VecNorm.
+__global__ __launch_bounds__(TPB) void k_residual(Geo g, const double* __restrict__ sig, double* __restrict__ b,
+                                                  double* __restrict__ part) {
   __shared__ double sh[TPB / 64];
-  int n = blockIdx.x * TPB + threadIdx.x;
+  const int n = blockIdx.x * TPB + threadIdx.x;
   double nrm = 0.;
   if (n < g.nown) {
     int i, j, k;
     node_ijk(g, n, i, j, k);
-    int gi = g.xs + i, gj = g.ys + j, gk = g.zs + k;
+    const int gi = g.xs + i, gj = g.ys + j, gk = g.zs + k;
+    const int64_t E = g.nelem, NG = 8 * E;
     double acc[3] = {0., 0., 0.};
-    for (int ez = gk - 1; ez <= gk; ez++) {
+    for (int oz = 1; oz >= 0; oz--) {
+      const int ez = gk - oz;
       if (ez < 0 || ez > g.NZ - 2) continue;
-      for (int ey = gj - 1; ey <= gj; ey++) {
+      for (int oy = 1; oy >= 0; oy--) {
+        const int ey = gj - oy;
         if (ey < 0 || ey > g.NY - 2) continue;
-        for (int ex = gi - 1; ex <= gi; ex++) {
+        for (int ox = 1; ox >= 0; ox--) {
+          const int ex = gi - ox;
           if (ex < 0 || ex > g.NX - 2) continue;
-          int64_t le = (ex - g.ex0) + (int64_t)(ey - g.ey0) * g.nex + (int64_t)(ez - g.ez0) * g.nex * g.ney;
-          int a = q1_local(gi - ex, gj - ey, gk - ez);
+          const int64_t le = (ex - g.ex0) + (int64_t)(ey - g.ey0) * g.nex + (int64_t)(ez - g.ez0) * g.nex * g.ney;
+          const int a = q1_local(ox, oy, oz);
+          double be[3] = {0., 0., 0.};
+          for (int gp = 0; gp < 8; gp++) {
 #pragma unroll
-          for (int r = 0; r < 3; r++) acc[r] += be[(3 * a + r) * g.nelem + le];
+            for (int r = 0; r < 3; r++)
+#pragma unroll
+              for (int q = 0; q < 3; q++) {
+                const int kk = krow(r, q);
+                be[r] += cB[gp][kk][3 * a + r] * sig[kk * NG + gp * E + le] * g.wg;
+              }
+          }
+#pragma unroll
+          for (int r = 0; r < 3; r++) acc[r] += be[r];
         }
       }
     }
-    int m = dirichlet_mask(g, gi, gj, gk);
+    const int m = dirichlet_mask(g, gi, gj, gk);
 #pragma unroll
     for (int r = 0; r < 3; r++) {
       double v = (m >> r & 1) ? 0. : acc[r];
@@ -424,112 +423,81 @@ __global__ __launch_bounds__(TPB) void k_gather_res(Geo g, const double* __restr
       nrm += v * v;
     }
   }
-  double s = block_sum<TPB>(nrm, sh);
+  const double s = block_sum<TPB>(nrm, sh);
   if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
 
 // ---------------------------------------------------------------------------- Jacobian
-// assembly_jac's 4-nest (src/assembly.c:94-99): Ke[i][j] += B[k][i]*C[k][l]*B[l][j]*wg with
-// gp, k, l ascending, evaluated as ((B*C)*B)*wg.  One thread = (element, node a, half of the
-// column nodes b): 4 column blocks x 9 = 36 accumulators.  Zero B terms are skipped (exact).
-// Grid: blocks b -> (XCD group, a, half, element group) so the 16 blocks that read one
-// element group's ctan share an XCD's L2.
-__constant__ int cK[3][3] = {{0, 3, 4}, {1, 3, 5}, {2, 4, 5}};  // rows k with B[k][3a+r] != 0
-
-template <int BH>
-__device__ __forceinline__ void ke_body(const Geo& g, int64_t le, int a, const double* __restrict__ ctan,
-                                        double* __restrict__ Ke) {
+// Element-matrix block Ke[3a+r][3bn+c] (r, c = 0..2) of element le, evaluated on the fly:
+// assembly_jac's 4-nest (src/assembly.c:94-99) restricted to the block, Ke[i][j] +=
+// B[k][i]*C[k][l]*B[l][j]*wg with gp, k, l ascending, as ((B*C)*B)*wg.  Zero B terms and, for the
+// isotropic elastic law (TABLE = false: C from the kernel argument, no per-GP tangent array),
+// C's structural zeros are skipped: each skipped term is +-0 added to a sum that is never -0,
+// so the block is bit-identical to the full loop.  TABLE = true: C_tan per GP from ctan
+// [36][8][nelem] (micropp_C_get_ctan3, src/assembly.c:92).  a, bn are wave-uniform.
+template <bool TABLE>
+__device__ __forceinline__ void ke_block(const Geo& g, const Material& mat, const double* __restrict__ ctan,
+                                         int64_t le, int a, int bn, double (&ke)[9]) {
+#pragma unroll
+  for (int q = 0; q < 9; q++) ke[q] = 0.;
   const int64_t E = g.nelem, NG = 8 * E;
-  double acc[4][9];
-#pragma unroll
-  for (int bb = 0; bb < 4; bb++)
-#pragma unroll
-    for (int q = 0; q < 9; q++) acc[bb][q] = 0.;
   const double wg = g.wg;
   for (int gp = 0; gp < 8; gp++) {
-    // B[k][3a+r] for the 9 non-zero (r,k): wave-uniform scalar loads
-    double Ba[3][3];
+    double Ba[3][3], Bb[3][3];
 #pragma unroll
     for (int r = 0; r < 3; r++)
 #pragma unroll
-      for (int kq = 0; kq < 3; kq++) Ba[r][kq] = cB[gp][cK[r][kq]][3 * a + r];
+      for (int q = 0; q < 3; q++) {
+        Ba[r][q] = cB[gp][krow(r, q)][3 * a + r];
+        Bb[r][q] = cB[gp][krow(r, q)][3 * bn + r];
+      }
 #pragma unroll
-    for (int k = 0; k < 6; k++) {
+    for (int k = 0; k < 6; k++)
 #pragma unroll
       for (int l = 0; l < 6; l++) {
-        const double Ckl = ctan[(k * 6 + l) * NG + gp * E + le];
+        if (!TABLE && !((k < 3 && l < 3) || k == l)) continue;
+        const double Ckl = TABLE ? ctan[(k * 6 + l) * NG + gp * E + le] : mat.C[k * 6 + l];
 #pragma unroll
         for (int r = 0; r < 3; r++) {
-          // position of k in K(r), compile-time
-          const int kq = (k == r) ? 0 : ((k == 3 || (k == 4 && r == 2)) ? 1 : 2);
-          const bool krow = (k == r) || (r == 0 && (k == 3 || k == 4)) || (r == 1 && (k == 3 || k == 5)) ||
-                            (r == 2 && (k == 4 || k == 5));
-          if (!krow) continue;
-          const double t0 = Ba[r][kq] * Ckl;
+          if (!kin(r, k)) continue;
+          const double t0 = Ba[r][kpos(r, k)] * Ckl;
 #pragma unroll
           for (int c = 0; c < 3; c++) {
-            const bool lcol = (l == c) || (c == 0 && (l == 3 || l == 4)) || (c == 1 && (l == 3 || l == 5)) ||
-                              (c == 2 && (l == 4 || l == 5));
-            if (!lcol) continue;
-#pragma unroll
-            for (int bb = 0; bb < 4; bb++) {
-              const int bnode = BH * 4 + bb;
-              acc[bb][r * 3 + c] += t0 * cB[gp][l][3 * bnode + c] * wg;
-            }
+            if (!kin(c, l)) continue;
+            ke[r * 3 + c] += t0 * Bb[c][kpos(c, l)] * wg;
           }
         }
       }
-    }
-  }
-#pragma unroll
-  for (int bb = 0; bb < 4; bb++) {
-    const int bnode = BH * 4 + bb;
-#pragma unroll
-    for (int q = 0; q < 9; q++) Ke[((int64_t)(a * 8 + bnode) * 9 + q) * E + le] = acc[bb][q];
   }
 }
 
-__global__ __launch_bounds__(TPB) void k_element_ke(Geo g, const double* __restrict__ ctan, double* __restrict__ Ke,
-                                                    int64_t ngroups) {
-  // block -> (xcd, a, half, element group): blocks sharing an element group are 8 apart
-  const int64_t b = blockIdx.x;
-  const int x = (int)(b & 7);
-  const int64_t t = b >> 3;
-  const int ah = (int)(t & 15);
-  const int64_t grp = (t >> 4) * 8 + x;
-  if (grp >= ngroups) return;
-  const int64_t le = grp * TPB + threadIdx.x;
-  if (le >= g.nelem) return;
-  const int a = ah >> 1;
-  if (ah & 1) ke_body<1>(g, le, a, ctan, Ke);
-  else ke_body<0>(g, le, a, ctan, Ke);
-}
-
-// MatSetValuesLocal(ADD) + MatAssembly + MatZeroRowsColumns(diag=1) (src/assembly.c:106-112,
-// src/bcs.c:341-347) as a deterministic gather: thread = (owned node, neighbour block nb);
-// the 9 entries are 0 + Ke_e1 + Ke_e2 + ... over the shared elements in ascending element
-// order (the reference's insertion order on one rank), then Dirichlet rows/columns.
-// one 3x3 block A(node g, node g+d) of the assembled matrix: 0 + Ke_e1 + Ke_e2 + ... over the
-// shared elements in ascending element order, then MatZeroRowsColumns(diag = 1)
-__device__ __forceinline__ void matrix_block(const Geo& g, const double* __restrict__ Ke, int gi, int gj, int gk,
-                                             int dx, int dy, int dz, double (&val)[9]) {
+// One 3x3 block A(node g, node g+d) of the assembled matrix (MatSetValuesLocal(ADD) +
+// MatAssembly + MatZeroRowsColumns(diag = 1), src/assembly.c:106-112, src/bcs.c:341-347):
+// 0 + Ke_e1 + Ke_e2 + ... over the shared elements in ascending element order (the reference's
+// insertion order on one rank), each element block computed on the fly (no element-matrix
+// array), then the Dirichlet rows / columns.
+template <bool TABLE>
+__device__ __forceinline__ void matrix_block(const Geo& g, const Material& mat, const double* __restrict__ ctan,
+                                             int gi, int gj, int gk, int dx, int dy, int dz, double (&val)[9]) {
   const int hi = gi + dx, hj = gj + dy, hk = gk + dz;
 #pragma unroll
   for (int q = 0; q < 9; q++) val[q] = 0.;
   if (gi < 0 || gj < 0 || gk < 0 || gi >= g.NX || gj >= g.NY || gk >= g.NZ) return;
   if (hi < 0 || hj < 0 || hk < 0 || hi >= g.NX || hj >= g.NY || hk >= g.NZ) return;
-  for (int ez = gk - 1 + (dz > 0); ez <= gk + (dz < 0 ? -1 : 0); ez++) {
-    if (ez < 0 || ez > g.NZ - 2) continue;
-    for (int ey = gj - 1 + (dy > 0); ey <= gj + (dy < 0 ? -1 : 0); ey++) {
-      if (ey < 0 || ey > g.NY - 2) continue;
-      for (int ex = gi - 1 + (dx > 0); ex <= gi + (dx < 0 ? -1 : 0); ex++) {
-        if (ex < 0 || ex > g.NX - 2) continue;
+  for (int oz = 1; oz >= 0; oz--) {
+    const int pz = oz + dz, ez = gk - oz;
+    if (pz < 0 || pz > 1 || ez < 0 || ez > g.NZ - 2) continue;
+    for (int oy = 1; oy >= 0; oy--) {
+      const int py = oy + dy, ey = gj - oy;
+      if (py < 0 || py > 1 || ey < 0 || ey > g.NY - 2) continue;
+      for (int ox = 1; ox >= 0; ox--) {
+        const int px = ox + dx, ex = gi - ox;
+        if (px < 0 || px > 1 || ex < 0 || ex > g.NX - 2) continue;
         const int64_t le = (ex - g.ex0) + (int64_t)(ey - g.ey0) * g.nex + (int64_t)(ez - g.ez0) * g.nex * g.ney;
-        const int a = q1_local(gi - ex, gj - ey, gk - ez);
-        const int bn = q1_local(hi - ex, hj - ey, hk - ez);
-        const double* src = Ke + (int64_t)((a * 8 + bn) * 9) * g.nelem + le;
+        double ke[9];
+        ke_block<TABLE>(g, mat, ctan, le, q1_local(ox, oy, oz), q1_local(px, py, pz), ke);
 #pragma unroll
-        for (int q = 0; q < 9; q++) val[q] += src[(int64_t)q * g.nelem];
+        for (int q = 0; q < 9; q++) val[q] += ke[q];
       }
     }
   }
@@ -544,18 +512,17 @@ __device__ __forceinline__ void matrix_block(const Geo& g, const double* __restr
     }
 }
 
-// MatSetValuesLocal(ADD) + MatAssembly + MatZeroRowsColumns(diag=1) (src/assembly.c:106-112,
-// src/bcs.c:341-347) as a deterministic gather: thread = (owned node, neighbour block nb);
-// the 9 entries are 0 + Ke_e1 + Ke_e2 + ... over the shared elements in ascending element
-// order (the reference's insertion order on one rank), then Dirichlet rows/columns.
-__global__ __launch_bounds__(TPB) void k_gather_matrix(Geo g, const double* __restrict__ Ke, double* __restrict__ V) {
+// AIJ stencil blocks: thread = (owned node, neighbour block nb)
+template <bool TABLE>
+__global__ __launch_bounds__(TPB) void k_gather_matrix(Geo g, Material mat, const double* __restrict__ ctan,
+                                                       double* __restrict__ V) {
   const int n = blockIdx.x * TPB + threadIdx.x;
   const int nb = blockIdx.y;
   if (n >= g.nown) return;
   int i, j, k;
   node_ijk(g, n, i, j, k);
   double val[9];
-  matrix_block(g, Ke, g.xs + i, g.ys + j, g.zs + k, nb % 3 - 1, (nb / 3) % 3 - 1, nb / 9 - 1, val);
+  matrix_block<TABLE>(g, mat, ctan, g.xs + i, g.ys + j, g.zs + k, nb % 3 - 1, (nb / 3) % 3 - 1, nb / 9 - 1, val);
   double* Vg = V + (int64_t)(n >> 6) * (NPAIR * 128) + 2 * (n & 63);
 #pragma unroll
   for (int q = 0; q < 9; q++) {
@@ -570,7 +537,8 @@ __global__ __launch_bounds__(TPB) void k_gather_matrix(Geo g, const double* __re
 // (the mirrors the owned rows need); owner-computes covers them (every element shared by a
 // ghost and an owned node touches the owned node).  Thread = (padded node, t): t = 0 the
 // diagonal block, t = 1..13 upper block nb = 13 + t.
-__global__ __launch_bounds__(TPB) void k_gather_matrix_sym(Geo g, const double* __restrict__ Ke,
+template <bool TABLE>
+__global__ __launch_bounds__(TPB) void k_gather_matrix_sym(Geo g, Material mat, const double* __restrict__ ctan,
                                                            double* __restrict__ U, int npad) {
   const int p = blockIdx.x * TPB + threadIdx.x;
   const int t = blockIdx.y;
@@ -583,7 +551,7 @@ __global__ __launch_bounds__(TPB) void k_gather_matrix_sym(Geo g, const double* 
   const bool nbr_owned = qi >= 1 && qi <= g.nx && qj >= 1 && qj <= g.ny && qk >= 1 && qk <= g.nz;
   double val[9];
   if (owned || (t > 0 && nbr_owned)) {
-    matrix_block(g, Ke, g.xs + pi - 1, g.ys + pj - 1, g.zs + pk - 1, dx, dy, dz, val);
+    matrix_block<TABLE>(g, mat, ctan, g.xs + pi - 1, g.ys + pj - 1, g.zs + pk - 1, dx, dy, dz, val);
   } else {
 #pragma unroll
     for (int q = 0; q < 9; q++) val[q] = 0.;
@@ -603,68 +571,65 @@ __global__ __launch_bounds__(TPB) void k_gather_matrix_sym(Geo g, const double* 
   }
 }
 
-// AIJ-split assembly, pass 1: thread = (owned node n, lower block nb < 13).  The AIJ value
-// A(n,nb)[r][c] (matrix_block, exactly what k_gather_matrix stores) minus the mirrored upper
-// value U(m, nbp)[c][r] of the neighbour m = n + off(nb), nbp = 26 - nb, as f32 bits:
-// S[(nb*9 + r*3 + c) * npu + u_of(n)].  A width is usable only if every correction is exact in
-// it and U + correction == A bit for bit; d_mask[nb] collects the slots that are non-zero
-// anywhere, d_mask[14] bit 0 = some correction inexact in bf16, bit 1 = inexact in f32.
-// blockIdx.y = 13: the diagonal block's strictly-lower entries against their mirrors.
-__global__ __launch_bounds__(TPB) void k_split_deltas(Geo g, const double* __restrict__ Ke,
-                                                      const double* __restrict__ U, unsigned* __restrict__ S,
-                                                      int64_t npu, unsigned* __restrict__ mask) {
-  __shared__ unsigned s_bits, s_bad;
-  if (threadIdx.x == 0) s_bits = s_bad = 0;
-  __syncthreads();
-  const int n = blockIdx.x * TPB + threadIdx.x;
-  const int nb = blockIdx.y, nbp = 26 - nb;
-  if (n < g.nown && nb == 13) {
-    // diagonal block: stored as its upper triangle; the strictly-lower AIJ entries (1,0), (2,0),
-    // (2,1) are corrected against their mirrors
-    int i, j, k;
-    node_ijk(g, n, i, j, k);
-    double blk[9];
-    matrix_block(g, Ke, g.xs + i, g.ys + j, g.zs + k, 0, 0, 0, blk);
-    const int un = u_of(g, i, j, k);
-    unsigned bits = 0, bad = 0;
+// AIJ-split corrections of one owned node and lower block nb < 13 (nb = 13: the diagonal
+// block's strictly-lower entries against their mirrors): the AIJ value A(n,nb)[r][c]
+// (matrix_block, exactly what k_gather_matrix stores) minus the mirrored upper value
+// U(m, 26-nb)[c][r] of the neighbour m = n + off(nb), as f32 bits (bit q = r*3+c in *valid).
+template <bool TABLE>
+__device__ __forceinline__ void split_block(const Geo& g, const Material& mat, const double* __restrict__ ctan,
+                                            const double* __restrict__ U, int n, int nb, unsigned (&f32)[9],
+                                            unsigned& bits, unsigned& bad) {
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  bits = bad = 0;
+  double low[9], mir[9];
+  if (nb == 13) {
+    matrix_block<TABLE>(g, mat, ctan, g.xs + i, g.ys + j, g.zs + k, 0, 0, 0, low);
 #pragma unroll
-    for (int r = 1; r < 3; r++)
+    for (int r = 0; r < 3; r++)
 #pragma unroll
-      for (int c = 0; c < r; c++) {
-        const double mir = blk[c * 3 + r], d = blk[r * 3 + c] - mir;
-        const unsigned f32 = __float_as_uint((float)d), fb = f32 & 0xffff0000u;
-        const double df = (double)__uint_as_float(f32), db = (double)__uint_as_float(fb);
-        if (db != d || mir + db != blk[r * 3 + c]) bad |= 1;
-        if (df != d || mir + df != blk[r * 3 + c]) bad |= 2;
-        if (d != 0.) bits |= 1u << (r * 3 + c);
-        S[(int64_t)(13 * 9 + r * 3 + c) * npu + un] = f32;
-      }
-    if (bits) atomicOr(&s_bits, bits);
-    if (bad) atomicOr(&s_bad, bad);
-  } else if (n < g.nown) {
-    int i, j, k;
-    node_ijk(g, n, i, j, k);
+      for (int c = 0; c < 3; c++) mir[r * 3 + c] = r > c ? low[c * 3 + r] : low[r * 3 + c];
+  } else {
     const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
-    double low[9];
-    matrix_block(g, Ke, g.xs + i, g.ys + j, g.zs + k, dx, dy, dz, low);
+    matrix_block<TABLE>(g, mat, ctan, g.xs + i, g.ys + j, g.zs + k, dx, dy, dz, low);
     const int um = u_of(g, i + dx, j + dy, k + dz);
     const double* Um = U + (int64_t)(um >> 6) * (UPAIR * 128) + 2 * (um & 63);
-    const int base = 6 + 9 * (nbp - 14), un = u_of(g, i, j, k);
-    unsigned bits = 0, bad = 0;
+    const int base = 6 + 9 * (12 - nb);  // the neighbour's upper block 26 - nb
 #pragma unroll
     for (int r = 0; r < 3; r++)
 #pragma unroll
       for (int c = 0; c < 3; c++) {
         const int s = base + c * 3 + r;
-        const double mir = Um[(s >> 1) * 128 + (s & 1)];
-        const double d = low[r * 3 + c] - mir;
-        const unsigned f32 = __float_as_uint((float)d), fb = f32 & 0xffff0000u;
-        const double df = (double)__uint_as_float(f32), db = (double)__uint_as_float(fb);
-        if (db != d || mir + db != low[r * 3 + c]) bad |= 1;  // not exact in bf16
-        if (df != d || mir + df != low[r * 3 + c]) bad |= 2;  // not exact in f32
-        if (d != 0.) bits |= 1u << (r * 3 + c);
-        S[(int64_t)(nb * 9 + r * 3 + c) * npu + un] = f32;
+        mir[r * 3 + c] = Um[(s >> 1) * 128 + (s & 1)];
       }
+  }
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    const double d = low[q] - mir[q];
+    f32[q] = __float_as_uint((float)d);
+    const unsigned fb = f32[q] & 0xffff0000u;
+    const double df = (double)__uint_as_float(f32[q]), db = (double)__uint_as_float(fb);
+    if (db != d || mir[q] + db != low[q]) bad |= 1;  // not exact in bf16
+    if (df != d || mir[q] + df != low[q]) bad |= 2;  // not exact in f32
+    if (d != 0.) bits |= 1u << q;
+  }
+  if (nb == 13) bits &= (1u << 3) | (1u << 6) | (1u << 7);  // strictly lower: (1,0), (2,0), (2,1)
+}
+
+// AIJ-split assembly, pass 1: thread = (owned node, lower block nb <= 13); d_mask[nb] collects
+// the correction slots that are non-zero anywhere, d_mask[14] bit 0 = some correction inexact
+// in bf16, bit 1 = inexact in f32 (then the matrix is stored as plain AIJ blocks).
+template <bool TABLE>
+__global__ __launch_bounds__(TPB) void k_split_mask(Geo g, Material mat, const double* __restrict__ ctan,
+                                                    const double* __restrict__ U, unsigned* __restrict__ mask) {
+  __shared__ unsigned s_bits, s_bad;
+  if (threadIdx.x == 0) s_bits = s_bad = 0;
+  __syncthreads();
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  const int nb = blockIdx.y;
+  if (n < g.nown) {
+    unsigned f32[9], bits, bad;
+    split_block<TABLE>(g, mat, ctan, U, n, nb, f32, bits, bad);
     if (bits) atomicOr(&s_bits, bits);
     if (bad) atomicOr(&s_bad, bad);
   }
@@ -675,18 +640,31 @@ __global__ __launch_bounds__(TPB) void k_split_deltas(Geo g, const double* __res
   }
 }
 
-// AIJ-split assembly, pass 2: the active slots of every node of the padded box (u_of index),
-// 16 B per quad: 8 bf16 (D[(((u/64) * Lq + p/8) * 64 + u%64) * 8 + p%8]) or 4 f32
-__global__ __launch_bounds__(TPB) void k_split_pack(const unsigned* __restrict__ S, int64_t npu,
-                                                    uint16_t* __restrict__ D, DSlots dl) {
-  const int64_t u = (int64_t)blockIdx.x * TPB + threadIdx.x;
-  if (u >= npu) return;
-  const int per = dl.wide ? 4 : 8;
-  for (int p = 0; p < dl.Lq * per; p++) {
-    const unsigned v = p < dl.L ? S[(int64_t)dl.s[p] * npu + u] : 0u;
-    const int64_t q = (((u >> 6) * dl.Lq + p / per) * 64 + (u & 63));
-    if (dl.wide) reinterpret_cast<unsigned*>(D)[q * 4 + p % 4] = v;
-    else D[q * 8 + p % 8] = (uint16_t)(v >> 16);
+// AIJ-split assembly, pass 2: the same corrections recomputed and written to their packed
+// positions (slot p of node u = u_of: D[(((u/64) * Lq + p/8) * 64 + u%64) * 8 + p%8] as bf16,
+// or 4 f32 per quad); D is zeroed first (ghost nodes and padding hold zeros).
+template <bool TABLE>
+__global__ __launch_bounds__(TPB) void k_split_pack(Geo g, Material mat, const double* __restrict__ ctan,
+                                                    const double* __restrict__ U, uint16_t* __restrict__ D, DSlots dl) {
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  const int nb = blockIdx.y;
+  const unsigned m9 = dl.m9[nb];
+  if (n >= g.nown || !m9) return;
+  unsigned f32[9], bits, bad;
+  split_block<TABLE>(g, mat, ctan, U, n, nb, f32, bits, bad);
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  const int64_t u = u_of(g, i, j, k);
+  int p = dl.pos[nb];
+#pragma unroll
+  for (int q = 0; q < 9; q++) {
+    if (!(m9 >> q & 1)) continue;
+    if (dl.wide) {
+      reinterpret_cast<unsigned*>(D)[((((u >> 6) * dl.Lq + p / 4) * 64 + (u & 63)) * 4) + p % 4] = f32[q];
+    } else {
+      D[((((u >> 6) * dl.Lq + p / 8) * 64 + (u & 63)) * 8) + p % 8] = (uint16_t)(f32[q] >> 16);
+    }
+    p++;
   }
 }
 
@@ -1820,41 +1798,46 @@ void launch_homogenize(Ctx& c) {
   if (c.mat.law == MCX_LAW_PLASTIC)
     hipLaunchKernelGGL(k_homogenize_plastic, dim3(nblk(ngp)), dim3(TPB), 0, c.stream, ngp, c.mat, c.eps, c.hist_old,
                        c.sig, c.ctan, c.hist_new, c.ftrial);
-  else
-    hipLaunchKernelGGL(k_homogenize_elastic, dim3(nblk(ngp)), dim3(TPB), 0, c.stream, ngp, c.mat, c.eps, c.sig,
-                       c.ctan);
+  else if (c.mat.law == MCX_LAW_ELASTIC)
+    hipLaunchKernelGGL(k_homogenize_elastic, dim3(nblk(ngp)), dim3(TPB), 0, c.stream, ngp, c.mat, c.eps, c.sig);
 }
 
 void launch_residual(Ctx& c) {
-  hipLaunchKernelGGL(k_element_res, dim3(nblk(c.g.nelem)), dim3(TPB), 0, c.stream, c.g, c.sig, c.be);
-  hipLaunchKernelGGL(k_gather_res, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.be, c.b, c.partials);
+  hipLaunchKernelGGL(k_residual, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.sig, c.b, c.partials);
 }
 
-void launch_element_ke(Ctx& c) {
-  int64_t ngroups = nblk(c.g.nelem);
-  int64_t blocks = pad8(ngroups) * 16;
-  hipLaunchKernelGGL(k_element_ke, dim3((unsigned)blocks), dim3(TPB), 0, c.stream, c.g, c.ctan, c.Ke, ngroups);
-}
+// every law but the isotropic elastic one hands over a per-GP tangent (ctan)
+static bool table_law(const Ctx& c) { return c.mat.law != MCX_LAW_ELASTIC; }
 
 void launch_gather_matrix(Ctx& c) {
-  hipLaunchKernelGGL(k_gather_matrix, dim3(nblk(c.g.nown), 27), dim3(TPB), 0, c.stream, c.g, c.Ke, c.V);
+  if (table_law(c))
+    hipLaunchKernelGGL(k_gather_matrix<true>, dim3(nblk(c.g.nown), 27), dim3(TPB), 0, c.stream, c.g, c.mat, c.ctan,
+                       c.V);
+  else
+    hipLaunchKernelGGL(k_gather_matrix<false>, dim3(nblk(c.g.nown), 27), dim3(TPB), 0, c.stream, c.g, c.mat, c.ctan,
+                       c.V);
 }
 
 void launch_gather_matrix_sym(Ctx& c) {
   const int npad = c.g.PX * c.g.PY * c.g.PZ;
-  hipLaunchKernelGGL(k_gather_matrix_sym, dim3(nblk(npad), 14), dim3(TPB), 0, c.stream, c.g, c.Ke, c.U, npad);
+  if (table_law(c))
+    hipLaunchKernelGGL(k_gather_matrix_sym<true>, dim3(nblk(npad), 14), dim3(TPB), 0, c.stream, c.g, c.mat, c.ctan,
+                       c.U, npad);
+  else
+    hipLaunchKernelGGL(k_gather_matrix_sym<false>, dim3(nblk(npad), 14), dim3(TPB), 0, c.stream, c.g, c.mat, c.ctan,
+                       c.U, npad);
 }
 
-// exact = the split storage is used (every correction exact and at most split_maxq quads)
+// exact = the split storage is used (every correction exact and at most split_maxq quads).
+// Pass 1 (k_split_mask) finds the active slots and exactness; pass 2 (k_split_pack) recomputes
+// the corrections and writes the packed ones, so no per-slot scratch array exists.
 int build_split(Ctx& c, bool* exact) {
-  // pass-1 scratch: 126 f32 slots (13 lower blocks + the diagonal) per node of the padded box, in
-  // the (then unused) AIJ block storage
-  const int64_t npu = c.npgroups * 64;
-  unsigned* S = reinterpret_cast<unsigned*>(c.V);
-  MCX_HIP(hipMemsetAsync(S, 0, sizeof(unsigned) * 126 * npu, c.stream));
   MCX_HIP(hipMemsetAsync(c.d_mask, 0, 16 * sizeof(unsigned), c.stream));
-  hipLaunchKernelGGL(k_split_deltas, dim3(nblk(c.g.nown), 14), dim3(TPB), 0, c.stream, c.g, c.Ke, c.U, S, npu,
-                     c.d_mask);
+  const dim3 grid(nblk(c.g.nown), 14);
+  if (table_law(c))
+    hipLaunchKernelGGL(k_split_mask<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.ctan, c.U, c.d_mask);
+  else
+    hipLaunchKernelGGL(k_split_mask<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.ctan, c.U, c.d_mask);
   unsigned hm[16];
   MCX_HIP(hipMemcpyAsync(hm, c.d_mask, sizeof(hm), hipMemcpyDeviceToHost, c.stream));
   MCX_HIP(hipStreamSynchronize(c.stream));
@@ -1878,8 +1861,26 @@ int build_split(Ctx& c, bool* exact) {
     *exact = false;
     return 0;
   }
+  const int64_t need = std::max<int64_t>(1, c.npgroups * dl.Lq) * 64 * 16;  // bytes of [u/64][Lq][64] x 16 B
+  if (need > c.D_bytes) {
+    if (c.D) {
+      MCX_HIP(hipStreamSynchronize(c.stream));
+      MCX_HIP(hipFree(c.D));
+      c.device_bytes -= c.D_bytes;
+      c.D = nullptr;
+    }
+    MCX_HIP(hipMalloc(&c.D, need));
+    c.D_bytes = need;
+    c.device_bytes += need;
+  }
   c.dsl = dl;
-  if (dl.L) hipLaunchKernelGGL(k_split_pack, dim3(nblk(npu)), dim3(TPB), 0, c.stream, S, npu, c.D, dl);
+  if (dl.L) {
+    MCX_HIP(hipMemsetAsync(c.D, 0, (size_t)c.npgroups * dl.Lq * 64 * 16, c.stream));
+    if (table_law(c))
+      hipLaunchKernelGGL(k_split_pack<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.ctan, c.U, c.D, dl);
+    else
+      hipLaunchKernelGGL(k_split_pack<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.ctan, c.U, c.D, dl);
+  }
   return 0;
 }
 

@@ -16,7 +16,6 @@ constexpr int NGP = 8, NPE = 8, NVOI = 6;
 constexpr int NSLOT = 243;   // 27 neighbour blocks x 3x3
 constexpr int NPAIR = 122;   // slots stored as double2 pairs (slot 243 = zero pad)
 constexpr int GROUP = 64;    // nodes per AoSoA group (= one wavefront)
-constexpr int NKE = 576;     // 24x24 element matrix
 constexpr int USLOT = 123;   // sbaij: 6 upper-triangle diagonal values + 13 upper blocks x 9
 constexpr int UPAIR = 62;
 
@@ -125,8 +124,10 @@ struct Ctx {
   double* V = nullptr;       // aij stencil-block matrix, AoSoA [ngroups][NPAIR][64] double2
   double* U = nullptr;       // sbaij upper stencil blocks over the padded box [npgroups][UPAIR][64] double2
   uint16_t* D = nullptr;     // AIJ-split: bf16 corrections of the padded box [u_of/64][dsl.Lq][64] x 8
+  int64_t D_bytes = 0;       // allocated bytes of D (grown to the active slots' quads)
   unsigned* d_mask = nullptr;  // AIJ-split assembly: [0..13] slot masks per lower block, [14] inexact
   int fmt = FMT_V;           // storage the matrix is currently assembled in
+  bool assembled = false;    // a matrix has been assembled (mcx_assembly_jac)
   int aij_split = 1;         // aij: assemble in FMT_SPLIT when every correction is exact in bf16
   int split_maxq = 4;        // AIJ-split only while the corrections fit this many 16-B quads per node
   int split_dbg = 0;         // timing-only diagnostics of the split SpMV (option split_dbg)
@@ -144,12 +145,10 @@ struct Ctx {
   int64_t partials_cap = 0;
   double* eps = nullptr;     // [6][8][nelem]
   double* sig = nullptr;     // [6][8][nelem]
-  double* ctan = nullptr;    // [36][8][nelem]
+  double* ctan = nullptr;    // [36][8][nelem] per-GP tangent (plastic / external laws only)
   double* hist_old = nullptr; // plastic law: [7][8][nelem] plastic strain (tensor comps) + alpha
   double* hist_new = nullptr;
   double* ftrial = nullptr;  // [8][nelem]
-  double* Ke = nullptr;      // [576][nelem] element matrices (assembly scratch)
-  double* be = nullptr;      // [24][nelem] element residuals
   double* partials = nullptr;
   double* red = nullptr;     // reduction results (device)
   double* red_loc = nullptr; // local sums before all-reduce
@@ -160,6 +159,13 @@ struct Ctx {
   int64_t ngroups = 0;
   int64_t device_bytes = 0;
   int64_t nnz_local = 0, nnz_global = 0;
+
+  // external Gauss-point law (-mat_law external): host MicroPP-shaped callbacks or a device law
+  mcx_micropp_api mpp{};
+  bool has_mpp = false;
+  mcx_device_law dlaw{};
+  bool has_dlaw = false;
+  std::vector<double> h_gp;  // host staging of eps / sig / ctan for the host callbacks
 
   // timing
   bool timing = false;
@@ -203,10 +209,9 @@ void launch_apply_bc_u(Ctx& c, double U);
 void launch_strains(Ctx& c);
 void launch_homogenize(Ctx& c);
 void launch_residual(Ctx& c);          // b + partial sums of b.b
-void launch_element_ke(Ctx& c);
 void launch_gather_matrix(Ctx& c);
 void launch_gather_matrix_sym(Ctx& c);
-int build_split(Ctx& c, bool* exact);  // AIJ-split corrections from U + Ke (exact = usable)
+int build_split(Ctx& c, bool* exact);  // AIJ-split corrections from U (exact = usable)
 void launch_jacobi(Ctx& c);
 void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated);
 void launch_update_u(Ctx& c);
