@@ -128,7 +128,8 @@ typedef struct {
 typedef struct {
   /* wall milliseconds of the last call of each phase (HIP events on the compute stream) */
   double strains_ms, homogenize_ms, residual_ms, jacobian_ms, solve_ms, update_ms;
-  /* SpMV kernel inside the last mcx_solve: launches counted and summed device time */
+  /* SpMV kernel inside the last mcx_solve: HIP event pairs around every 8th launch (at most
+     512), their count and summed device time */
   int64_t spmv_launches;
   double spmv_ms_total;
   int64_t spmv_bytes_per_launch; /* algorithmic bytes of one SpMV (values + x once + y once) */

@@ -185,8 +185,8 @@ static int cg_solve(Ctx& c, int* its, double* rnorm, int* reason) {
   launch_cg_init(c);
   int rc = cg_finish_init(c);
   if (rc) return rc;
-  // spmv event pairs (timing mode): the first kTimed iterations
-  const int kTimed = 256;
+  // spmv event pairs (timing mode): every 8th iteration (spread over the solve), at most kTimed
+  const int kTimed = 512;
   if (c.timing && c.ev_pool.empty()) {
     c.ev_pool.resize(2 * kTimed);
     for (auto& e : c.ev_pool) MCX_HIP(hipEventCreate(&e));
@@ -194,14 +194,17 @@ static int cg_solve(Ctx& c, int* its, double* rnorm, int* reason) {
   // chunks of CH iterations; the host polls the previous chunk's CgState while the next chunk
   // runs (kernels of a converged solve return at once)
   const int CH = 8;
-  int issued = 0, slot = 0, pending = -1;
+  int issued = 0, slot = 0, pending = -1, npairs = 0;
+  std::vector<int> pair_it;
   const int cap = c.o.ksp_max_it + 4 * CH;
   while (true) {
     for (int q = 0; q < CH; q++, issued++) {
       hipEvent_t e0 = nullptr, e1 = nullptr;
-      if (c.timing && issued < kTimed) {
-        e0 = c.ev_pool[2 * issued];
-        e1 = c.ev_pool[2 * issued + 1];
+      if (c.timing && (issued & 7) == 4 && npairs < kTimed) {
+        e0 = c.ev_pool[2 * npairs];
+        e1 = c.ev_pool[2 * npairs + 1];
+        pair_it.push_back(issued);
+        npairs++;
       }
       if ((rc = cg_iteration(c, e0, e1))) return rc;
     }
@@ -232,12 +235,14 @@ static int cg_solve(Ctx& c, int* its, double* rnorm, int* reason) {
     MCX_HIP(hipMemcpy(c.last_hist.data(), c.hist, sizeof(double) * (fin.its + 1), hipMemcpyDeviceToHost));
   }
   if (c.timing) {
-    int n = std::min(fin.its, std::min(issued, kTimed));
+    int n = 0;  // pairs around iterations that ran (later launches of the last chunk return at once)
     double tot = 0.;
-    for (int q = 0; q < n; q++) {
+    for (int q = 0; q < npairs; q++) {
+      if (pair_it[q] >= fin.its) break;
       float ms = 0.f;
       MCX_HIP(hipEventElapsedTime(&ms, c.ev_pool[2 * q], c.ev_pool[2 * q + 1]));
       tot += ms;
+      n++;
     }
     c.t.spmv_launches = n;
     c.t.spmv_ms_total = tot;
