@@ -53,9 +53,10 @@ static int free_ctx(Ctx* c) {
   if (!c) return 0;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
   void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->V, c->U, c->D, c->d_mask, c->eps, c->sig, c->ctan,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
-                  c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf};
+                  c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf, c->halo.d_bnd};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_cg) (void)hipHostFree(c->h_cg);
@@ -68,6 +69,9 @@ static int free_ctx(Ctx* c) {
   for (int q = 0; q < 2; q++)
     if (c->ev_chunk[q]) (void)hipEventDestroy(c->ev_chunk[q]);
   comm_destroy(*c);
+  if (c->ev_pack) (void)hipEventDestroy(c->ev_pack);
+  if (c->ev_comm) (void)hipEventDestroy(c->ev_comm);
+  if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -115,6 +119,9 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
     c.fmt = FMT_U;
   }
   MCX_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+  MCX_HIP(hipStreamCreateWithFlags(&c.comm_stream, hipStreamNonBlocking));
+  MCX_HIP(hipEventCreateWithFlags(&c.ev_pack, hipEventDisableTiming));
+  MCX_HIP(hipEventCreateWithFlags(&c.ev_comm, hipEventDisableTiming));
   MCX_HIP(hipEventCreate(&c.ev_a));
   MCX_HIP(hipEventCreate(&c.ev_b));
   for (auto& pr : c.ev_phase)
@@ -1253,6 +1260,23 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.split_tx = v;
     if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
       set_error("split_tx: partials buffer too small");
+      return 2;
+    }
+    return 0;
+  }
+  if (!std::strcmp(name, "halo_overlap")) {
+    c.overlap = value != 0.;
+    return 0;
+  }
+  if (!std::strcmp(name, "split_ty")) {
+    const int v = (int)value;
+    if (v != 0 && v != 2 && v != 4 && v != 8 && v != 16) {
+      set_error("split_ty: 0, 2, 4, 8 or 16");
+      return 2;
+    }
+    c.split_ty = v;
+    if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
+      set_error("split_ty: partials buffer too small");
       return 2;
     }
     return 0;

@@ -2,9 +2,11 @@
 //
 // Replaces the MPI traffic PETSc generates on the hot path: the
 // DMGlobalToLocal / MatMult ghost scatter becomes one grouped ncclSend/ncclRecv per
-// neighbour (each neighbour of a 2x2x2 box is one direct xGMI link), and the 1-double
-// MPI_Allreduce of VecTDot/VecNorm becomes ncclAllReduce on the compute stream, so the CG
-// loop never returns to the host between iterations.
+// neighbour (each neighbour of a 2x2x2 box is one direct xGMI link) on a comm stream that
+// overlaps interior work (halo_start / halo_finish), and the 1-double MPI_Allreduce of
+// VecTDot/VecNorm becomes ncclAllReduce on the compute stream, so the CG loop never returns to
+// the host between iterations.  Collective order is identical on every rank: each halo is
+// finished (waited for by the compute stream) before the next all-reduce is enqueued.
 #include <rccl/rccl.h>
 
 #include <condition_variable>
@@ -60,47 +62,65 @@ void group_barrier(LocalGroup* g) {
   }
 }
 
-static int halo_exchange_local(Ctx& c, double* xpad) {
-  LocalGroup* g = c.lg;
+// Forward halo in two halves so interior work can run while the bytes move:
+//   halo_start:  pack the sent nodes (compute stream), then the exchange on the comm stream
+//                (grouped ncclSend/ncclRecv, or device copies from the neighbours' send buffers
+//                for the in-process transport);
+//   halo_finish: the compute stream waits for the exchange and unpacks into the ghost layer.
+// halo_exchange = start + finish.  Anything enqueued on the compute stream in between overlaps
+// the exchange (cg_iteration: the interior p update).
+int halo_start(Ctx& c, double* xpad) {
+  if (c.nranks <= 1 || c.halo.nbr_rank.empty()) return 0;
   HaloPlan& h = c.halo;
-  // neighbours finished reading my previous send buffer
-  for (int q : h.nbr_rank) MCX_HIP(hipStreamWaitEvent(c.stream, g->ev_halo_done[q], 0));
-  launch_pack(c, xpad);
-  MCX_HIP(hipEventRecord(g->ev_packed[c.rank], c.stream));
-  group_barrier(g);
-  for (size_t t = 0; t < h.nbr_rank.size(); t++) {
-    const Ctx& q = *g->members[h.nbr_rank[t]];
-    size_t idx = 0;
-    while (idx < q.halo.nbr_rank.size() && q.halo.nbr_rank[idx] != c.rank) idx++;
-    if (idx == q.halo.nbr_rank.size() || q.halo.send_cnt[idx] != h.recv_cnt[t]) {
-      set_error("local halo: inconsistent neighbour plans");
-      return 22;
+  if (c.lg) {
+    LocalGroup* g = c.lg;
+    // neighbours finished reading my previous send buffer
+    for (int q : h.nbr_rank) MCX_HIP(hipStreamWaitEvent(c.stream, g->ev_halo_done[q], 0));
+    launch_pack(c, xpad);
+    MCX_HIP(hipEventRecord(g->ev_packed[c.rank], c.stream));
+    group_barrier(g);
+    for (size_t t = 0; t < h.nbr_rank.size(); t++) {
+      const Ctx& q = *g->members[h.nbr_rank[t]];
+      size_t idx = 0;
+      while (idx < q.halo.nbr_rank.size() && q.halo.nbr_rank[idx] != c.rank) idx++;
+      if (idx == q.halo.nbr_rank.size() || q.halo.send_cnt[idx] != h.recv_cnt[t]) {
+        set_error("local halo: inconsistent neighbour plans");
+        return 22;
+      }
+      MCX_HIP(hipStreamWaitEvent(c.comm_stream, g->ev_packed[h.nbr_rank[t]], 0));
+      MCX_HIP(hipMemcpyAsync(h.d_recvbuf + 3 * h.recv_off[t], q.halo.d_sendbuf + 3 * q.halo.send_off[idx],
+                             sizeof(double) * 3 * h.recv_cnt[t], hipMemcpyDeviceToDevice, c.comm_stream));
     }
-    MCX_HIP(hipStreamWaitEvent(c.stream, g->ev_packed[h.nbr_rank[t]], 0));
-    MCX_HIP(hipMemcpyAsync(h.d_recvbuf + 3 * h.recv_off[t], q.halo.d_sendbuf + 3 * q.halo.send_off[idx],
-                           sizeof(double) * 3 * h.recv_cnt[t], hipMemcpyDeviceToDevice, c.stream));
+    MCX_HIP(hipEventRecord(g->ev_halo_done[c.rank], c.comm_stream));
+    MCX_HIP(hipEventRecord(c.ev_comm, c.comm_stream));
+    group_barrier(g);  // every member recorded ev_halo_done before anyone waits on it again
+    return 0;
   }
-  MCX_HIP(hipEventRecord(g->ev_halo_done[c.rank], c.stream));
-  group_barrier(g);
+  launch_pack(c, xpad);
+  MCX_HIP(hipEventRecord(c.ev_pack, c.stream));
+  MCX_HIP(hipStreamWaitEvent(c.comm_stream, c.ev_pack, 0));
+  MCX_NCCL(ncclGroupStart());
+  for (size_t q = 0; q < h.nbr_rank.size(); q++) {
+    MCX_NCCL(ncclSend(h.d_sendbuf + 3 * h.send_off[q], 3 * h.send_cnt[q], ncclDouble, h.nbr_rank[q],
+                      (ncclComm_t)c.comm, c.comm_stream));
+    MCX_NCCL(ncclRecv(h.d_recvbuf + 3 * h.recv_off[q], 3 * h.recv_cnt[q], ncclDouble, h.nbr_rank[q],
+                      (ncclComm_t)c.comm, c.comm_stream));
+  }
+  MCX_NCCL(ncclGroupEnd());
+  MCX_HIP(hipEventRecord(c.ev_comm, c.comm_stream));
+  return 0;
+}
+
+int halo_finish(Ctx& c, double* xpad) {
+  if (c.nranks <= 1 || c.halo.nbr_rank.empty()) return 0;
+  MCX_HIP(hipStreamWaitEvent(c.stream, c.ev_comm, 0));
   launch_unpack(c, xpad);
   return 0;
 }
 
 int halo_exchange(Ctx& c, double* xpad) {
-  if (c.nranks <= 1 || c.halo.nbr_rank.empty()) return 0;
-  if (c.lg) return halo_exchange_local(c, xpad);
-  HaloPlan& h = c.halo;
-  launch_pack(c, xpad);
-  MCX_NCCL(ncclGroupStart());
-  for (size_t q = 0; q < h.nbr_rank.size(); q++) {
-    MCX_NCCL(ncclSend(h.d_sendbuf + 3 * h.send_off[q], 3 * h.send_cnt[q], ncclDouble, h.nbr_rank[q],
-                      (ncclComm_t)c.comm, c.stream));
-    MCX_NCCL(ncclRecv(h.d_recvbuf + 3 * h.recv_off[q], 3 * h.recv_cnt[q], ncclDouble, h.nbr_rank[q],
-                      (ncclComm_t)c.comm, c.stream));
-  }
-  MCX_NCCL(ncclGroupEnd());
-  launch_unpack(c, xpad);
-  return 0;
+  int rc = halo_start(c, xpad);
+  return rc ? rc : halo_finish(c, xpad);
 }
 
 static int allreduce_op(Ctx& c, const double* in, double* out, int count, int op) {

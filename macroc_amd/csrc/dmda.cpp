@@ -1,3 +1,4 @@
+#include <algorithm>
 // dmda.cpp — host-side DMDA decomposition of the MI355X MacroC path.
 //
 // Restates what PETSc's DMDACreate3d/DMSetUp (src/init.c:85-94 of the reference) produce for
@@ -245,6 +246,19 @@ int build_halo_plan(Ctx& c) {
   MCX_HIP(hipMemcpy(h.d_send_idx, sidx.data(), sizeof(int) * h.nsend, hipMemcpyHostToDevice));
   MCX_HIP(hipMemcpy(h.d_recv_idx, ridx.data(), sizeof(int) * h.nrecv, hipMemcpyHostToDevice));
   c.device_bytes += (int64_t)(sizeof(int) + 3 * sizeof(double)) * (h.nsend + h.nrecv);
+  // the sent nodes once each, as owned indices (their p update runs before the exchange)
+  const Geo& g = c.g;
+  std::vector<int> bnd(sidx);
+  std::sort(bnd.begin(), bnd.end());
+  bnd.erase(std::unique(bnd.begin(), bnd.end()), bnd.end());
+  for (int& p : bnd) {
+    const int pi = p % g.PX, pj = (p / g.PX) % g.PY, pk = p / (g.PX * g.PY);
+    p = (pi - 1) + (pj - 1) * g.nx + (pk - 1) * g.nx * g.ny;
+  }
+  h.nbnd = (int64_t)bnd.size();
+  MCX_HIP(hipMalloc(&h.d_bnd, sizeof(int) * h.nbnd));
+  MCX_HIP(hipMemcpy(h.d_bnd, bnd.data(), sizeof(int) * h.nbnd, hipMemcpyHostToDevice));
+  c.device_bytes += (int64_t)sizeof(int) * h.nbnd;
   return 0;
 }
 

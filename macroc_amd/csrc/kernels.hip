@@ -1316,9 +1316,11 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
       // Edge terms: the lower terms the tile's y-edge rows would pull after the barrier (row 0:
       // sources at dy = -1, row TY-1: dy = +1), computed now by one helper thread each into
       // edge[][h] (the same expression as the pull), so no wave waits on a chain of pulls there.
-      //   ph 0: h < 3 TX: row 0, this plane, nb 9 + h / TX;  3 TX <= h < 4 TX: row TY-1, next plane, nb 8
-      //   ph 1: h < 2 TX: row TY-1, next plane, nb 6 + h / TX;  ph 2: h < 3 TX: row 0, next plane, nb h / TX
+      // (Helpers for every out-of-tile term, x-edge columns included, and squarer tiles were
+      // slower: profiles/r02b_ab_tiles.log.)
       if constexpr (HELP) {
+        //   ph 0: h < 3 TX: row 0, this plane, nb 9 + h / TX;  3 TX <= h < 4 TX: row TY-1, next plane, nb 8
+        //   ph 1: h < 2 TX: row TY-1, next plane, nb 6 + h / TX;  ph 2: h < 3 TX: row 0, next plane, nb h / TX
         const int grp = me / TX, it = txi * TX + me % TX;  // group: wave-uniform (TX % 64 == 0)
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -1343,9 +1345,10 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
       __syncthreads();
       if (active) {
         // lower term nb: from the helpers' edge[] (y-edge rows), the LDS exchange or pulled now
-        auto term2 = [&](int nb, int eidx, int pcn, int ucn, int kt, double& c0, double& c1, double& c2) {
+        auto term2 = [&](int nb, int pcn, int ucn, int kt, double& c0, double& c1, double& c2) {
           const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1;
           if (HELP && dy != 0 && (ly + dy < 0 || ly + dy >= TY)) {
+            const int eidx = (nb >= 9 ? (nb - 9) * TX : (nb == 8 ? 3 * TX : (nb >= 5 ? (nb - 6) * TX : nb * TX))) + lx;
             c0 = edge[0][eidx];
             c1 = edge[1][eidx];
             c2 = edge[2][eidx];
@@ -1358,7 +1361,7 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
 #pragma unroll
           for (int nb = 9; nb <= 12; nb++) {
             double c0, c1, c2;
-            term2(nb, (nb - 9) * TX + lx, pc, uc, k, c0, c1, c2);
+            term2(nb, pc, uc, k, c0, c1, c2);
             a0 += c0;
             a1 += c1;
             a2 += c2;
@@ -1371,9 +1374,8 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
 #pragma unroll
           for (int nb = 0; nb <= 8; nb++) {
             if (nb < nb_lo || nb > nb_hi) continue;
-            const int eidx = (ph == 0 ? 3 * TX : 0) + (ph == 1 ? nb - 6 : (ph == 2 ? nb : 0)) * TX + lx;
             double c0, c1, c2;
-            term2(nb, eidx, pc + PXY, uc + g.UXY, k + 1, c0, c1, c2);
+            term2(nb, pc + PXY, uc + g.UXY, k + 1, c0, c1, c2);
             n0 += c0;
             n1 += c1;
             n2 += c2;
@@ -1502,11 +1504,9 @@ __device__ __forceinline__ void st(double* p, double v) {
 }
 
 template <bool NT>
-__global__ void k_cg_pupdate(Geo g, const double* __restrict__ z, double* __restrict__ ppad,
-                             double* __restrict__ x, const CgState* __restrict__ cg) {
-  if (cg->reason) return;
-  int n = blockIdx.x * TPB + threadIdx.x;
-  if (n >= g.nown) return;
+__device__ __forceinline__ void pupdate_node(const Geo& g, int n, const double* __restrict__ z,
+                                             double* __restrict__ ppad, double* __restrict__ x,
+                                             const CgState* __restrict__ cg) {
   int i, j, k;
   node_ijk(g, n, i, j, k);
   const int pc = pad_of(g, i, j, k);
@@ -1523,6 +1523,37 @@ __global__ void k_cg_pupdate(Geo g, const double* __restrict__ z, double* __rest
       st<NT>(&ppad[3 * pc + d], z[q] + bc * pv);
     }
   }
+}
+
+// a node some neighbour rank receives: on a subdomain face that has a neighbour (width-1 halo)
+__device__ __forceinline__ bool sent_node(const Geo& g, int i, int j, int k) {
+  return (i == 0 && g.xs > 0) || (i == g.nx - 1 && g.xs + g.nx < g.NX) || (j == 0 && g.ys > 0) ||
+         (j == g.ny - 1 && g.ys + g.ny < g.NY) || (k == 0 && g.zs > 0) || (k == g.nz - 1 && g.zs + g.nz < g.NZ);
+}
+
+// SKIP_SENT: the sent nodes were updated before the halo exchange (k_cg_pupdate_list)
+template <bool NT, bool SKIP_SENT = false>
+__global__ void k_cg_pupdate(Geo g, const double* __restrict__ z, double* __restrict__ ppad,
+                             double* __restrict__ x, const CgState* __restrict__ cg) {
+  if (cg->reason) return;
+  int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  if (SKIP_SENT) {
+    int i, j, k;
+    node_ijk(g, n, i, j, k);
+    if (sent_node(g, i, j, k)) return;
+  }
+  pupdate_node<NT>(g, n, z, ppad, x, cg);
+}
+
+template <bool NT>
+__global__ void k_cg_pupdate_list(Geo g, const double* __restrict__ z, double* __restrict__ ppad,
+                                  double* __restrict__ x, const CgState* __restrict__ cg,
+                                  const int* __restrict__ list, int64_t cnt) {
+  if (cg->reason) return;
+  const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (t >= cnt) return;
+  pupdate_node<NT>(g, list[t], z, ppad, x, cg);
 }
 
 // the last iteration's x += alpha p (when that iteration reached its update)
@@ -1763,7 +1794,7 @@ int64_t node_blocks(const Ctx& c) { return nblk(c.g.nown); }
 // AIJ-split SpMV tile: the phased z-marching kernel, 128x4 where the subdomain is wide enough
 static void split_shape(const Ctx& c, int& ztx, int& zty) {
   ztx = c.split_tx ? c.split_tx : (c.g.nx >= 256 ? 256 : (c.g.nx >= 128 ? 128 : 64));
-  zty = 4;
+  zty = c.split_ty ? c.split_ty : 4;  // tiles 256x4 (1 block / CU), 128x4 (2), 64x4 (4); 256x2, 128x8, 64x16, 32x32
 }
 
 int64_t spmv_grid_blocks(const Ctx& c) {
@@ -1898,8 +1929,11 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
     int ztx, zty;
     split_shape(c, ztx, zty);
     const ZTiling zt = z_tiling(c.g, ztx, zty, c.spmv_zblocks);
-    if (ztx == 256) launch_symp<256, 4, true>(c, xpad, y, dot, gated, zt, nb);
+    if (ztx == 256 && zty == 4) launch_symp<256, 4, true>(c, xpad, y, dot, gated, zt, nb);
+    else if (ztx == 256) launch_symp<256, 2, true>(c, xpad, y, dot, gated, zt, nb);
+    else if (ztx == 128 && zty == 8) launch_symp<128, 8, true>(c, xpad, y, dot, gated, zt, nb);
     else if (ztx == 128) launch_symp<128, 4, true>(c, xpad, y, dot, gated, zt, nb);
+    else if (ztx == 64 && zty == 16) launch_symp<64, 16, true>(c, xpad, y, dot, gated, zt, nb);
     else launch_symp<64, 4, true>(c, xpad, y, dot, gated, zt, nb);
     return;
   }
@@ -2040,16 +2074,44 @@ void launch_cg_xfinal(Ctx& c) {
   hipLaunchKernelGGL(k_cg_xfinal, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.p_pad, c.du, c.cg);
 }
 
+void launch_cg_pupdate(Ctx& c, int part) {
+  const unsigned nbn = nblk(c.g.nown);
+  if (part == 1) {
+    if (!c.halo.nbnd) return;
+    const unsigned nb = nblk(c.halo.nbnd);
+    if (c.cg_nt)
+      hipLaunchKernelGGL(k_cg_pupdate_list<true>, dim3(nb), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg,
+                         c.halo.d_bnd, c.halo.nbnd);
+    else
+      hipLaunchKernelGGL(k_cg_pupdate_list<false>, dim3(nb), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg,
+                         c.halo.d_bnd, c.halo.nbnd);
+  } else if (part == 2) {
+    if (c.cg_nt)
+      hipLaunchKernelGGL((k_cg_pupdate<true, true>), dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg);
+    else
+      hipLaunchKernelGGL((k_cg_pupdate<false, true>), dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg);
+  } else {
+    if (c.cg_nt)
+      hipLaunchKernelGGL((k_cg_pupdate<true>), dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg);
+    else
+      hipLaunchKernelGGL((k_cg_pupdate<false>), dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg);
+  }
+}
+
 int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1) {
-  const int nbn = (int)nblk(c.g.nown);
   const int nbs = (int)spmv_grid_blocks(c);
   const int nbu = (int)((c.g.nown + UTPB - 1) / UTPB);
-  if (c.cg_nt)
-    hipLaunchKernelGGL(k_cg_pupdate<true>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg);
-  else
-    hipLaunchKernelGGL(k_cg_pupdate<false>, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg);
-  int rc = halo_exchange(c, c.p_pad);
-  if (rc) return rc;
+  int rc;
+  if (c.nranks > 1 && c.overlap && c.halo.nbnd) {
+    // the sent nodes' p first, then their exchange overlaps the interior p update
+    launch_cg_pupdate(c, 1);
+    if ((rc = halo_start(c, c.p_pad))) return rc;
+    launch_cg_pupdate(c, 2);
+    if ((rc = halo_finish(c, c.p_pad))) return rc;
+  } else {
+    launch_cg_pupdate(c, 0);
+    if ((rc = halo_exchange(c, c.p_pad))) return rc;
+  }
   if (ev0) MCX_HIP(hipEventRecord(ev0, c.stream));
   launch_spmv(c, c.p_pad, c.w, true, true);
   if (ev1) MCX_HIP(hipEventRecord(ev1, c.stream));

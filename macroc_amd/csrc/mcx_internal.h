@@ -59,6 +59,8 @@ struct HaloPlan {
   double* d_sendbuf = nullptr;
   double* d_recvbuf = nullptr;
   int64_t nsend = 0, nrecv = 0;
+  int* d_bnd = nullptr;               // owned node index of every sent node, each once
+  int64_t nbnd = 0;
 };
 
 struct Ctx;
@@ -108,6 +110,9 @@ struct Ctx {
   double dy = 0;
   Material mat{};
   hipStream_t stream = nullptr;
+  hipStream_t comm_stream = nullptr;            // halo exchange (overlaps interior work on `stream`)
+  hipEvent_t ev_pack = nullptr, ev_comm = nullptr;
+  int overlap = 1;                              // CG: interior p update overlaps the halo (option halo_overlap)
   void* comm = nullptr;                         // ncclComm_t when nranks > 1 (RCCL transport)
   LocalGroup* lg = nullptr;                     // in-process transport
   HaloPlan halo;
@@ -132,7 +137,8 @@ struct Ctx {
   int split_maxq = 4;        // AIJ-split only while the corrections fit this many 16-B quads per node
   int split_dbg = 0;         // timing-only diagnostics of the split SpMV (option split_dbg)
   int split_wide = 0;        // force f32 corrections (testing the wide path)
-  int split_tx = 0;          // AIJ-split tile width (0: by subdomain width; option split_tx)
+  int split_tx = 0;          // AIJ-split tile width (0: by subdomain width, 4 rows; else 1024 / split_tx rows)
+  int split_ty = 0;          // AIJ-split: 2 with split_tx 256 selects 256x2 tiles (option split_ty)
   DSlots dsl;
   int64_t npgroups = 0;
   int64_t nupper_local = 0;  // sbaij: stored upper values of the owned rows
@@ -195,7 +201,9 @@ int64_t count_upper_values(const Ctx& c);
 // ---- communication (comm.cpp)
 int comm_init(Ctx& c, const void* id);
 void comm_destroy(Ctx& c);
-int halo_exchange(Ctx& c, double* xpad);
+int halo_exchange(Ctx& c, double* xpad);   // halo_start + halo_finish
+int halo_start(Ctx& c, double* xpad);      // pack + exchange on the comm stream
+int halo_finish(Ctx& c, double* xpad);     // compute stream waits, unpacks
 int allreduce_sum(Ctx& c, const double* in, double* out, int count);
 int allreduce_max(Ctx& c, const double* in, double* out, int count);
 int allreduce_prepare(Ctx& c);
@@ -216,6 +224,7 @@ void launch_jacobi(Ctx& c);
 void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated);
 void launch_update_u(Ctx& c);
 void launch_cg_xfinal(Ctx& c);
+void launch_cg_pupdate(Ctx& c, int part);  // 0 all owned nodes, 1 the sent (subdomain-face) nodes, 2 the rest
 void launch_reduce(Ctx& c, int nvals, int nparts, double* out);
 void launch_cg_init(Ctx& c);
 int cg_iteration(Ctx& c, hipEvent_t spmv_start, hipEvent_t spmv_stop);

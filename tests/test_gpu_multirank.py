@@ -147,7 +147,7 @@ def _multirank(name, sbaij, extra=(), split=False):
         assert not du.any()
 
 
-@pytest.mark.parametrize("mat", ["aij", "sbaij", "sbaij-phased"])
+@pytest.mark.parametrize("mat", ["aij", "aij-tall", "sbaij", "sbaij-phased"])
 @pytest.mark.parametrize("grid,procs", [((140, 10, 8), (2, 1, 1)), ((132, 12, 12), (2, 2, 2))])
 def test_multirank_full_tiles(grid, procs, mat):
     """Subdomains wide enough for full z-marching tiles (64 x 4) next to partial ones: internal
@@ -160,7 +160,9 @@ def test_multirank_full_tiles(grid, procs, mat):
     nr, rtol = px * py * pz, 1e-10
     argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
             "-da_processors_z", pz, "-ksp_rtol", repr(rtol), "-dm_mat_type", mat.split("-")[0]]
-    opts = {"aij": [("split_maxq", 30)], "sbaij": [], "sbaij-phased": [("spmv_kernel", 8)]}[mat]  # 8: phased 64x4
+    # 8: phased 64x4; aij-tall: 64x16 AIJ-split tiles (internal x faces at every tile's lanes 0 / 63)
+    opts = {"aij": [("split_maxq", 30)], "aij-tall": [("split_maxq", 30), ("split_tx", 64), ("split_ty", 16)], "sbaij": [],
+            "sbaij-phased": [("spmv_kernel", 8)]}[mat]
     ref = O.Problem(NX, NY, NZ, rtol=rtol)
     ref.apply_bc_u(ref.get_displacement(0))
     ref.apply_bc_u(ref.get_displacement(1))
@@ -180,3 +182,19 @@ def test_multirank_full_tiles(grid, procs, mat):
         assert np.all(np.abs(o["y"] - y1[o["nat"]]) <= 1e-14 * absrow[o["nat"]] + 1e-300)
         du[o["nat"]] = o["du"]
     assert np.linalg.norm(du - duref) <= 1e-8 * np.linalg.norm(duref)
+
+
+@pytest.mark.parametrize("grid,procs", [((20, 12, 10), (2, 2, 1)), ((12, 10, 14), (2, 2, 2))])
+def test_halo_overlap_bitwise(grid, procs):
+    """The CG's halo exchange overlapped with the interior p update (sent nodes updated first,
+    exchange on the comm stream, rest of p meanwhile) computes exactly what the serialised
+    exchange computes: du bitwise equal, same iteration count."""
+    NX, NY, NZ = grid
+    px, py, pz = procs
+    argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
+            "-da_processors_z", pz, "-ksp_rtol", "1e-10"]
+    x = np.zeros(3 * NX * NY * NZ)
+    on = run_group(argv, px * py * pz, newton_step(x, [("halo_overlap", 1)]))
+    off = run_group(argv, px * py * pz, newton_step(x, [("halo_overlap", 0)]))
+    for a, b in zip(on, off):
+        assert a["its"] == b["its"] and np.array_equal(a["du"], b["du"])
