@@ -155,6 +155,8 @@ int mcx_plan(const mcx_opts* o, int rank, int nranks, mcx_info* info);
 int mcx_plan_halo(const mcx_opts* o, int rank, int nranks, int* nnbr, int* nbr_rank, int64_t* send_cnt,
                   int64_t* recv_cnt, int64_t* send_nat, int64_t* recv_nat, int64_t* nsend, int64_t* nrecv);
 
+/* comm_id: rank 0's mcx_comm_unique_id, required when nranks > 1; with nranks == 1 a non-NULL id
+   makes a one-rank RCCL communicator, so the reductions take the multi-rank (RCCL) path */
 int mcx_init(const mcx_opts* o, int rank, int nranks, const void* comm_id, void** ctx);
 /* In-process transport: `nranks` contexts on one device, each driven by its own host thread,
    exchanging halos / partial sums by device copies (multi-rank path without RCCL; every

@@ -255,9 +255,9 @@ class Macroc:
         self.opts = opts if opts is not None else parse_args(argv)
         self._ctx = C.c_void_p()
         cid = None
-        if nranks > 1 and group is None:
-            if comm_id is None or len(comm_id) != COMM_ID_BYTES:
-                raise MacrocError("nranks > 1 needs the 128-byte id from comm_unique_id() on every rank")
+        if nranks > 1 and group is None and (comm_id is None or len(comm_id) != COMM_ID_BYTES):
+            raise MacrocError("nranks > 1 needs the 128-byte id from comm_unique_id() on every rank")
+        if comm_id is not None and group is None:  # one rank + an id: a one-rank RCCL communicator
             cid = C.create_string_buffer(comm_id, COMM_ID_BYTES)
         if group is not None:
             _check(L.mcx_init_local(C.byref(self.opts), rank, group._g, C.byref(self._ctx)), "mcx_init_local")

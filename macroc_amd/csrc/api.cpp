@@ -863,7 +863,7 @@ int mcx_get_nonlinear_stats(void* ctx, int64_t* n_nonlinear, double* f_trial_max
 
 // all-reduce of a few host doubles through red_loc / red (collective; op 0 sum, 1 max)
 static int host_allreduce(Ctx& c, double* v, int n, int op) {
-  if (c.nranks <= 1) return 0;
+  if (c.nranks <= 1 && !c.comm) return 0;
   int rc;
   if ((rc = allreduce_prepare(c))) return rc;
   MCX_HIP(hipMemcpyAsync(c.red_loc, v, sizeof(double) * n, hipMemcpyHostToDevice, c.stream));

@@ -26,8 +26,10 @@ namespace mcx {
     }                                                                                           \
   } while (0)
 
+// One rank with an id given: an RCCL communicator of one, so the all-reduces take the multi-rank
+// path (k_reduce partial sums, ncclAllReduce, k_cg_logic) — the RCCL transport on one GPU.
 int comm_init(Ctx& c, const void* id) {
-  if (c.nranks <= 1 || c.lg) return 0;
+  if (c.lg || (c.nranks <= 1 && !id)) return 0;
   if (!id) {
     set_error("nranks > 1 needs a communicator id from mcx_comm_unique_id");
     return 21;
@@ -124,7 +126,7 @@ int halo_exchange(Ctx& c, double* xpad) {
 }
 
 static int allreduce_op(Ctx& c, const double* in, double* out, int count, int op) {
-  if (c.nranks <= 1) {
+  if (c.nranks <= 1 && !c.comm) {
     if (in != out) MCX_HIP(hipMemcpyAsync(out, in, sizeof(double) * count, hipMemcpyDeviceToDevice, c.stream));
     return 0;
   }

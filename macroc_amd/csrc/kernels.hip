@@ -2040,7 +2040,7 @@ void launch_force_layer(Ctx& c, int comp, int fa, int fixed, int a0, int na, int
 }
 
 static int reduce_and_logic(Ctx& c, int nvals, int nparts, int mode, bool gated) {
-  if (c.nranks == 1) {
+  if (c.nranks == 1 && !c.comm) {
     hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, c.stream, c.partials, nparts, nvals, c.red, mode, c.cg, c.hist,
                        gated ? 1 : 0);
     return 0;

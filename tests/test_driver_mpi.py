@@ -66,3 +66,20 @@ def test_single_rank_build_refuses_a_rank_grid(tmp_path):
     r = subprocess.run([exe, "-da_grid_x", "5", "-da_grid_y", "2", "-da_grid_z", "2", "-da_processors_x", "2"],
                        capture_output=True, text=True, timeout=60, cwd=tmp_path)
     assert r.returncode != 0 and "driver-mpi" in r.stderr
+
+
+@pytest.mark.gpu
+def test_mpi_driver_one_rank_on_gpu(tmp_path):
+    """The MPI build under `mpirun -np 1` on the GPU runs BASELINE config 1 (4x4x2, -ts 2) and
+    prints the same |RES| / KSP lines as the single-rank build, and the same info.dat."""
+    flags = ["-da_grid_x", "4", "-da_grid_y", "4", "-da_grid_z", "2", "-ts", "2"]
+    single = os.path.join(ROOT, "macroc_amd", "driver", "macroc_amd")
+    out = {}
+    for name, cmd in (("mpi", [MPIRUN, "-np", "1", EXE, *flags]), ("single", [single, *flags])):
+        d = tmp_path / name
+        d.mkdir()
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd=d)
+        assert r.returncode == 0, r.stderr
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith(("|RES|", "KSP", "Time Step", "Non-Linear"))]
+        out[name] = (lines, (d / "info.dat").read_text())
+    assert out["mpi"] == out["single"] and any(ln.startswith("KSP") for ln in out["mpi"][0])

@@ -198,3 +198,25 @@ def test_halo_overlap_bitwise(grid, procs):
     off = run_group(argv, px * py * pz, newton_step(x, [("halo_overlap", 0)]))
     for a, b in zip(on, off):
         assert a["its"] == b["its"] and np.array_equal(a["du"], b["du"])
+
+
+def test_rccl_transport_one_rank():
+    """The RCCL transport on one GPU: a one-rank communicator routes every reduction through
+    the multi-rank path (k_reduce partial sums, ncclAllReduce on the compute stream,
+    k_cg_logic) and the host all-reduces (force, non-linear counts) through ncclAllReduce;
+    the result must be bitwise what the single-rank path computes."""
+    argv = ["-da_grid_x", 16, "-da_grid_y", 12, "-da_grid_z", 10, "-ksp_rtol", "1e-10"]
+    outs = []
+    for cid in (None, M.comm_unique_id()):
+        with M.Macroc(argv, rank=0, nranks=1, comm_id=cid) as m:
+            m.apply_bc_on_u(m.get_displacement(1))
+            m.set_strains(); m.homogenize()
+            res = m.assembly_res()
+            m.assembly_jac()
+            its, rn, reason = m.solve_Ax()
+            m.update_u()
+            m.set_strains(); m.homogenize()
+            outs.append((res, its, reason, m.du(), m.calc_force(), m.reduce_nonlinear()))
+    (r0, i0, c0, d0, f0, n0), (r1, i1, c1, d1, f1, n1) = outs
+    assert (i0, c0, f0, n0) == (i1, c1, f1, n1) and np.array_equal(d0, d1)
+    assert abs(r0 - r1) <= 1e-15 * r0
