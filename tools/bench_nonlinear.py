@@ -21,10 +21,12 @@ ap.add_argument("--split", type=int, default=1, help="aij: -mat_aij_split (1: up
 ap.add_argument("--rtol", type=float, default=1e-8)
 ap.add_argument("--dt", type=float, default=0.01, help="load step (U = -ts*dt); 0.01 drives the circle plastic")
 ap.add_argument("--maxq", type=int, default=None, help="aij-split: split_maxq (correction quads per node allowed)")
+ap.add_argument("--micro-n", type=int, default=10, help="-micro_n (BASELINE config 5: 10; sizes MicroPP's micro-cell, "
+                "which the device law does not have: reported, no effect)")
 a = ap.parse_args()
 N = a.grid
 m = M.Macroc(["-da_grid_x", N, "-da_grid_y", N, "-da_grid_z", N, "-mat_law", "plastic", "-ksp_rtol", repr(a.rtol),
-              "-dm_mat_type", a.mat_type, "-mat_aij_split", a.split, "-ts", a.ts, "-dt", a.dt])
+              "-dm_mat_type", a.mat_type, "-mat_aij_split", a.split, "-ts", a.ts, "-dt", a.dt, "-micro_n", a.micro_n])
 m.set_timing(True)
 if a.maxq is not None:
     m.set_option("split_maxq", a.maxq)
@@ -35,13 +37,18 @@ for ts in range(a.ts):
     out = m.time_step(ts)
     dt = time.perf_counter() - t0
     nl, fmax = m.nonlinear_stats()
+    tm = m.timing()
     steps.append(dict(ts=ts, newton_its=out["newton_its"], ksp_its=out["ksp_its"], res=out["res"], seconds=dt,
-                      nonlinear_gps=nl, f_trial_max=fmax))
+                      nonlinear_gps=nl, f_trial_max=fmax,
+                      last_phases_ms={k: tm[k] for k in ("strains_ms", "homogenize_ms", "residual_ms", "jacobian_ms",
+                                                         "solve_ms")}))
     print(json.dumps(steps[-1]), file=sys.stderr, flush=True)
 tot = time.perf_counter() - t_all
 nits = sum(s["newton_its"] for s in steps)
 info = m.get_info()
 print(json.dumps({"workload": f"config 5 path: {N}^3 non-linear Newton (J2 callback), {a.ts} time steps, dt {a.dt}",
+                  "micro_n": a.micro_n, "micro_n_note": "no micro-scale FE problem behind the device law (MicroPP out of scope)",
+                  "device_gb": m.get_info()["device_bytes"] / 1e9,
                   "mat_type": a.mat_type, "storage": {0: "aij-blocks", 1: "sbaij", 2: "aij-split"}[info["storage"]],
                   "split_slots": info["split_slots"], "split_bits": info["split_bits"], "newton_its": nits, "cg_its": sum(sum(s["ksp_its"]) for s in steps),
                   "seconds": tot, "ms_per_newton_iter": tot / max(nits, 1) * 1e3,

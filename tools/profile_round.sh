@@ -3,7 +3,7 @@
 # the default bench, the same command under rocprofv3 --kernel-trace --stats, and the PMC HBM
 # traffic passes of the headline SpMV (tools/pmc_spmv.sh).  Everything lands in gpurun_out/.
 set -euo pipefail
-TAG=${1:-r01}
+TAG=${1:-r02}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 timeout -k 10 420 python3 bench.py > gpurun_out/${TAG}_bench_default.json 2> gpurun_out/${TAG}_bench_default.log
