@@ -54,7 +54,7 @@ static int free_ctx(Ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
-  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->V, c->U, c->D, c->d_mask, c->eps, c->sig, c->ctan,
+  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->V, c->U, c->D, c->d_mask, c->eps, c->sig, c->ctan, c->Ke,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf, c->halo.d_bnd};
   for (void* p : ptrs)
@@ -146,7 +146,9 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
       (rc = dalloc(c, &c.hist, (int64_t)o->ksp_max_it + 2)))
     return rc;
   // per-GP tangent: only laws that hand one over (the isotropic elastic C is a kernel argument)
-  if (o->mat_law != MCX_LAW_ELASTIC && (rc = dalloc(c, &c.ctan, 36 * 8 * E))) return rc;
+  if (o->mat_law != MCX_LAW_ELASTIC &&
+      ((rc = dalloc(c, &c.ctan, 36 * 8 * E)) || (rc = dalloc(c, &c.Ke, (int64_t)576 * E))))
+    return rc;
   if (o->mat_law == MCX_LAW_PLASTIC &&
       ((rc = dalloc(c, &c.hist_old, 7 * 8 * E)) || (rc = dalloc(c, &c.hist_new, 7 * 8 * E)) ||
        (rc = dalloc(c, &c.ftrial, 8 * E))))
@@ -748,17 +750,20 @@ int mcx_assembly_jac(void* ctx) {
   CTX(ctx);
   PhaseTimer t(c, PH_JAC);
   int rc;
+  if (c.mat.law != MCX_LAW_ELASTIC) launch_element_ke(c);  // per-GP tangent: element matrices first
   if (c.o.mat_type == MCX_MAT_SBAIJ) {
     launch_gather_matrix_sym(c);
     c.fmt = FMT_U;
-  } else if (c.aij_split) {
+  } else if (c.aij_split && !c.split_declined) {
     launch_gather_matrix_sym(c);
     bool exact = false;
     if ((rc = build_split(c, &exact))) return rc;
     c.fmt = exact ? FMT_SPLIT : FMT_V;
-    if (!exact) {  // a correction is not exact in bf16 / f32: plain AIJ blocks
+    if (!exact) {  // a correction is not exact, or they are too many: plain AIJ blocks
       if ((rc = ensure_V(c))) return rc;
       launch_gather_matrix(c);
+      // a per-GP-tangent law keeps its dense corrections: later assemblies go straight to blocks
+      c.split_declined = c.mat.law != MCX_LAW_ELASTIC;
     }
   } else {
     if ((rc = ensure_V(c))) return rc;
@@ -1244,6 +1249,7 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     return 0;
   }
   if (!std::strcmp(name, "split_maxq")) {  // takes effect at the next mcx_assembly_jac
+    c.split_declined = false;
     c.split_maxq = std::max(0, std::min(30, (int)value));
     return 0;
   }
@@ -1282,6 +1288,7 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     return 0;
   }
   if (!std::strcmp(name, "aij_split")) {  // takes effect at the next mcx_assembly_jac
+    c.split_declined = false;
     if (value != 0. && (!c.U || !c.d_mask)) {
       set_error("aij_split: context created with -mat_aij_split 0 (no split storage)");
       return 2;

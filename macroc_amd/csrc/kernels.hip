@@ -428,19 +428,15 @@ __global__ __launch_bounds__(TPB) void k_residual(Geo g, const double* __restric
 }
 
 // ---------------------------------------------------------------------------- Jacobian
-// Element-matrix block Ke[3a+r][3bn+c] (r, c = 0..2) of element le, evaluated on the fly:
-// assembly_jac's 4-nest (src/assembly.c:94-99) restricted to the block, Ke[i][j] +=
-// B[k][i]*C[k][l]*B[l][j]*wg with gp, k, l ascending, as ((B*C)*B)*wg.  Zero B terms and, for the
-// isotropic elastic law (TABLE = false: C from the kernel argument, no per-GP tangent array),
-// C's structural zeros are skipped: each skipped term is +-0 added to a sum that is never -0,
-// so the block is bit-identical to the full loop.  TABLE = true: C_tan per GP from ctan
-// [36][8][nelem] (micropp_C_get_ctan3, src/assembly.c:92).  a, bn are wave-uniform.
-template <bool TABLE>
-__device__ __forceinline__ void ke_block(const Geo& g, const Material& mat, const double* __restrict__ ctan,
-                                         int64_t le, int a, int bn, double (&ke)[9]) {
+// Element-matrix block Ke[3a+r][3bn+c] (r, c = 0..2) of element le, evaluated on the fly for the
+// isotropic elastic law (C from the kernel argument, no per-GP tangent array): assembly_jac's
+// 4-nest (src/assembly.c:94-99) restricted to the block, Ke[i][j] += B[k][i]*C[k][l]*B[l][j]*wg
+// with gp, k, l ascending, as ((B*C)*B)*wg.  Zero B terms and C's structural zeros are skipped:
+// each skipped term is +-0 added to a sum that is never -0, so the block is bit-identical to the
+// full loop.  a, bn are wave-uniform.
+__device__ __forceinline__ void ke_block(const Geo& g, const Material& mat, int a, int bn, double (&ke)[9]) {
 #pragma unroll
   for (int q = 0; q < 9; q++) ke[q] = 0.;
-  const int64_t E = g.nelem, NG = 8 * E;
   const double wg = g.wg;
   for (int gp = 0; gp < 8; gp++) {
     double Ba[3][3], Bb[3][3];
@@ -455,8 +451,8 @@ __device__ __forceinline__ void ke_block(const Geo& g, const Material& mat, cons
     for (int k = 0; k < 6; k++)
 #pragma unroll
       for (int l = 0; l < 6; l++) {
-        if (!TABLE && !((k < 3 && l < 3) || k == l)) continue;
-        const double Ckl = TABLE ? ctan[(k * 6 + l) * NG + gp * E + le] : mat.C[k * 6 + l];
+        if (!((k < 3 && l < 3) || k == l)) continue;
+        const double Ckl = mat.C[k * 6 + l];
 #pragma unroll
         for (int r = 0; r < 3; r++) {
           if (!kin(r, k)) continue;
@@ -471,13 +467,76 @@ __device__ __forceinline__ void ke_block(const Geo& g, const Material& mat, cons
   }
 }
 
+// Laws with a per-GP tangent (plastic, external): the element matrices are formed once into
+// Ke[576][elements] (each C_tan read once per element and thread group, not once per matrix
+// block) and the blocks are summed from there.  Same 4-nest and term order as ke_block, all
+// 36 C entries.  One thread = (element, node a, half of the column nodes b): 4 column blocks x
+// 9 = 36 accumulators.  Grid: blocks b -> (XCD group, a, half, element group) so the 16 blocks
+// that read one element group's ctan share an XCD's L2.
+template <int BH>
+__device__ __forceinline__ void ke_body(const Geo& g, int64_t le, int a, const double* __restrict__ ctan,
+                                        double* __restrict__ Ke) {
+  const int64_t E = g.nelem, NG = 8 * E;
+  double acc[4][9];
+#pragma unroll
+  for (int bb = 0; bb < 4; bb++)
+#pragma unroll
+    for (int q = 0; q < 9; q++) acc[bb][q] = 0.;
+  const double wg = g.wg;
+  for (int gp = 0; gp < 8; gp++) {
+    double Ba[3][3];
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+      for (int q = 0; q < 3; q++) Ba[r][q] = cB[gp][krow(r, q)][3 * a + r];
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+#pragma unroll
+      for (int l = 0; l < 6; l++) {
+        const double Ckl = ctan[(k * 6 + l) * NG + gp * E + le];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+          if (!kin(r, k)) continue;
+          const double t0 = Ba[r][kpos(r, k)] * Ckl;
+#pragma unroll
+          for (int c = 0; c < 3; c++) {
+            if (!kin(c, l)) continue;
+#pragma unroll
+            for (int bb = 0; bb < 4; bb++) acc[bb][r * 3 + c] += t0 * cB[gp][l][3 * (BH * 4 + bb) + c] * wg;
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int bb = 0; bb < 4; bb++)
+#pragma unroll
+    for (int q = 0; q < 9; q++) Ke[((int64_t)(a * 8 + BH * 4 + bb) * 9 + q) * E + le] = acc[bb][q];
+}
+
+__global__ __launch_bounds__(TPB) void k_element_ke(Geo g, const double* __restrict__ ctan, double* __restrict__ Ke,
+                                                    int64_t ngroups) {
+  // block -> (xcd, a, half, element group): blocks sharing an element group are 8 apart
+  const int64_t b = blockIdx.x;
+  const int x = (int)(b & 7);
+  const int64_t t = b >> 3;
+  const int ah = (int)(t & 15);
+  const int64_t grp = (t >> 4) * 8 + x;
+  if (grp >= ngroups) return;
+  const int64_t le = grp * TPB + threadIdx.x;
+  if (le >= g.nelem) return;
+  const int a = ah >> 1;
+  if (ah & 1) ke_body<1>(g, le, a, ctan, Ke);
+  else ke_body<0>(g, le, a, ctan, Ke);
+}
+
 // One 3x3 block A(node g, node g+d) of the assembled matrix (MatSetValuesLocal(ADD) +
 // MatAssembly + MatZeroRowsColumns(diag = 1), src/assembly.c:106-112, src/bcs.c:341-347):
 // 0 + Ke_e1 + Ke_e2 + ... over the shared elements in ascending element order (the reference's
-// insertion order on one rank), each element block computed on the fly (no element-matrix
-// array), then the Dirichlet rows / columns.
+// insertion order on one rank), each element block computed on the fly (elastic) or read from
+// the element matrices Ke (TABLE: laws with a per-GP tangent), then the Dirichlet rows / columns.
 template <bool TABLE>
-__device__ __forceinline__ void matrix_block(const Geo& g, const Material& mat, const double* __restrict__ ctan,
+__device__ __forceinline__ void matrix_block(const Geo& g, const Material& mat, const double* __restrict__ Ke,
                                              int gi, int gj, int gk, int dx, int dy, int dz, double (&val)[9]) {
   const int hi = gi + dx, hj = gj + dy, hk = gk + dz;
 #pragma unroll
@@ -494,10 +553,17 @@ __device__ __forceinline__ void matrix_block(const Geo& g, const Material& mat, 
         const int px = ox + dx, ex = gi - ox;
         if (px < 0 || px > 1 || ex < 0 || ex > g.NX - 2) continue;
         const int64_t le = (ex - g.ex0) + (int64_t)(ey - g.ey0) * g.nex + (int64_t)(ez - g.ez0) * g.nex * g.ney;
-        double ke[9];
-        ke_block<TABLE>(g, mat, ctan, le, q1_local(ox, oy, oz), q1_local(px, py, pz), ke);
+        const int a = q1_local(ox, oy, oz), bn = q1_local(px, py, pz);
+        if constexpr (TABLE) {  // element matrices formed by k_element_ke
+          const double* src = Ke + (int64_t)((a * 8 + bn) * 9) * g.nelem + le;
 #pragma unroll
-        for (int q = 0; q < 9; q++) val[q] += ke[q];
+          for (int q = 0; q < 9; q++) val[q] += src[(int64_t)q * g.nelem];
+        } else {
+          double ke[9];
+          ke_block(g, mat, a, bn, ke);
+#pragma unroll
+          for (int q = 0; q < 9; q++) val[q] += ke[q];
+        }
       }
     }
   }
@@ -514,7 +580,7 @@ __device__ __forceinline__ void matrix_block(const Geo& g, const Material& mat, 
 
 // AIJ stencil blocks: thread = (owned node, neighbour block nb)
 template <bool TABLE>
-__global__ __launch_bounds__(TPB) void k_gather_matrix(Geo g, Material mat, const double* __restrict__ ctan,
+__global__ __launch_bounds__(TPB) void k_gather_matrix(Geo g, Material mat, const double* __restrict__ Ke,
                                                        double* __restrict__ V) {
   const int n = blockIdx.x * TPB + threadIdx.x;
   const int nb = blockIdx.y;
@@ -522,7 +588,7 @@ __global__ __launch_bounds__(TPB) void k_gather_matrix(Geo g, Material mat, cons
   int i, j, k;
   node_ijk(g, n, i, j, k);
   double val[9];
-  matrix_block<TABLE>(g, mat, ctan, g.xs + i, g.ys + j, g.zs + k, nb % 3 - 1, (nb / 3) % 3 - 1, nb / 9 - 1, val);
+  matrix_block<TABLE>(g, mat, Ke, g.xs + i, g.ys + j, g.zs + k, nb % 3 - 1, (nb / 3) % 3 - 1, nb / 9 - 1, val);
   double* Vg = V + (int64_t)(n >> 6) * (NPAIR * 128) + 2 * (n & 63);
 #pragma unroll
   for (int q = 0; q < 9; q++) {
@@ -538,7 +604,7 @@ __global__ __launch_bounds__(TPB) void k_gather_matrix(Geo g, Material mat, cons
 // ghost and an owned node touches the owned node).  Thread = (padded node, t): t = 0 the
 // diagonal block, t = 1..13 upper block nb = 13 + t.
 template <bool TABLE>
-__global__ __launch_bounds__(TPB) void k_gather_matrix_sym(Geo g, Material mat, const double* __restrict__ ctan,
+__global__ __launch_bounds__(TPB) void k_gather_matrix_sym(Geo g, Material mat, const double* __restrict__ Ke,
                                                            double* __restrict__ U, int npad) {
   const int p = blockIdx.x * TPB + threadIdx.x;
   const int t = blockIdx.y;
@@ -551,7 +617,7 @@ __global__ __launch_bounds__(TPB) void k_gather_matrix_sym(Geo g, Material mat, 
   const bool nbr_owned = qi >= 1 && qi <= g.nx && qj >= 1 && qj <= g.ny && qk >= 1 && qk <= g.nz;
   double val[9];
   if (owned || (t > 0 && nbr_owned)) {
-    matrix_block<TABLE>(g, mat, ctan, g.xs + pi - 1, g.ys + pj - 1, g.zs + pk - 1, dx, dy, dz, val);
+    matrix_block<TABLE>(g, mat, Ke, g.xs + pi - 1, g.ys + pj - 1, g.zs + pk - 1, dx, dy, dz, val);
   } else {
 #pragma unroll
     for (int q = 0; q < 9; q++) val[q] = 0.;
@@ -576,7 +642,7 @@ __global__ __launch_bounds__(TPB) void k_gather_matrix_sym(Geo g, Material mat, 
 // (matrix_block, exactly what k_gather_matrix stores) minus the mirrored upper value
 // U(m, 26-nb)[c][r] of the neighbour m = n + off(nb), as f32 bits (bit q = r*3+c in *valid).
 template <bool TABLE>
-__device__ __forceinline__ void split_block(const Geo& g, const Material& mat, const double* __restrict__ ctan,
+__device__ __forceinline__ void split_block(const Geo& g, const Material& mat, const double* __restrict__ Ke,
                                             const double* __restrict__ U, int n, int nb, unsigned (&f32)[9],
                                             unsigned& bits, unsigned& bad) {
   int i, j, k;
@@ -584,14 +650,14 @@ __device__ __forceinline__ void split_block(const Geo& g, const Material& mat, c
   bits = bad = 0;
   double low[9], mir[9];
   if (nb == 13) {
-    matrix_block<TABLE>(g, mat, ctan, g.xs + i, g.ys + j, g.zs + k, 0, 0, 0, low);
+    matrix_block<TABLE>(g, mat, Ke, g.xs + i, g.ys + j, g.zs + k, 0, 0, 0, low);
 #pragma unroll
     for (int r = 0; r < 3; r++)
 #pragma unroll
       for (int c = 0; c < 3; c++) mir[r * 3 + c] = r > c ? low[c * 3 + r] : low[r * 3 + c];
   } else {
     const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
-    matrix_block<TABLE>(g, mat, ctan, g.xs + i, g.ys + j, g.zs + k, dx, dy, dz, low);
+    matrix_block<TABLE>(g, mat, Ke, g.xs + i, g.ys + j, g.zs + k, dx, dy, dz, low);
     const int um = u_of(g, i + dx, j + dy, k + dz);
     const double* Um = U + (int64_t)(um >> 6) * (UPAIR * 128) + 2 * (um & 63);
     const int base = 6 + 9 * (12 - nb);  // the neighbour's upper block 26 - nb
@@ -620,7 +686,7 @@ __device__ __forceinline__ void split_block(const Geo& g, const Material& mat, c
 // the correction slots that are non-zero anywhere, d_mask[14] bit 0 = some correction inexact
 // in bf16, bit 1 = inexact in f32 (then the matrix is stored as plain AIJ blocks).
 template <bool TABLE>
-__global__ __launch_bounds__(TPB) void k_split_mask(Geo g, Material mat, const double* __restrict__ ctan,
+__global__ __launch_bounds__(TPB) void k_split_mask(Geo g, Material mat, const double* __restrict__ Ke,
                                                     const double* __restrict__ U, unsigned* __restrict__ mask) {
   __shared__ unsigned s_bits, s_bad;
   if (threadIdx.x == 0) s_bits = s_bad = 0;
@@ -629,7 +695,7 @@ __global__ __launch_bounds__(TPB) void k_split_mask(Geo g, Material mat, const d
   const int nb = blockIdx.y;
   if (n < g.nown) {
     unsigned f32[9], bits, bad;
-    split_block<TABLE>(g, mat, ctan, U, n, nb, f32, bits, bad);
+    split_block<TABLE>(g, mat, Ke, U, n, nb, f32, bits, bad);
     if (bits) atomicOr(&s_bits, bits);
     if (bad) atomicOr(&s_bad, bad);
   }
@@ -644,14 +710,14 @@ __global__ __launch_bounds__(TPB) void k_split_mask(Geo g, Material mat, const d
 // positions (slot p of node u = u_of: D[(((u/64) * Lq + p/8) * 64 + u%64) * 8 + p%8] as bf16,
 // or 4 f32 per quad); D is zeroed first (ghost nodes and padding hold zeros).
 template <bool TABLE>
-__global__ __launch_bounds__(TPB) void k_split_pack(Geo g, Material mat, const double* __restrict__ ctan,
+__global__ __launch_bounds__(TPB) void k_split_pack(Geo g, Material mat, const double* __restrict__ Ke,
                                                     const double* __restrict__ U, uint16_t* __restrict__ D, DSlots dl) {
   const int n = blockIdx.x * TPB + threadIdx.x;
   const int nb = blockIdx.y;
   const unsigned m9 = dl.m9[nb];
   if (n >= g.nown || !m9) return;
   unsigned f32[9], bits, bad;
-  split_block<TABLE>(g, mat, ctan, U, n, nb, f32, bits, bad);
+  split_block<TABLE>(g, mat, Ke, U, n, nb, f32, bits, bad);
   int i, j, k;
   node_ijk(g, n, i, j, k);
   const int64_t u = u_of(g, i, j, k);
@@ -1840,22 +1906,29 @@ void launch_residual(Ctx& c) {
 // every law but the isotropic elastic one hands over a per-GP tangent (ctan)
 static bool table_law(const Ctx& c) { return c.mat.law != MCX_LAW_ELASTIC; }
 
+// element matrices of a per-GP-tangent law (k_element_ke), read by the gathers below
+void launch_element_ke(Ctx& c) {
+  const int64_t ngroups = nblk(c.g.nelem);
+  const int64_t blocks = pad8(ngroups) * 16;
+  hipLaunchKernelGGL(k_element_ke, dim3((unsigned)blocks), dim3(TPB), 0, c.stream, c.g, c.ctan, c.Ke, ngroups);
+}
+
 void launch_gather_matrix(Ctx& c) {
   if (table_law(c))
-    hipLaunchKernelGGL(k_gather_matrix<true>, dim3(nblk(c.g.nown), 27), dim3(TPB), 0, c.stream, c.g, c.mat, c.ctan,
+    hipLaunchKernelGGL(k_gather_matrix<true>, dim3(nblk(c.g.nown), 27), dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke,
                        c.V);
   else
-    hipLaunchKernelGGL(k_gather_matrix<false>, dim3(nblk(c.g.nown), 27), dim3(TPB), 0, c.stream, c.g, c.mat, c.ctan,
+    hipLaunchKernelGGL(k_gather_matrix<false>, dim3(nblk(c.g.nown), 27), dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke,
                        c.V);
 }
 
 void launch_gather_matrix_sym(Ctx& c) {
   const int npad = c.g.PX * c.g.PY * c.g.PZ;
   if (table_law(c))
-    hipLaunchKernelGGL(k_gather_matrix_sym<true>, dim3(nblk(npad), 14), dim3(TPB), 0, c.stream, c.g, c.mat, c.ctan,
+    hipLaunchKernelGGL(k_gather_matrix_sym<true>, dim3(nblk(npad), 14), dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke,
                        c.U, npad);
   else
-    hipLaunchKernelGGL(k_gather_matrix_sym<false>, dim3(nblk(npad), 14), dim3(TPB), 0, c.stream, c.g, c.mat, c.ctan,
+    hipLaunchKernelGGL(k_gather_matrix_sym<false>, dim3(nblk(npad), 14), dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke,
                        c.U, npad);
 }
 
@@ -1866,9 +1939,9 @@ int build_split(Ctx& c, bool* exact) {
   MCX_HIP(hipMemsetAsync(c.d_mask, 0, 16 * sizeof(unsigned), c.stream));
   const dim3 grid(nblk(c.g.nown), 14);
   if (table_law(c))
-    hipLaunchKernelGGL(k_split_mask<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.ctan, c.U, c.d_mask);
+    hipLaunchKernelGGL(k_split_mask<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.U, c.d_mask);
   else
-    hipLaunchKernelGGL(k_split_mask<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.ctan, c.U, c.d_mask);
+    hipLaunchKernelGGL(k_split_mask<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.U, c.d_mask);
   unsigned hm[16];
   MCX_HIP(hipMemcpyAsync(hm, c.d_mask, sizeof(hm), hipMemcpyDeviceToHost, c.stream));
   MCX_HIP(hipStreamSynchronize(c.stream));
@@ -1908,9 +1981,9 @@ int build_split(Ctx& c, bool* exact) {
   if (dl.L) {
     MCX_HIP(hipMemsetAsync(c.D, 0, (size_t)c.npgroups * dl.Lq * 64 * 16, c.stream));
     if (table_law(c))
-      hipLaunchKernelGGL(k_split_pack<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.ctan, c.U, c.D, dl);
+      hipLaunchKernelGGL(k_split_pack<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.U, c.D, dl);
     else
-      hipLaunchKernelGGL(k_split_pack<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.ctan, c.U, c.D, dl);
+      hipLaunchKernelGGL(k_split_pack<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.U, c.D, dl);
   }
   return 0;
 }

@@ -135,6 +135,7 @@ struct Ctx {
   bool assembled = false;    // a matrix has been assembled (mcx_assembly_jac)
   int aij_split = 1;         // aij: assemble in FMT_SPLIT when every correction is exact in bf16
   int split_maxq = 4;        // AIJ-split only while the corrections fit this many 16-B quads per node
+  bool split_declined = false;  // a per-GP-tangent law's corrections were dense: assemble AIJ blocks directly
   int split_dbg = 0;         // timing-only diagnostics of the split SpMV (option split_dbg)
   int split_wide = 0;        // force f32 corrections (testing the wide path)
   int split_tx = 0;          // AIJ-split tile width (0: by subdomain width, 4 rows; else 1024 / split_tx rows)
@@ -152,6 +153,7 @@ struct Ctx {
   double* eps = nullptr;     // [6][8][nelem]
   double* sig = nullptr;     // [6][8][nelem]
   double* ctan = nullptr;    // [36][8][nelem] per-GP tangent (plastic / external laws only)
+  double* Ke = nullptr;      // [576][nelem] element matrices (plastic / external laws only)
   double* hist_old = nullptr; // plastic law: [7][8][nelem] plastic strain (tensor comps) + alpha
   double* hist_new = nullptr;
   double* ftrial = nullptr;  // [8][nelem]
@@ -217,6 +219,7 @@ void launch_apply_bc_u(Ctx& c, double U);
 void launch_strains(Ctx& c);
 void launch_homogenize(Ctx& c);
 void launch_residual(Ctx& c);          // b + partial sums of b.b
+void launch_element_ke(Ctx& c);        // Ke of a per-GP-tangent law
 void launch_gather_matrix(Ctx& c);
 void launch_gather_matrix_sym(Ctx& c);
 int build_split(Ctx& c, bool* exact);  // AIJ-split corrections from U (exact = usable)
