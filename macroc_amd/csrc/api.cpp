@@ -142,10 +142,11 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
       (c.o.mat_type == MCX_MAT_AIJ && !c.aij_split && (rc = dalloc(c, &c.V, c.ngroups * NPAIR * 128))) ||
       (rc = dalloc(c, &c.eps, 6 * 8 * E)) || (rc = dalloc(c, &c.sig, 6 * 8 * E)) ||
       (rc = dalloc(c, &c.partials, c.partials_cap = 4 * std::max(max_spmv_blocks(c), node_blocks(c)) + 64)) ||
-      (rc = dalloc(c, &c.red, 16)) || (rc = dalloc(c, &c.red_loc, 16)) || (rc = dalloc(c, &c.cg, 1)) ||
+      (rc = dalloc(c, &c.red, 16)) || (rc = dalloc(c, &c.red_loc, 16)) || (rc = dalloc(c, &c.cg, 2)) ||
       (rc = dalloc(c, &c.hist, (int64_t)o->ksp_max_it + 2)))
     return rc;
   // per-GP tangent: only laws that hand one over (the isotropic elastic C is a kernel argument)
+  c.partials2 = c.partials + c.partials_cap / 2;
   if (o->mat_law != MCX_LAW_ELASTIC &&
       ((rc = dalloc(c, &c.ctan, 36 * 8 * E)) || (rc = dalloc(c, &c.Ke, (int64_t)576 * E))))
     return rc;
@@ -215,7 +216,7 @@ static int cg_solve(Ctx& c, int* its, double* rnorm, int* reason) {
         pair_it.push_back(issued);
         npairs++;
       }
-      if ((rc = cg_iteration(c, e0, e1))) return rc;
+      if ((rc = cg_iteration(c, e0, e1, q == 0, q == CH - 1))) return rc;
     }
     MCX_HIP(hipMemcpyAsync(&c.h_cg[slot], c.cg, sizeof(CgState), hipMemcpyDeviceToHost, c.stream));
     MCX_HIP(hipEventRecord(c.ev_chunk[slot], c.stream));
@@ -1268,6 +1269,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
       set_error("split_tx: partials buffer too small");
       return 2;
     }
+    return 0;
+  }
+  if (!std::strcmp(name, "cg_fuse")) {
+    c.fuse = value != 0.;
     return 0;
   }
   if (!std::strcmp(name, "halo_overlap")) {

@@ -1671,6 +1671,114 @@ __global__ __launch_bounds__(UTPB) void k_cg_update(Geo g, const double* __restr
   }
 }
 
+// ---- single rank: the CG scalar steps folded into the vector kernels (no k_reduce launch) ----
+// Two device CgState buffers alternate between kernels: the update reads B and writes A, the
+// fused p update reads A and writes B.  Every block reduces the partial sums it needs itself,
+// in one fixed order (so all blocks compute the same scalars), runs the PETSc CG step on a
+// private copy of the state, and block 0 stores it.  A finished solve's state is copied on
+// unchanged, so gated kernels keep seeing its reason.
+__device__ void cg_logic_alpha(CgState* s, double dpi);
+__device__ void cg_logic_beta(CgState* s, double zz, double zr, double* hist);
+
+// r += (-a) w; z = D^-1 r; partials z.z, z.r — with alpha from the SpMV's p.w partials
+// (k_reduce's RED_ALPHA step, same summation tree for npw <= UTPB)
+template <bool NT>
+__global__ __launch_bounds__(UTPB) void k_cg_update_fa(Geo g, const double* __restrict__ w,
+                                                      const double* __restrict__ dinv, double* __restrict__ r,
+                                                      double* __restrict__ z, double* __restrict__ part, int nparts,
+                                                      const double* __restrict__ part_pw, int npw,
+                                                      const CgState* __restrict__ cg_in, CgState* __restrict__ cg_out) {
+  __shared__ double sh[UTPB / 64];
+  __shared__ double s_alpha;
+  __shared__ int s_reason;
+  double v = 0.;
+  for (int q = threadIdx.x; q < npw; q += UTPB) v += part_pw[q];
+  const double pw = block_sum<UTPB>(v, sh);
+  if (threadIdx.x == 0) {
+    CgState st = *cg_in;
+    cg_logic_alpha(&st, pw);
+    if (blockIdx.x == 0) *cg_out = st;
+    s_alpha = st.alpha;
+    s_reason = st.reason;
+  }
+  __syncthreads();
+  if (s_reason) return;
+  const double ma = -s_alpha;
+  int n = blockIdx.x * UTPB + threadIdx.x;
+  double zz = 0., zr = 0.;
+  if (n < g.nown) {
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      const int q = 3 * n + d;
+      const double rv = r[q] + ma * w[q];
+      st<NT>(&r[q], rv);
+      const double zv = rv * dinv[q];
+      st<NT>(&z[q], zv);
+      zz += zv * zv;
+      zr += zv * rv;
+    }
+  }
+  double s0 = block_sum<UTPB>(zz, sh);
+  double s1 = block_sum<UTPB>(zr, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = s0;
+    part[nparts + blockIdx.x] = s1;
+  }
+}
+
+// the sum k_reduce forms over n <= 1024 values (block_sum<1024>: one value per thread, a
+// shuffle tree per 64-value group, the 16 group sums added in order), with 256 threads, so the
+// fused steps compute the same scalars bit for bit
+__device__ __forceinline__ double sum1024_by256(const double* __restrict__ v, int n, double* sh) {
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int gq = 0; gq < 4; gq++) {
+    const int q = (w * 4 + gq) * 64 + l;
+    const double x = wave_sum(q < n ? v[q] : 0.);
+    if (l == 0) sh[w * 4 + gq] = x;
+  }
+  __syncthreads();
+  double r = 0.;
+  if (threadIdx.x == 0)
+    for (int q = 0; q < 16; q++) r += sh[q];
+  __syncthreads();
+  return r;
+}
+
+// p update with beta from the update's z.z / z.r partials (k_reduce's RED_BETA step)
+template <bool NT>
+__global__ __launch_bounds__(TPB) void k_cg_pupdate_fb(Geo g, const double* __restrict__ z,
+                                                      double* __restrict__ ppad, double* __restrict__ x,
+                                                      const double* __restrict__ part, int nparts,
+                                                      const CgState* __restrict__ cg_in, CgState* __restrict__ cg_out,
+                                                      double* __restrict__ hist) {
+  __shared__ double sh[16];
+  __shared__ CgState s_st;
+  const double zz = sum1024_by256(part, nparts, sh);
+  const double zr = sum1024_by256(part + nparts, nparts, sh);
+  if (threadIdx.x == 0) {
+    CgState st = *cg_in;
+    cg_logic_beta(&st, zz, zr, blockIdx.x == 0 ? hist : nullptr);
+    if (blockIdx.x == 0) *cg_out = st;
+    s_st = st;
+  }
+  __syncthreads();
+  if (s_st.reason) return;
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  const int pc = pad_of(g, i, j, k);
+  const double bc = s_st.bcoef, a = s_st.alpha;
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    const int q = 3 * n + d;
+    const double pv = ppad[3 * pc + d];
+    st<NT>(&x[q], x[q] + a * pv);
+    st<NT>(&ppad[3 * pc + d], z[q] + bc * pv);
+  }
+}
+
 // CG scalar steps (thread 0 of the reduction block)
 __device__ void cg_logic_init(CgState* s, double zz, double zr, double* hist) {
   const double dp = sqrt(zz);
@@ -1709,7 +1817,7 @@ __device__ void cg_logic_beta(CgState* s, double zz, double zr, double* hist) {
   if (s->reason) return;
   const double dp = sqrt(zz);
   s->dp = dp;
-  if (s->hist_on) hist[s->i + 1] = dp;
+  if (s->hist_on && hist) hist[s->i + 1] = dp;
   int rs = converged_default(s, dp);
   if (rs) {
     s->reason = rs;
@@ -1737,11 +1845,13 @@ enum { RED_STORE = 0, RED_INIT = 1, RED_ALPHA = 2, RED_BETA = 3, RED_NORM = 4 };
 
 // one block: out[v] = sum_i part[v*nparts + i] (fixed order); then optional CG logic.
 // mode RED_STORE writes the local sums only (an all-reduce + k_cg_logic follows).
+// cg_src: the state the step starts from (copied to cg first when it is the other buffer)
 __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ part, int nparts, int nvals,
                                                  double* __restrict__ out, int mode, CgState* cg,
-                                                 double* __restrict__ hist, int gated) {
+                                                 double* __restrict__ hist, int gated, const CgState* cg_src) {
   __shared__ double sh[16];
-  if (gated && cg->reason) return;
+  if (cg_src != cg && threadIdx.x == 0) *cg = *cg_src;  // read by thread 0 only below
+  if (gated && cg_src->reason) return;
   double res[2] = {0., 0.};
   for (int v = 0; v < nvals; v++) {
     // 8 independent accumulators per thread keep 8 loads in flight; fixed combination order
@@ -2112,16 +2222,19 @@ void launch_force_layer(Ctx& c, int comp, int fa, int fixed, int a0, int na, int
                      a0, na, b0, nb, out);
 }
 
-static int reduce_and_logic(Ctx& c, int nvals, int nparts, int mode, bool gated) {
+// part: the partial sums (c.partials, or c.partials2 for the update's); single rank: the step
+// runs on c.cg starting from *src (c.cg, or the fused path's other buffer c.cg + 1)
+static int reduce_and_logic(Ctx& c, int nvals, int nparts, int mode, bool gated, const double* part,
+                            const CgState* src) {
   if (c.nranks == 1 && !c.comm) {
-    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, c.stream, c.partials, nparts, nvals, c.red, mode, c.cg, c.hist,
-                       gated ? 1 : 0);
+    hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, c.stream, part, nparts, nvals, c.red, mode, c.cg, c.hist,
+                       gated ? 1 : 0, src);
     return 0;
   }
   int rc0 = allreduce_prepare(c);
   if (rc0) return rc0;
-  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, c.stream, c.partials, nparts, nvals, c.red_loc, (int)RED_STORE,
-                     c.cg, c.hist, gated ? 1 : 0);
+  hipLaunchKernelGGL(k_reduce, dim3(1), dim3(1024), 0, c.stream, part, nparts, nvals, c.red_loc, (int)RED_STORE,
+                     c.cg, c.hist, gated ? 1 : 0, c.cg);
   int rc = allreduce_sum(c, c.red_loc, c.red, nvals);
   if (rc) return rc;
   hipLaunchKernelGGL(k_cg_logic, dim3(1), dim3(64), 0, c.stream, c.red, mode, c.cg, c.hist, c.red);
@@ -2130,7 +2243,7 @@ static int reduce_and_logic(Ctx& c, int nvals, int nparts, int mode, bool gated)
 
 void launch_reduce(Ctx& c, int nvals, int nparts, double* out) {
   (void)out;
-  reduce_and_logic(c, nvals, nparts, RED_NORM, false);
+  reduce_and_logic(c, nvals, nparts, RED_NORM, false, c.partials, c.cg);
 }
 
 void launch_cg_init(Ctx& c) {
@@ -2140,7 +2253,7 @@ void launch_cg_init(Ctx& c) {
 
 int cg_finish_init(Ctx& c) {
   int nb = (int)nblk(c.g.nown);
-  return reduce_and_logic(c, 2, nb, RED_INIT, false);
+  return reduce_and_logic(c, 2, nb, RED_INIT, false, c.partials, c.cg);
 }
 
 void launch_cg_xfinal(Ctx& c) {
@@ -2171,11 +2284,26 @@ void launch_cg_pupdate(Ctx& c, int part) {
   }
 }
 
-int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1) {
+// Fused scalar steps (single rank, c.fuse): the alpha step runs in the update kernel, the beta
+// step in the next iteration's p update when the update's partials are few (<= 1024 per value;
+// else k_reduce), and a chunk's last beta step in k_reduce so the host poll and the next chunk
+// read c.cg.  first: the chunk's first iteration (its p update starts from c.cg).
+static bool fused(const Ctx& c) { return c.fuse && c.nranks == 1 && !c.comm; }
+
+int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) {
   const int nbs = (int)spmv_grid_blocks(c);
   const int nbu = (int)((c.g.nown + UTPB - 1) / UTPB);
+  CgState* A = c.cg + 1;  // fused path: the state after the alpha step
+  const bool fa = fused(c), fb = fa && nbu <= 1024;
   int rc;
-  if (c.nranks > 1 && c.overlap && c.halo.nbnd) {
+  if (fb && !first) {
+    if (c.cg_nt)
+      hipLaunchKernelGGL(k_cg_pupdate_fb<true>, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du,
+                         c.partials2, nbu, A, c.cg, c.hist);
+    else
+      hipLaunchKernelGGL(k_cg_pupdate_fb<false>, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad,
+                         c.du, c.partials2, nbu, A, c.cg, c.hist);
+  } else if (c.nranks > 1 && c.overlap && c.halo.nbnd) {
     // the sent nodes' p first, then their exchange overlaps the interior p update
     launch_cg_pupdate(c, 1);
     if ((rc = halo_start(c, c.p_pad))) return rc;
@@ -2183,21 +2311,30 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1) {
     if ((rc = halo_finish(c, c.p_pad))) return rc;
   } else {
     launch_cg_pupdate(c, 0);
-    if ((rc = halo_exchange(c, c.p_pad))) return rc;
   }
+  if (!(c.nranks > 1 && c.overlap && c.halo.nbnd) && (rc = halo_exchange(c, c.p_pad))) return rc;
   if (ev0) MCX_HIP(hipEventRecord(ev0, c.stream));
   launch_spmv(c, c.p_pad, c.w, true, true);
   if (ev1) MCX_HIP(hipEventRecord(ev1, c.stream));
-  rc = reduce_and_logic(c, 1, nbs, RED_ALPHA, true);
+  if (fa) {
+    if (c.cg_nt)
+      hipLaunchKernelGGL(k_cg_update_fa<true>, dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, c.dinv, c.r, c.z,
+                         c.partials2, nbu, c.partials, nbs, c.cg, A);
+    else
+      hipLaunchKernelGGL(k_cg_update_fa<false>, dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, c.dinv, c.r, c.z,
+                         c.partials2, nbu, c.partials, nbs, c.cg, A);
+    if (!fb || last) return reduce_and_logic(c, 2, nbu, RED_BETA, true, c.partials2, A);
+    return 0;
+  }
+  rc = reduce_and_logic(c, 1, nbs, RED_ALPHA, true, c.partials, c.cg);
   if (rc) return rc;
   if (c.cg_nt)
     hipLaunchKernelGGL(k_cg_update<true>, dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, c.dinv, c.r, c.z,
-                     c.partials, nbu, c.cg);
+                       c.partials2, nbu, c.cg);
   else
     hipLaunchKernelGGL(k_cg_update<false>, dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, c.dinv, c.r, c.z,
-                     c.partials, nbu, c.cg);
-  rc = reduce_and_logic(c, 2, nbu, RED_BETA, true);
-  return rc;
+                       c.partials2, nbu, c.cg);
+  return reduce_and_logic(c, 2, nbu, RED_BETA, true, c.partials2, c.cg);
 }
 
 }  // namespace mcx

@@ -158,9 +158,11 @@ struct Ctx {
   double* hist_new = nullptr;
   double* ftrial = nullptr;  // [8][nelem]
   double* partials = nullptr;
+  double* partials2 = nullptr;  // second half of partials: the CG update's z.z / z.r partial sums
+  int fuse = 1;              // single rank: CG scalar steps folded into the vector kernels (option cg_fuse)
   double* red = nullptr;     // reduction results (device)
   double* red_loc = nullptr; // local sums before all-reduce
-  CgState* cg = nullptr;
+  CgState* cg = nullptr;     // [2]: cg[0] the state the host polls; cg[1] the fused path's post-alpha state
   double* hist = nullptr;
   double* tmp = nullptr;     // owned-vector scratch for host copies
   CgState* h_cg = nullptr;   // pinned mirror
@@ -230,7 +232,7 @@ void launch_cg_xfinal(Ctx& c);
 void launch_cg_pupdate(Ctx& c, int part);  // 0 all owned nodes, 1 the sent (subdomain-face) nodes, 2 the rest
 void launch_reduce(Ctx& c, int nvals, int nparts, double* out);
 void launch_cg_init(Ctx& c);
-int cg_iteration(Ctx& c, hipEvent_t spmv_start, hipEvent_t spmv_stop);
+int cg_iteration(Ctx& c, hipEvent_t spmv_start, hipEvent_t spmv_stop, bool first, bool last);
 int cg_finish_init(Ctx& c);
 void launch_pack(Ctx& c, const double* xpad);
 void launch_unpack(Ctx& c, double* xpad);

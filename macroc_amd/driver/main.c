@@ -82,14 +82,20 @@ static int plan_only(const mcx_opts* o, int nranks) {
     int nnbr = 0, nbr[26];
     int64_t sc[26], rc[26], ns = 0, nr = 0;
     CHK(mcx_plan_halo(o, r, nranks, &nnbr, nbr, sc, rc, NULL, NULL, &ns, &nr));
-    printf("PLAN rank %d of %d grid %d %d %d corners %ld %ld %ld %ld %ld %ld dof_offset %ld ndofs %ld nnz %ld"
-           " nelem %ld halo %d",
-           r, nranks, in.px, in.py, in.pz, (long)in.xs, (long)in.ys, (long)in.zs, (long)in.nx, (long)in.ny,
-           (long)in.nz, (long)in.dof_offset, (long)in.ndofs_local, (long)in.nnz_local, (long)in.nelem_local, nnbr);
-    for (int q = 0; q < nnbr; q++) printf(" %d:%ld:%ld", nbr[q], (long)sc[q], (long)rc[q]);
-    printf("\n");
+    /* one write per line (ranks share stdout; a pipe write of < 4 KiB is not interleaved) */
+    char line[2048];
+    int len = snprintf(line, sizeof(line),
+                       "PLAN rank %d of %d grid %d %d %d corners %ld %ld %ld %ld %ld %ld dof_offset %ld ndofs %ld nnz %ld"
+                       " nelem %ld halo %d",
+                       r, nranks, in.px, in.py, in.pz, (long)in.xs, (long)in.ys, (long)in.zs, (long)in.nx, (long)in.ny,
+                       (long)in.nz, (long)in.dof_offset, (long)in.ndofs_local, (long)in.nnz_local, (long)in.nelem_local,
+                       nnbr);
+    for (int q = 0; q < nnbr; q++)
+      len += snprintf(line + len, sizeof(line) - len, " %d:%ld:%ld", nbr[q], (long)sc[q], (long)rc[q]);
+    snprintf(line + len, sizeof(line) - len, "\n");
+    fputs(line, stdout);
+    fflush(stdout);
   }
-  fflush(stdout);
   return 0;
 }
 
