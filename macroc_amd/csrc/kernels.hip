@@ -2284,17 +2284,20 @@ void launch_cg_pupdate(Ctx& c, int part) {
   }
 }
 
-// Fused scalar steps (single rank, c.fuse): the alpha step runs in the update kernel, the beta
-// step in the next iteration's p update when the update's partials are few (<= 1024 per value;
-// else k_reduce), and a chunk's last beta step in k_reduce so the host poll and the next chunk
-// read c.cg.  first: the chunk's first iteration (its p update starts from c.cg).
+// Fused scalar steps (single rank, c.fuse, small grids: <= 1024 update blocks): the alpha step
+// runs in the update kernel, the beta step in the next iteration's p update, and a chunk's last
+// beta step in k_reduce so the host poll and the next chunk read c.cg.  first: the chunk's first
+// iteration (its p update starts from c.cg).
 static bool fused(const Ctx& c) { return c.fuse && c.nranks == 1 && !c.comm; }
 
 int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) {
   const int nbs = (int)spmv_grid_blocks(c);
   const int nbu = (int)((c.g.nown + UTPB - 1) / UTPB);
   CgState* A = c.cg + 1;  // fused path: the state after the alpha step
-  const bool fa = fused(c), fb = fa && nbu <= 1024;
+  // both folds or none: at 256^3 (16,384 update blocks) the alpha prologue of every block costs
+  // more than the k_reduce launch it saves (4.177 vs 4.159 ms per CG iteration); at 64^3 the two
+  // folds save 1.6 % (profiles/r02_cg_ab_fuse{64,256}.log)
+  const bool fa = fused(c) && nbu <= 1024, fb = fa;
   int rc;
   if (fb && !first) {
     if (c.cg_nt)
