@@ -1970,7 +1970,13 @@ int64_t node_blocks(const Ctx& c) { return nblk(c.g.nown); }
 // AIJ-split SpMV tile: the phased z-marching kernel, 128x4 where the subdomain is wide enough
 static void split_shape(const Ctx& c, int& ztx, int& zty) {
   ztx = c.split_tx ? c.split_tx : (c.g.nx >= 256 ? 256 : (c.g.nx >= 128 ? 128 : 64));
-  zty = c.split_ty ? c.split_ty : 4;  // tiles 256x4 (1 block / CU), 128x4 (2), 64x4 (4); 256x2, 128x8, 64x16, 32x32
+  // tiles 256x4 (1 block / CU), 128x4 (2), 64x4 (4); 256x2, 128x8, 64x16.  Defaults by subdomain
+  // width: 256x4, 128x8 (128^3: 0.478 vs 0.496 ms for 128x4), 64x4 (64^3: 0.0716 ms, best of
+  // six shapes / chunkings), profiles/r02_ab_{64,128}.log
+  zty = c.split_ty ? c.split_ty : (ztx == 128 && !c.split_tx ? 8 : 4);
+  const bool built = (ztx == 256 && (zty == 2 || zty == 4)) || (ztx == 128 && (zty == 4 || zty == 8)) ||
+                     (ztx == 64 && (zty == 4 || zty == 16));
+  if (!built) zty = 4;  // the launcher instantiates only these shapes
 }
 
 int64_t spmv_grid_blocks(const Ctx& c) {
