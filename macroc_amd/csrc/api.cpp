@@ -765,7 +765,8 @@ int mcx_assembly_jac(void* ctx) {
     if (!exact) {  // a correction is not exact, or they are too many: plain AIJ blocks
       if ((rc = ensure_V(c))) return rc;
       launch_gather_matrix(c);
-      // a per-GP-tangent law keeps its dense corrections: later assemblies go straight to blocks
+      // a per-GP-tangent law keeps its inexact (or refused dense) corrections: later assemblies
+      // go straight to blocks
       c.split_declined = c.mat.law != MCX_LAW_ELASTIC;
     }
   } else {
@@ -1254,6 +1255,11 @@ int mcx_set_option(void* ctx, const char* name, double value) {
   if (!std::strcmp(name, "split_maxq")) {  // takes effect at the next mcx_assembly_jac
     c.split_declined = false;
     c.split_maxq = std::max(0, std::min(30, (int)value));
+    return 0;
+  }
+  if (!std::strcmp(name, "split_dense")) {  // takes effect at the next mcx_assembly_jac
+    c.split_declined = false;
+    c.split_dense = value != 0.;
     return 0;
   }
   if (!std::strcmp(name, "split_dbg")) {

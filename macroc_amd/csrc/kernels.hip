@@ -1473,6 +1473,67 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
   }
 }
 
+// AIJ-split with dense corrections (dl.dense): y += D x for every owned node, all 120 slots in
+// canonical order — per row, lower block nb ascending then column c, then the diagonal block's
+// strictly-lower entries — added to the z-march's (lower + upper) sum; with DOT the p.w partials
+// of the finished y.  One thread per owned node: 15 (bf16) or 30 (f32) coalesced 16-B quads, the
+// 13 source nodes' x (3 doubles each) gathered once per block.  No barriers, full occupancy.
+template <bool DOT, bool GATED, bool WIDE>
+__global__ __launch_bounds__(TPB) void k_split_dense(Geo g, const uint16_t* __restrict__ Dq, int Lq,
+                                                     const double* __restrict__ x, double* __restrict__ y,
+                                                     double* __restrict__ part, const CgState* __restrict__ cg) {
+  __shared__ double sh[TPB / 64];
+  if (GATED && cg->reason) return;
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  double dot = 0.;
+  if (n < g.nown) {
+    int i, j, k;
+    node_ijk(g, n, i, j, k);
+    const int pc = pad_of(g, i, j, k);
+    const int64_t u = u_of(g, i, j, k);
+    const u32x4* Dn = reinterpret_cast<const u32x4*>(Dq) + (u >> 6) * Lq * 64 + (u & 63);
+    const int PX = g.PX, PXY = g.PX * g.PY;
+    // all quads of the node issued up front (15 bf16 quads; the f32 form loads per use)
+    constexpr int NQ = WIDE ? 1 : 15;
+    u32x4 wq[NQ];
+#pragma unroll
+    for (int t = 0; t < NQ; t++) wq[t] = WIDE ? u32x4{0u, 0u, 0u, 0u} : __builtin_nontemporal_load(Dn + t * 64);
+    auto corr = [&](int p) -> double {
+      if (WIDE) {
+        const u32x4 w = __builtin_nontemporal_load(Dn + (p / 4) * 64);
+        return (double)__uint_as_float(w[p & 3]);
+      }
+      const unsigned hw = wq[p >> 3][(p & 7) >> 1];
+      return (double)__uint_as_float((p & 1) ? (hw & 0xffff0000u) : (hw << 16));
+    };
+    double d0 = 0., d1 = 0., d2 = 0.;
+#pragma unroll
+    for (int nb = 0; nb < 13; nb++) {
+      const int q = pc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
+      const double xm[3] = {x[3 * (int64_t)q], x[3 * (int64_t)q + 1], x[3 * (int64_t)q + 2]};
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        d0 += corr(nb * 9 + c) * xm[c];
+        d1 += corr(nb * 9 + 3 + c) * xm[c];
+        d2 += corr(nb * 9 + 6 + c) * xm[c];
+      }
+    }
+    const double x0 = x[3 * (int64_t)pc], x1 = x[3 * (int64_t)pc + 1];
+    d1 += corr(117) * x0;  // (1,0)
+    d2 += corr(118) * x0;  // (2,0)
+    d2 += corr(119) * x1;  // (2,1)
+    const double y0 = y[3 * (int64_t)n] + d0, y1 = y[3 * (int64_t)n + 1] + d1, y2 = y[3 * (int64_t)n + 2] + d2;
+    y[3 * (int64_t)n] = y0;
+    y[3 * (int64_t)n + 1] = y1;
+    y[3 * (int64_t)n + 2] = y2;
+    if (DOT) dot = x0 * y0 + x1 * y1 + x[3 * (int64_t)pc + 2] * y2;
+  }
+  if (DOT) {
+    const double s = block_sum<TPB>(dot, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+  }
+}
+
 static void z_shape(int kern, int& ztx, int& zty) {
   switch (kern) {
     case 2: ztx = 32; zty = 4; break;
@@ -1493,6 +1554,37 @@ template <int ZTX, int ZTY, bool AIJS = false>
 static void launch_symp(Ctx& c, const double* xpad, double* y, bool dot, bool gated, const ZTiling& zt, int nb) {
   const uint16_t* Dq = c.D;
   DSlots dl = c.dsl;
+  if (AIJS && dl.dense) {  // the z-march without corrections, then the dense pass (with the dot)
+    DSlots none = dl;
+    none.L = 0;
+    none.Lq = 0;
+    if (gated)
+      hipLaunchKernelGGL((k_spmv_symp<false, true, ZTX, ZTY, AIJS>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g, c.U,
+                         xpad, y, c.partials, c.cg, zt, Dq, none);
+    else
+      hipLaunchKernelGGL((k_spmv_symp<false, false, ZTX, ZTY, AIJS>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g,
+                         c.U, xpad, y, c.partials, c.cg, zt, Dq, none);
+    const dim3 gd((unsigned)((c.g.nown + TPB - 1) / TPB));
+    if (dot && gated && dl.wide)
+      hipLaunchKernelGGL((k_split_dense<true, true, true>), gd, dim3(TPB), 0, c.stream, c.g, Dq, dl.Lq, xpad, y,
+                         c.partials, c.cg);
+    else if (dot && gated)
+      hipLaunchKernelGGL((k_split_dense<true, true, false>), gd, dim3(TPB), 0, c.stream, c.g, Dq, dl.Lq, xpad, y,
+                         c.partials, c.cg);
+    else if (dot && dl.wide)
+      hipLaunchKernelGGL((k_split_dense<true, false, true>), gd, dim3(TPB), 0, c.stream, c.g, Dq, dl.Lq, xpad, y,
+                         c.partials, c.cg);
+    else if (dot)
+      hipLaunchKernelGGL((k_split_dense<true, false, false>), gd, dim3(TPB), 0, c.stream, c.g, Dq, dl.Lq, xpad, y,
+                         c.partials, c.cg);
+    else if (dl.wide)
+      hipLaunchKernelGGL((k_split_dense<false, false, true>), gd, dim3(TPB), 0, c.stream, c.g, Dq, dl.Lq, xpad, y,
+                         c.partials, c.cg);
+    else
+      hipLaunchKernelGGL((k_split_dense<false, false, false>), gd, dim3(TPB), 0, c.stream, c.g, Dq, dl.Lq, xpad, y,
+                         c.partials, c.cg);
+    return;
+  }
   if (c.split_dbg) {  // timing-only diagnostics (wrong products): 1 = loads, no corrections; 2 = neither
     dl.L = 0;
     if (c.split_dbg == 2) dl.Lq = 0;
@@ -1991,6 +2083,11 @@ int64_t spmv_grid_blocks(const Ctx& c) {
   if (c.spmv_subl < 0) return (int64_t)c.g.nz * t.jgroups * t.nxc;
   return 8 * (int64_t)t.per_xcd;
 }
+int64_t spmv_nparts(const Ctx& c) {
+  if (c.fmt == FMT_SPLIT && c.dsl.dense) return node_blocks(c);
+  return spmv_grid_blocks(c);
+}
+
 int upload_constants(Ctx& c) {
   double B[8][6][24];
   compute_B_table(B);
@@ -2077,9 +2174,23 @@ int build_split(Ctx& c, bool* exact) {
     const int off = (nb % 3 - 1) + ((nb / 3) % 3 - 1) * c.g.PX + (nb / 9 - 1) * c.g.PX * c.g.PY;
     dl.xc[p] = (3 * off + rc % 3) * 4 + rc / 3;
   }
-  if (dl.Lq > c.split_maxq) {  // dense corrections: the AIJ blocks stream is faster
-    *exact = false;
-    return 0;
+  if (dl.Lq > c.split_maxq) {
+    // many corrections: the in-kernel walk would take one round trip per slot.  Either store all
+    // 120 slots in canonical order and add them in a second streaming pass (k_split_dense), or
+    // use the AIJ blocks
+    if (!c.split_dense) {
+      *exact = false;
+      return 0;
+    }
+    dl.dense = 1;
+    dl.L = 0;
+    for (int b = 0; b < 14; b++) {
+      dl.m9[b] = b < 13 ? 511 : (unsigned short)((1u << 3) | (1u << 6) | (1u << 7));
+      dl.pos[b] = (unsigned char)dl.L;
+      for (int q = 0; q < 9; q++)
+        if (dl.m9[b] >> q & 1) dl.s[dl.L++] = (unsigned char)(b * 9 + q);
+    }
+    dl.Lq = dl.wide ? (dl.L + 3) / 4 : (dl.L + 7) / 8;
   }
   const int64_t need = std::max<int64_t>(1, c.npgroups * dl.Lq) * 64 * 16;  // bytes of [u/64][Lq][64] x 16 B
   if (need > c.D_bytes) {
@@ -2297,7 +2408,7 @@ void launch_cg_pupdate(Ctx& c, int part) {
 static bool fused(const Ctx& c) { return c.fuse && c.nranks == 1 && !c.comm; }
 
 int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) {
-  const int nbs = (int)spmv_grid_blocks(c);
+  const int nbs = (int)spmv_nparts(c);
   const int nbu = (int)((c.g.nown + UTPB - 1) / UTPB);
   CgState* A = c.cg + 1;  // fused path: the state after the alpha step
   // both folds or none: at 256^3 (16,384 update blocks) the alpha prologue of every block costs

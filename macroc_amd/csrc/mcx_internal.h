@@ -82,6 +82,8 @@ struct DSlots {
   unsigned short m9[14];    // per lower block nb (13: diagonal): active (r*3+c) bits
   unsigned char pos[14];    // per block: index of its first active slot
   int xc[24];               // slot p < 24: (x offset from 3 * padded index of the row node) * 4 + row
+  int dense = 0;            // 1: all 120 slots stored in canonical order (nb*9 + r*3 + c, then the diagonal's
+                            // (1,0) (2,0) (2,1)) and applied by a second pass, k_split_dense
 };
 
 // In-process transport: several contexts (one host thread each) exchanging halos and partial
@@ -135,7 +137,8 @@ struct Ctx {
   bool assembled = false;    // a matrix has been assembled (mcx_assembly_jac)
   int aij_split = 1;         // aij: assemble in FMT_SPLIT when every correction is exact in bf16
   int split_maxq = 4;        // AIJ-split only while the corrections fit this many 16-B quads per node
-  bool split_declined = false;  // a per-GP-tangent law's corrections were dense: assemble AIJ blocks directly
+  int split_dense = 1;       // corrections beyond split_maxq quads: 1 = all 120 slots + a second pass, 0 = AIJ blocks
+  bool split_declined = false;  // a correction was not exact (or dense ones are refused): assemble AIJ blocks directly
   int split_dbg = 0;         // timing-only diagnostics of the split SpMV (option split_dbg)
   int split_wide = 0;        // force f32 corrections (testing the wide path)
   int split_tx = 0;          // AIJ-split tile width (0: by subdomain width, 4 rows; else 1024 / split_tx rows)
@@ -239,6 +242,7 @@ void launch_unpack(Ctx& c, double* xpad);
 void launch_copy_owned_to_pad(Ctx& c, const double* owned, double* pad);
 void launch_copy_pad_to_owned(Ctx& c, const double* pad, double* owned);
 int64_t spmv_grid_blocks(const Ctx& c);
+int64_t spmv_nparts(const Ctx& c);   // partial sums the CG's SpMV leaves (its own grid, or the dense pass's)
 int64_t node_blocks(const Ctx& c);
 int dirichlet_mask_host(const Geo& g, int gi, int gj, int gk);
 

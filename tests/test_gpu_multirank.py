@@ -147,7 +147,7 @@ def _multirank(name, sbaij, extra=(), split=False):
         assert not du.any()
 
 
-@pytest.mark.parametrize("mat", ["aij", "aij-tall", "sbaij", "sbaij-phased"])
+@pytest.mark.parametrize("mat", ["aij", "aij-tall", "aij-dense", "sbaij", "sbaij-phased"])
 @pytest.mark.parametrize("grid,procs", [((140, 10, 8), (2, 1, 1)), ((132, 12, 12), (2, 2, 2))])
 def test_multirank_full_tiles(grid, procs, mat):
     """Subdomains wide enough for full z-marching tiles (64 x 4) next to partial ones: internal
@@ -161,7 +161,9 @@ def test_multirank_full_tiles(grid, procs, mat):
     argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
             "-da_processors_z", pz, "-ksp_rtol", repr(rtol), "-dm_mat_type", mat.split("-")[0]]
     # 8: phased 64x4; aij-tall: 64x16 AIJ-split tiles (internal x faces at every tile's lanes 0 / 63)
-    opts = {"aij": [("split_maxq", 30)], "aij-tall": [("split_maxq", 30), ("split_tx", 64), ("split_ty", 16)], "sbaij": [],
+    # aij-dense: split_maxq 0 sends every correction to the dense second pass (k_split_dense)
+    opts = {"aij": [("split_maxq", 30)], "aij-tall": [("split_maxq", 30), ("split_tx", 64), ("split_ty", 16)],
+            "aij-dense": [("split_maxq", 0)], "sbaij": [],
             "sbaij-phased": [("spmv_kernel", 8)]}[mat]
     ref = O.Problem(NX, NY, NZ, rtol=rtol)
     ref.apply_bc_u(ref.get_displacement(0))

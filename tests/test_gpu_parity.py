@@ -121,11 +121,14 @@ def test_aij_split_single_rank(name):
             assert np.linalg.norm(m.du() - ref) <= du_tol(rtol) * np.linalg.norm(ref)
 
 
-@pytest.mark.parametrize("maxq,wide,storage", [(4, 0, 0), (30, 0, 2), (30, 1, 2)])
-def test_aij_split_dense_plastic(maxq, wide, storage):
-    """A plastic tangent fills all 117 correction slots: by default (at most 4 quads per node)
-    the AIJ blocks are used; allowed more quads, the split storage holds them in bf16 or f32
-    (forced) — the matrix is bit-exact either way, the SpMV within rounding."""
+@pytest.mark.parametrize("maxq,wide,dense,storage", [(4, 0, 0, 0), (4, 0, 1, 2), (4, 1, 1, 2), (30, 0, 1, 2),
+                                                     (30, 1, 1, 2)])
+def test_aij_split_dense_plastic(maxq, wide, dense, storage):
+    """A plastic tangent fills all 117 correction slots.  Beyond split_maxq quads per node the
+    split storage keeps all 120 slots in canonical order and adds them in a second pass
+    (split_dense 1, the default) or the AIJ blocks are used (split_dense 0); within maxq the
+    z-march walks them; bf16 or f32 (forced) — the matrix is bit-exact either way, the SpMV
+    within rounding."""
     NX, NY, NZ, dt = 12, 10, 12, 0.05
     P = O.Problem(NX, NY, NZ, rtol=1e-10, law=1, dt=dt, bc_type=0)
     P.apply_bc_u(P.get_displacement(1))
@@ -137,6 +140,7 @@ def test_aij_split_dense_plastic(maxq, wide, storage):
     with M.Macroc(argv) as m:
         m.set_option("split_maxq", maxq)
         m.set_option("split_wide", wide)
+        m.set_option("split_dense", dense)
         m.apply_bc_on_u(m.get_displacement(1))
         m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac(); m.solve_Ax(); m.update_u()
         m.set_u(u)
