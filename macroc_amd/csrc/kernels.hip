@@ -1493,16 +1493,13 @@ __global__ __launch_bounds__(TPB) void k_split_dense(Geo g, const uint16_t* __re
     const int64_t u = u_of(g, i, j, k);
     const u32x4* Dn = reinterpret_cast<const u32x4*>(Dq) + (u >> 6) * Lq * 64 + (u & 63);
     const int PX = g.PX, PXY = g.PX * g.PY;
-    // all quads of the node issued up front (15 bf16 quads; the f32 form loads per use)
-    constexpr int NQ = WIDE ? 1 : 15;
+    // all quads of the node issued up front (15 bf16 or 30 f32 quads)
+    constexpr int NQ = WIDE ? 30 : 15;
     u32x4 wq[NQ];
 #pragma unroll
-    for (int t = 0; t < NQ; t++) wq[t] = WIDE ? u32x4{0u, 0u, 0u, 0u} : __builtin_nontemporal_load(Dn + t * 64);
+    for (int t = 0; t < NQ; t++) wq[t] = __builtin_nontemporal_load(Dn + t * 64);
     auto corr = [&](int p) -> double {
-      if (WIDE) {
-        const u32x4 w = __builtin_nontemporal_load(Dn + (p / 4) * 64);
-        return (double)__uint_as_float(w[p & 3]);
-      }
+      if (WIDE) return (double)__uint_as_float(wq[p >> 2][p & 3]);
       const unsigned hw = wq[p >> 3][(p & 7) >> 1];
       return (double)__uint_as_float((p & 1) ? (hw & 0xffff0000u) : (hw << 16));
     };
