@@ -115,9 +115,9 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   c.g.ncu = c.ncu;
   c.aij_split = o->mat_type == MCX_MAT_AIJ && o->mat_aij_split;
   if (o->mat_type == MCX_MAT_SBAIJ) {
-    // phased z-march 256x4 / 128x4 (128^3: 0.436 vs 0.502 ms for symz 128x2,
-    // profiles/r02_ab_sbaij128.log), symz 64x4 below
-    c.spmv_kernel = c.g.nx >= 256 ? 11 : (c.g.nx >= 128 ? 7 : 1);
+    // phased z-march 256x4 / 128x4 / 64x4 (128^3: 0.436 vs 0.502 ms for symz 128x2; 64^3:
+    // 0.0555 vs 0.0625 ms for symz 64x4; profiles/r02_ab_sbaij{128,64}.log)
+    c.spmv_kernel = c.g.nx >= 256 ? 11 : (c.g.nx >= 128 ? 7 : 8);
     c.fmt = FMT_U;
   }
   MCX_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));

@@ -308,7 +308,7 @@ def test_sbaij_single_rank(NX, NY, NZ):
         # phased kernels: one canonical row order whatever the tile shape (LDS or pulled terms)
         for y in phased[1:]:
             assert np.array_equal(y, phased[0])
-        m.set_option("spmv_kernel", 7 if NX >= 128 else 1)  # the init-time default
+        m.set_option("spmv_kernel", 7 if NX >= 128 else 8)  # the init-time default
         its, rn, reason = m.solve_Ax()
         o_its = P.solve()["its"]
         assert abs(its - o_its) <= 1
