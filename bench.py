@@ -143,6 +143,20 @@ def cpu_baseline(N, threads, gpu_its, rtol, ndofs_target, nelem_target, nnz_targ
     }
 
 
+def room_for_warmup(t_step, steps, args, rank, world):
+    """True when one more warmup step, the timed steps and the tail (true-residual check, CPU
+    baseline) still fit the --wall budget of the invocation.  Decided by rank 0 and broadcast, so
+    every rank runs the same number of warmup steps.  At 256^3 per GPU one step takes ~12 s on one
+    GPU but ~25 s on 2-8 (the global grid doubles, and so do the CG iterations): there the driver's
+    `--steps 20 --warmup 5` would not fit 600 s with every warmup run; the first warmup always runs."""
+    ok = time.perf_counter() - T_START + (1 + steps) * t_step + args.tail <= args.wall
+    if world > 1:
+        t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+        dist.broadcast(t, src=0)
+        ok = bool(t[0])
+    return ok
+
+
 def measure(argv, rank, world, comm_id, args, steps, warmup):
     """Setup + warmup + timed steps of one configuration; returns the timings of this rank.
     Timing mode only records HIP events on the compute stream (no host waits): one event pair
@@ -175,6 +189,10 @@ def measure(argv, rank, world, comm_id, args, steps, warmup):
 
     t_warm = []
     for w in range(warmup):
+        if w >= 1 and not room_for_warmup(max(t_warm), steps, args, rank, world):
+            log(f"[rank {rank}] warmup: {warmup - w} of {warmup} skipped, {steps} timed steps would not fit "
+                f"--wall {args.wall:.0f}s")
+            break
         t = time.perf_counter()
         r = step()
         m.synchronize()
@@ -234,6 +252,11 @@ def main():
                     help="other storages measured after the headline line is printed (comma list, 1 warmup + "
                          "1 step each, reported on stderr, skipped once --budget is spent)")
     ap.add_argument("--budget", type=float, default=480.0, help="wall seconds the optional variants may use up to")
+    ap.add_argument("--wall", type=float, default=570.0,
+                    help="wall seconds the invocation must fit: warmup steps after the first are skipped when the "
+                         "timed steps would not fit (reported as warmup_run); the timed steps are never cut")
+    ap.add_argument("--tail", type=float, default=30.0, help="seconds reserved after the timed steps (check, CPU "
+                                                             "baseline)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -277,6 +300,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_run": len(r["warmup_s"]),
             "ms_per_step": ms_step,
             "higher_is_better": True,
             "scaling": "weak",

@@ -141,3 +141,37 @@ def test_gloo_world2_distributed_cg(grid, procs):
         x[rows] = xr
     duref = res[0][4]
     assert np.linalg.norm(x - duref) <= 1e-10 * np.linalg.norm(duref)
+
+
+def _warmup_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import types
+
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # rank 0's budget decides for every rank (rank 1's own budget would allow the warmup)
+        tight = types.SimpleNamespace(wall=1e-3 if rank == 0 else 1e9, tail=0.0)
+        loose = types.SimpleNamespace(wall=1e9, tail=0.0)
+        q.put((rank, bench.room_for_warmup(10.0, 20, tight, rank, world),
+               bench.room_for_warmup(10.0, 20, loose, rank, world)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_warmup_guard_is_collective():
+    """bench.py's --wall guard: whether another warmup step runs is rank 0's decision, broadcast,
+    so every rank runs the same number of warmup steps (the timed steps are never cut)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_warmup_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(2))
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res == [(0, False, True), (1, False, True)]
