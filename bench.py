@@ -10,9 +10,13 @@ the same state, nothing is cached across steps.  Workload: 256^3 nodes per GPU
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Rank 0 prints ONE JSON line (see the contract in the task statement / DESIGN.md §6) as soon as
-the headline and the CPU baseline are measured; `--variants aij-blocks,sbaij` then measures other
-storages (1 warmup + 1 step each, on stderr) while the `--budget` wall time lasts.
+The headline storage is the default AIJ one: value-indexed (one index byte per matrix value into
+a dictionary of the matrix's distinct values, rebuilt by every assembly inside the step; exact,
+rows in the CPU AIJ order).  On one GPU the AIJ-split storage of the same matrix is measured
+after it (1 warmup + 1 step, `variants` in the line; `--variants aij-split,aij-blocks,sbaij`
+for more) while the `--budget` wall time lasts.  Rank 0 prints ONE JSON line (the contract in
+the task statement / DESIGN.md §6) once the headline, the variants and the CPU baseline are
+measured.
 """
 import argparse
 import json
@@ -36,14 +40,17 @@ import macroc_amd as M  # noqa: E402
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
 # matrix storages: the reference's -dm_mat_type aij (DMSetMatType(da, MATAIJ), src/init.c:92) held
-# as upper blocks + exact bf16 lower corrections (default) or as plain AIJ blocks summed in the
-# CPU AIJ order; -dm_mat_type sbaij through DMSetFromOptions (src/init.c:93)
-STORAGE_ARGS = {"aij": ["-dm_mat_type", "aij"], "aij-blocks": ["-dm_mat_type", "aij", "-mat_aij_split", 0],
+# value-indexed (one index byte per value into the matrix's <= 256 distinct values; the default,
+# with fallback), as upper blocks + exact bf16 lower corrections (aij-split) or as plain AIJ blocks
+# summed in the CPU AIJ order; -dm_mat_type sbaij through DMSetFromOptions (src/init.c:93)
+STORAGE_ARGS = {"aij": ["-dm_mat_type", "aij"], "aij-split": ["-dm_mat_type", "aij", "-mat_aij_vi", 0],
+                "aij-blocks": ["-dm_mat_type", "aij", "-mat_aij_vi", 0, "-mat_aij_split", 0],
                 "sbaij": ["-dm_mat_type", "sbaij"]}
-STORAGE_NAME = {0: "aij-blocks", 1: "sbaij", 2: "aij-split"}
+STORAGE_NAME = {0: "aij-blocks", 1: "sbaij", 2: "aij-split", 3: "aij-vi"}
 KERNEL_NAME = {0: "k_spmv (AIJ stencil blocks, CPU AIJ row order)",
                1: "k_spmv_symp (SBAIJ phased z-marching tiles)",
-               2: "k_spmv_symp<AIJS> (AIJ-split: upper blocks + bf16 lower corrections, z-marching)"}
+               2: "k_spmv_symp<AIJS> (AIJ-split: upper blocks + bf16 lower corrections, z-marching)",
+               3: "k_spmv_vi (value-indexed AIJ: index bytes + dictionary in LDS, CPU AIJ row order)"}
 
 
 def log(*a):
@@ -232,6 +239,7 @@ def measure(argv, rank, world, comm_id, args, steps, warmup):
     return {"its": its, "tm": tm, "info": info, "check": check, "spmv_avg_ms": spmv_avg_ms, "spmv_bytes": spmv_bytes,
             "csr_bytes": csr_bytes, "storage": STORAGE_NAME[storage["storage"]], "storage_id": storage["storage"],
             "split_slots": storage["split_slots"], "split_bits": storage["split_bits"],
+            "vi_values": storage["vi_values"],
             "achieved": spmv_bytes / (spmv_avg_ms * 1e-3) / 1e9, "ms_step": dt / max(steps, 1) * 1e3,
             "warmup_s": t_warm}
 
@@ -248,9 +256,10 @@ def main():
     ap.add_argument("--cpu-cg-its", type=int, default=60, help="CG iterations of the oracle sample")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--mat-type", default="aij", choices=list(STORAGE_ARGS), help="matrix storage of the headline")
-    ap.add_argument("--variants", default="",
-                    help="other storages measured after the headline line is printed (comma list, 1 warmup + "
-                         "1 step each, reported on stderr, skipped once --budget is spent)")
+    ap.add_argument("--variants", default=None,
+                    help="other storages measured after the headline, 1 warmup + 1 step each, reported in the line's "
+                         "'variants' (comma list; default aij-split on one GPU, none on several; skipped once "
+                         "--budget would be exceeded)")
     ap.add_argument("--budget", type=float, default=480.0, help="wall seconds the optional variants may use up to")
     ap.add_argument("--wall", type=float, default=570.0,
                     help="wall seconds the invocation must fit: warmup steps after the first are skipped when the "
@@ -260,6 +269,8 @@ def main():
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.variants is None:
+        args.variants = "aij-split" if world == 1 and args.mat_type == "aij" else ""
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -283,6 +294,23 @@ def main():
     its, tm, info, check = r["its"], r["tm"], r["info"], r["check"]
     spmv_avg_ms, spmv_bytes, achieved, ms_step = r["spmv_avg_ms"], r["spmv_bytes"], r["achieved"], r["ms_step"]
     ndofs = 3 * NX * NY * NZ
+    # other storages of the same matrix, 1 warmup + 1 step each, while the budget lasts (reported
+    # in the line so the headline's storage can be compared with them)
+    variants = []
+    per_step = max(r["warmup_s"] or [ms_step * 1e-3])
+    for v in [v for v in args.variants.split(",") if v and v != args.mat_type]:
+        if time.perf_counter() - T_START + 2 * 3 * per_step + 60 > args.budget:
+            log(f"variant {v}: skipped (budget {args.budget:.0f}s)")
+            continue
+        vr = measure(argv + STORAGE_ARGS[v], rank, world, new_comm_id(), args, 1, 1)
+        variants.append({
+            "mat_type": v, "value": ndofs / (vr["ms_step"] * 1e-3), "ms_per_step": vr["ms_step"], "steps": 1,
+            "warmup": 1, "storage": vr["storage"], "kernel": KERNEL_NAME[vr["storage_id"]], "cg_its": vr["its"],
+            "ms_per_cg_iter": vr["tm"]["solve_ms"] / max(vr["its"], 1), "spmv_avg_ms": vr["spmv_avg_ms"],
+            "spmv_bytes_per_launch": vr["spmv_bytes"], "spmv_achieved_GBs": vr["achieved"],
+            "spmv_frac": vr["achieved"] / PEAK_HBM_GBS, "spmv_traffic": pmc_traffic(vr["storage"], NX, NY, NZ),
+            "phases_ms": {k: vr["tm"][k] for k in ("jacobian_ms", "solve_ms")}, "check": vr["check"]})
+        log("variant " + json.dumps(variants[-1]))
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_sample > 0:
@@ -311,7 +339,8 @@ def main():
                        "grid": [NX, NY, NZ], "grid_per_gpu": [G, G, G], "processors": [px, py, pz],
                        "dofs": ndofs, "nnz": info["nnz_global"], "parallelism": f"dmda{px}x{py}x{pz}",
                        "mat_type": "aij" if args.mat_type.startswith("aij") else "sbaij", "storage": r["storage"],
-                       "split_slots": r["split_slots"], "split_bits": r["split_bits"]},
+                       "split_slots": r["split_slots"], "split_bits": r["split_bits"],
+                       "vi_values": r["vi_values"]},
             "cg_its": its,
             "ms_per_cg_iter": tm["solve_ms"] / max(its, 1),
             # CG iterations grow ~linearly with the global grid edge (720 at 64^3, 2814 at 256^3),
@@ -329,22 +358,9 @@ def main():
                          "csr_frac": csr_achieved / PEAK_HBM_GBS},
             "cpu_baseline": cpu,
             "check": check,
+            "variants": variants,
         }
         print(json.dumps(line), flush=True)
-    # optional storages: after the line, 1 warmup + 1 step each, while the budget lasts
-    per_step = max(r["warmup_s"] or [ms_step * 1e-3])
-    for v in [v for v in args.variants.split(",") if v and v != args.mat_type]:
-        if time.perf_counter() - T_START + 3 * per_step > args.budget:
-            log(f"variant {v}: skipped (budget {args.budget:.0f}s)")
-            continue
-        vr = measure(argv + STORAGE_ARGS[v], rank, world, new_comm_id(), args, 1, 1)
-        if rank == 0:
-            log("variant " + json.dumps({
-                "mat_type": v, "value": ndofs / (vr["ms_step"] * 1e-3), "ms_per_step": vr["ms_step"],
-                "storage": vr["storage"], "kernel": KERNEL_NAME[vr["storage_id"]], "cg_its": vr["its"],
-                "ms_per_cg_iter": vr["tm"]["solve_ms"] / max(vr["its"], 1), "spmv_avg_ms": vr["spmv_avg_ms"],
-                "spmv_bytes_per_launch": vr["spmv_bytes"], "spmv_achieved_GBs": vr["achieved"],
-                "spmv_traffic": pmc_traffic(vr["storage"], NX, NY, NZ), "check": vr["check"]}))
     if world > 1:
         dist.destroy_process_group()
 

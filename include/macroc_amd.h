@@ -96,6 +96,10 @@ typedef struct {
   int mat_aij_split;           /* -mat_aij_split 0|1 (1): hold the AIJ matrix exactly as upper blocks +
                                   bf16 lower corrections when all are exact (else plain AIJ blocks);
                                   0: AIJ blocks, rows summed in the CPU AIJ order (bit-exact SpMV) */
+  int mat_aij_vi;              /* -mat_aij_vi 0|1 (1): hold the AIJ matrix exactly as one index byte per
+                                  value into a dictionary of its distinct values when there are at most
+                                  256 (value-indexed AIJ; rows summed in the CPU AIJ order, bit-exact
+                                  SpMV); otherwise -mat_aij_split decides */
 } mcx_opts;
 
 typedef struct {
@@ -115,7 +119,8 @@ typedef struct {
   int64_t device_bytes;         /* device memory held by the context */
   int device;
   int storage;                  /* matrix as last assembled: 0 AIJ blocks, 1 SBAIJ upper blocks,
-                                   2 AIJ-split (upper blocks + bf16 lower corrections) */
+                                   2 AIJ-split (upper blocks + bf16 lower corrections),
+                                   3 AIJ value-indexed (index bytes + dictionary) */
   int split_slots;              /* AIJ-split: correction slots stored per node (of 117) */
   int split_bits;               /* AIJ-split: bits per correction (16 = bf16, 32 = f32) */
   /* Gauss-point box of the constitutive callback: the elements this context evaluates, x
@@ -123,6 +128,7 @@ typedef struct {
      nex*ney*nez; Gauss point gpi = ie*8 + gp.  One rank: DMDAGetElements' own order.  Several
      ranks: the rank's PETSc elements plus the upper ghost layer (owner computes). */
   int64_t ex0, ey0, ez0, nex, ney, nez;
+  int vi_values;                /* value-indexed AIJ: dictionary entries (distinct matrix values) */
 } mcx_info;
 
 typedef struct {

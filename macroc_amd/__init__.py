@@ -57,6 +57,7 @@ class Opts(C.Structure):
         ("micro_mat_1", C.c_double * 4), ("micro_mat_2", C.c_double * 4),
         ("device", C.c_int), ("ksp_monitor", C.c_int), ("mat_type", C.c_int), ("mat_law", C.c_int),
         ("mat_aij_split", C.c_int),
+        ("mat_aij_vi", C.c_int),
     ]
 
 
@@ -73,6 +74,7 @@ class Info(C.Structure):
         ("split_bits", C.c_int),
         ("ex0", C.c_int64), ("ey0", C.c_int64), ("ez0", C.c_int64), ("nex", C.c_int64), ("ney", C.c_int64),
         ("nez", C.c_int64),
+        ("vi_values", C.c_int),
     ]
 
     def as_dict(self):

@@ -54,7 +54,7 @@ static int free_ctx(Ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
-  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->V, c->U, c->D, c->d_mask, c->eps, c->sig, c->ctan, c->Ke,
+  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->eps, c->sig, c->ctan, c->Ke,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf, c->halo.d_bnd};
   for (void* p : ptrs)
@@ -114,6 +114,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   c.ncu = std::max(ncu, 1);
   c.g.ncu = c.ncu;
   c.aij_split = o->mat_type == MCX_MAT_AIJ && o->mat_aij_split;
+  c.aij_vi = o->mat_type == MCX_MAT_AIJ && o->mat_aij_vi;
   if (o->mat_type == MCX_MAT_SBAIJ) {
     // phased z-march 256x4 / 128x4 / 64x4 (128^3: 0.436 vs 0.502 ms for symz 128x2; 64^3:
     // 0.0555 vs 0.0625 ms for symz 64x4; profiles/r02_ab_sbaij{128,64}.log)
@@ -307,6 +308,7 @@ void mcx_default_opts(mcx_opts* o) {
   std::memcpy(o->micro_mat_2, mat, sizeof(mat));
   o->device = -1;
   o->mat_aij_split = 1;
+  o->mat_aij_vi = 1;
 }
 
 int mcx_parse_args(mcx_opts* o, int argc, const char* const* argv) {
@@ -349,7 +351,7 @@ int mcx_parse_args(mcx_opts* o, int argc, const char* const* argv) {
         D("-ksp_rtol", &o->ksp_rtol) || D("-ksp_atol", &o->ksp_abstol) || D("-ksp_divtol", &o->ksp_dtol) ||
         I("-ksp_max_it", &o->ksp_max_it) || I("-micro_n", &o->micro_n) || I("-micro_type", &o->micro_type) ||
         A4("-micro_mat_1", o->micro_mat_1) || A4("-micro_mat_2", o->micro_mat_2) || I("-device", &o->device) ||
-        I("-mat_aij_split", &o->mat_aij_split))
+        I("-mat_aij_split", &o->mat_aij_split) || I("-mat_aij_vi", &o->mat_aij_vi))
       continue;
     if (!std::strcmp(k, "-dm_mat_type")) {
       if (!v || (std::strcmp(v, "aij") && std::strcmp(v, "sbaij"))) {
@@ -481,6 +483,7 @@ static void fill_info(const Ctx& c, mcx_info* in) {
   in->storage = c.fmt;
   in->split_slots = c.fmt == FMT_SPLIT ? c.dsl.L : 0;
   in->split_bits = c.fmt == FMT_SPLIT ? (c.dsl.wide ? 32 : 16) : 0;
+  in->vi_values = c.fmt == FMT_VI ? c.vi_n : 0;
   in->ex0 = g.ex0;
   in->ey0 = g.ey0;
   in->ez0 = g.ez0;
@@ -748,12 +751,38 @@ static int ensure_V(Ctx& c) {
   return dalloc(c, &c.V, c.ngroups * NPAIR * 128);
 }
 
+// the value-indexed storage, allocated on first use
+static int ensure_VI(Ctx& c) {
+  if (c.vi_idx) return 0;
+  const int64_t idx_bytes = c.ngroups * VI_CHUNKS * 64 * 16;
+  MCX_HIP(hipMalloc(&c.vi_idx, idx_bytes));
+  MCX_HIP(hipMalloc(&c.vi_dict, VI_MAX * sizeof(double)));
+  MCX_HIP(hipMalloc(&c.vi_keys, VI_HASH * sizeof(unsigned long long)));
+  MCX_HIP(hipMalloc(&c.vi_slot, VI_HASH));
+  MCX_HIP(hipMalloc(&c.vi_ctl, 2 * sizeof(unsigned)));
+  c.device_bytes += idx_bytes + VI_MAX * sizeof(double) + VI_HASH * 9 + 8;
+  return 0;
+}
+
 int mcx_assembly_jac(void* ctx) {
   GUARD(ctx);
   CTX(ctx);
   PhaseTimer t(c, PH_JAC);
   int rc;
   if (c.mat.law != MCX_LAW_ELASTIC) launch_element_ke(c);  // per-GP tangent: element matrices first
+  if (c.o.mat_type == MCX_MAT_AIJ && c.aij_vi && !c.vi_declined) {
+    // value-indexed AIJ when the matrix has at most VI_MAX distinct values (the elastic law's
+    // matrices); otherwise the next storage below
+    bool ok = false;
+    if ((rc = ensure_VI(c)) || (rc = build_vi(c, &ok))) return rc;
+    if (ok) {
+      c.fmt = FMT_VI;
+      c.assembled = true;
+      MCX_HIP(hipGetLastError());
+      return 0;
+    }
+    c.vi_declined = c.mat.law != MCX_LAW_ELASTIC;  // a per-GP tangent stays varied: skip the attempt
+  }
   if (c.o.mat_type == MCX_MAT_SBAIJ) {
     launch_gather_matrix_sym(c);
     c.fmt = FMT_U;
@@ -1074,10 +1103,18 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
     return 5;
   }
   const Geo& g = c.g;
-  const bool up = c.fmt != FMT_V;  // FMT_U / FMT_SPLIT: values from the upper blocks
+  const bool up = c.fmt == FMT_U || c.fmt == FMT_SPLIT;  // values from the upper blocks
   std::vector<double> V;
   std::vector<uint16_t> Dh;
-  if (vals) {
+  std::vector<unsigned char> Ih;
+  std::vector<double> dict;
+  if (vals && c.fmt == FMT_VI) {
+    Ih.resize((size_t)c.ngroups * VI_CHUNKS * 64 * 16);
+    dict.resize(VI_MAX);
+    MCX_HIP(hipMemcpyAsync(Ih.data(), c.vi_idx, Ih.size(), hipMemcpyDeviceToHost, c.stream));
+    MCX_HIP(hipMemcpyAsync(dict.data(), c.vi_dict, VI_MAX * sizeof(double), hipMemcpyDeviceToHost, c.stream));
+    MCX_HIP(hipStreamSynchronize(c.stream));
+  } else if (vals) {
     V.resize(up ? c.npgroups * UPAIR * 128 : c.ngroups * NPAIR * 128);
     MCX_HIP(hipMemcpyAsync(V.data(), up ? c.U : c.V, sizeof(double) * V.size(), hipMemcpyDeviceToHost, c.stream));
     if (c.fmt == FMT_SPLIT && c.dsl.L) {
@@ -1131,6 +1168,9 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
               if (c.fmt == FMT_SPLIT && r > cc) v = v + corr(pc, 13 * 9 + r * 3 + cc);  // lower triangle
             }
             else v = uval(pc, 6 + 9 * (nb - 14) + r * 3 + cc);
+          } else if (vals && c.fmt == FMT_VI) {
+            const int s = nb * 9 + r * 3 + cc;
+            v = dict[Ih[(((n >> 6) * VI_CHUNKS + (s >> 4)) * 64 + (n & 63)) * 16 + (s & 15)]];
           } else if (vals) {
             int s = nb * 9 + r * 3 + cc;
             v = V[(n >> 6) * (NPAIR * 128) + (int64_t)(s >> 1) * 128 + 2 * (n & 63) + (s & 1)];
@@ -1224,7 +1264,9 @@ int mcx_get_timing(void* ctx, mcx_timing* t) {
   *t = c.t;
   // algorithmic bytes of one SpMV in this format: the stencil-block values actually present
   // (AIJ nonzeros of the owned rows x 8 B), x read once, y written once
-  t->spmv_bytes_per_launch = (c.fmt == FMT_V ? c.nnz_local : c.nupper_local) * 8 + 2 * 3 * (int64_t)c.g.nown * 8;
+  // (value-indexed: one index byte per nonzero; the 13 pad bytes per node it also loads are not counted)
+  t->spmv_bytes_per_launch = (c.fmt == FMT_V ? c.nnz_local * 8 : (c.fmt == FMT_VI ? c.nnz_local : c.nupper_local * 8)) +
+                             2 * 3 * (int64_t)c.g.nown * 8;
   if (c.fmt == FMT_SPLIT) t->spmv_bytes_per_launch += (int64_t)c.g.nown * c.dsl.Lq * 16;
   return 0;
 }
@@ -1298,6 +1340,15 @@ int mcx_set_option(void* ctx, const char* name, double value) {
       set_error("split_ty: partials buffer too small");
       return 2;
     }
+    return 0;
+  }
+  if (!std::strcmp(name, "aij_vi")) {  // takes effect at the next mcx_assembly_jac
+    if (c.o.mat_type != MCX_MAT_AIJ) {
+      set_error("aij_vi: -dm_mat_type aij only");
+      return 2;
+    }
+    c.vi_declined = false;
+    c.aij_vi = value != 0.;
     return 0;
   }
   if (!std::strcmp(name, "aij_split")) {  // takes effect at the next mcx_assembly_jac

@@ -13,6 +13,7 @@
 // so element kinematics, strains, stresses, element matrices, the assembled matrix, the
 // residual and the SpMV are bit-identical to the CPU restatement on one rank.
 #include <algorithm>
+#include <cstring>
 #include <cmath>
 
 #include "mcx_internal.h"
@@ -1531,6 +1532,207 @@ __global__ __launch_bounds__(TPB) void k_split_dense(Geo g, const uint16_t* __re
   }
 }
 
+// ---------------------------------------------------------------------------- value-indexed AIJ
+// FMT_VI.  The assembled AIJ values of the elastic law take few distinct values (the stencil of
+// a uniform grid, its boundary variants and the Dirichlet 0 / 1 entries: 129 at 12^3, the same
+// set at any size), so the matrix is held exactly as one index byte per value into a dictionary
+// of them: 243 bytes per node instead of 1,944 (value-indexed CSR, Kourtis, Goumas & Koziris,
+// CF'08).  Built at every assembly in two passes over the on-the-fly blocks (matrix_block):
+// k_vi_collect gathers the distinct values (a per-block LDS set, then a global set); the host
+// sorts them into the dictionary; k_vi_pack writes the index bytes.  More than VI_MAX distinct
+// values (a per-GP tangent) = overflow: the context falls back to AIJ-split / AIJ blocks.
+constexpr unsigned long long VI_EMPTY = ~0ull;  // a NaN payload arithmetic does not produce
+
+__device__ __forceinline__ unsigned vi_hash(unsigned long long k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  return (unsigned)k;
+}
+
+// pass 1: thread = (owned node, block nb); ctl[0] = distinct values, ctl[1] = overflow
+template <bool TABLE>
+__global__ __launch_bounds__(TPB) void k_vi_collect(Geo g, Material mat, const double* __restrict__ Ke,
+                                                    unsigned long long* __restrict__ keys, unsigned* __restrict__ ctl) {
+  constexpr int LS = 1024;  // block set: at most VI_MAX + 1 keys are ever inserted
+  __shared__ unsigned long long s_keys[LS];
+  __shared__ unsigned s_cnt, s_over;
+  for (int t = threadIdx.x; t < LS; t += TPB) s_keys[t] = VI_EMPTY;
+  if (threadIdx.x == 0) {
+    s_cnt = 0;
+    s_over = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (s_over) return;  // uniform: the dictionary already overflowed
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  const int nb = blockIdx.y;
+  if (n < g.nown) {
+    int i, j, k;
+    node_ijk(g, n, i, j, k);
+    double val[9];
+    matrix_block<TABLE>(g, mat, Ke, g.xs + i, g.ys + j, g.zs + k, nb % 3 - 1, (nb / 3) % 3 - 1, nb / 9 - 1, val);
+#pragma unroll
+    for (int q = 0; q < 9; q++) {
+      const unsigned long long key = (unsigned long long)__double_as_longlong(val[q]);
+      if (key == VI_EMPTY) s_over = 1;
+      if (s_over) break;
+      unsigned h = vi_hash(key) & (LS - 1);
+      for (int probe = 0; probe < LS; probe++) {
+        const unsigned long long cur = s_keys[h];
+        if (cur == key) break;
+        if (cur == VI_EMPTY) {
+          const unsigned long long old = atomicCAS(&s_keys[h], VI_EMPTY, key);
+          if (old == VI_EMPTY) {
+            if (atomicAdd(&s_cnt, 1u) >= (unsigned)VI_MAX) s_over = 1;
+            break;
+          }
+          if (old == key) break;
+        }
+        h = (h + 1) & (LS - 1);
+      }
+    }
+  }
+  __syncthreads();
+  if (s_over) {
+    if (threadIdx.x == 0) atomicOr(&ctl[1], 1u);
+    return;
+  }
+  for (int t = threadIdx.x; t < LS; t += TPB) {
+    const unsigned long long key = s_keys[t];
+    if (key == VI_EMPTY) continue;
+    unsigned h = vi_hash(key) & (VI_HASH - 1);
+    int probe = 0;
+    for (; probe < VI_HASH; probe++) {
+      const unsigned long long cur = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (cur == key) break;
+      if (cur == VI_EMPTY) {
+        const unsigned long long old = atomicCAS(&keys[h], VI_EMPTY, key);
+        if (old == VI_EMPTY) {
+          if (atomicAdd(&ctl[0], 1u) >= (unsigned)VI_MAX) atomicOr(&ctl[1], 1u);
+          break;
+        }
+        if (old == key) break;
+      }
+      h = (h + 1) & (VI_HASH - 1);
+    }
+    if (probe == VI_HASH) atomicOr(&ctl[1], 1u);
+  }
+}
+
+// pass 2: thread = owned node; its 27 blocks in slot order S = nb*9 + r*3 + c, each value's
+// dictionary index (set staged in LDS) packed into 16-B chunks [n/64][S/16][n%64]
+template <bool TABLE>
+__global__ __launch_bounds__(TPB) void k_vi_pack(Geo g, Material mat, const double* __restrict__ Ke,
+                                                 const unsigned long long* __restrict__ keys,
+                                                 const unsigned char* __restrict__ slot, u32x4* __restrict__ I) {
+  __shared__ unsigned long long s_keys[VI_HASH];
+  __shared__ unsigned char s_slot[VI_HASH];
+  for (int t = threadIdx.x; t < VI_HASH; t += TPB) {
+    s_keys[t] = keys[t];
+    s_slot[t] = slot[t];
+  }
+  __syncthreads();
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  u32x4* dst = I + (int64_t)(n >> 6) * (VI_CHUNKS * 64) + (n & 63);
+  unsigned w0 = 0, w1 = 0, w2 = 0, w3 = 0;
+  for (int nb = 0; nb < 27; nb++) {
+    double val[9];
+    matrix_block<TABLE>(g, mat, Ke, g.xs + i, g.ys + j, g.zs + k, nb % 3 - 1, (nb / 3) % 3 - 1, nb / 9 - 1, val);
+#pragma unroll
+    for (int q = 0; q < 9; q++) {
+      const unsigned long long key = (unsigned long long)__double_as_longlong(val[q]);
+      unsigned h = vi_hash(key) & (VI_HASH - 1);
+      for (int probe = 0; probe < VI_HASH && s_keys[h] != key; probe++) h = (h + 1) & (VI_HASH - 1);
+      const unsigned idx = s_slot[h];
+      const int S = nb * 9 + q, b = S & 15, sh = 8 * (b & 3);
+      if ((b >> 2) == 0) w0 |= idx << sh;
+      else if ((b >> 2) == 1) w1 |= idx << sh;
+      else if ((b >> 2) == 2) w2 |= idx << sh;
+      else w3 |= idx << sh;
+      if (b == 15 || S == NSLOT - 1) {  // uniform: chunk complete (the last one padded with zeros)
+        u32x4 v = {w0, w1, w2, w3};
+        dst[(S >> 4) * 64] = v;
+        w0 = w1 = w2 = w3 = 0;
+      }
+    }
+  }
+}
+
+// PCSetUp_Jacobi on FMT_VI
+__global__ void k_jacobi_vi(Geo g, const unsigned char* __restrict__ I, const double* __restrict__ dict,
+                            double* __restrict__ dinv) {
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  const unsigned char* ib = I + ((int64_t)(n >> 6) * (VI_CHUNKS * 64) + (n & 63)) * 16;
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    const int S = 13 * 9 + r * 4;
+    double d = dict[ib[(S >> 4) * 64 * 16 + (S & 15)]];
+    if (d != 0.0) d = 1.0 / d;
+    if (d == 0.0) d = 1.0;
+    dinv[3 * n + r] = d;
+  }
+}
+
+// y = A x on FMT_VI: k_spmv with the 122 16-B value pairs replaced by 16 16-B index chunks (256 B
+// per node) and the values read from the dictionary in LDS (interior lanes of a wave share an
+// index: LDS broadcast).  Same node sweep (XCD slabs), same slot order and products as k_spmv, so
+// y is bit-identical to the CPU AIJ product.
+template <bool DOT, bool GATED>
+__global__ __launch_bounds__(TPB) void k_spmv_vi(Geo g, const u32x4* __restrict__ I, const double* __restrict__ dict,
+                                                 const double* __restrict__ x, double* __restrict__ y,
+                                                 double* __restrict__ part, const CgState* __restrict__ cg,
+                                                 SpmvTiling tl) {
+  static_assert(TPB == VI_MAX, "one dictionary entry per thread");
+  __shared__ double tab[VI_MAX];
+  __shared__ double sh[TPB / 64];
+  if (GATED && cg->reason) return;
+  tab[threadIdx.x] = dict[threadIdx.x];
+  __syncthreads();
+  int i = 0, j = 0, k = 0;
+  const int n = spmv_node(g, tl.TX, tl.LPB, tl.nxc, tl.jgroups, tl.subl, i, j, k);
+  double dot = 0.;
+  if (n >= 0) {
+    const int PX = g.PX, PXY = g.PX * g.PY;
+    const int pc = (i + 1) + (j + 1) * PX + (k + 1) * PXY;
+    const u32x4* ip = I + (int64_t)(n >> 6) * (VI_CHUNKS * 64) + (n & 63);
+    u32x4 w[VI_CHUNKS];
+#pragma unroll
+    for (int q = 0; q < VI_CHUNKS; q++) w[q] = __builtin_nontemporal_load(ip + q * 64);
+    double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+#pragma unroll
+    for (int nb = 0; nb < 27; nb++) {
+      const int off = (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
+      const double* xp = x + 3 * (int64_t)(pc + off);
+      const double xv[3] = {xp[0], xp[1], xp[2]};
+      if (nb == 13) {
+        xc0 = xv[0];
+        xc1 = xv[1];
+        xc2 = xv[2];
+      }
+#pragma unroll
+      for (int q = 0; q < 9; q++) {
+        const int S = nb * 9 + q, r = q / 3, cc = q % 3;
+        const double v = tab[(w[S >> 4][(S >> 2) & 3] >> (8 * (S & 3))) & 255u];
+        if (r == 0) y0 += v * xv[cc];
+        else if (r == 1) y1 += v * xv[cc];
+        else y2 += v * xv[cc];
+      }
+    }
+    __builtin_nontemporal_store(y0, &y[3 * n + 0]);
+    __builtin_nontemporal_store(y1, &y[3 * n + 1]);
+    __builtin_nontemporal_store(y2, &y[3 * n + 2]);
+    if (DOT) dot = xc0 * y0 + xc1 * y1 + xc2 * y2;
+  }
+  if (DOT) {
+    double s = block_sum<TPB>(dot, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+  }
+}
+
 static void z_shape(int kern, int& ztx, int& zty) {
   switch (kern) {
     case 2: ztx = 32; zty = 4; break;
@@ -2212,8 +2414,56 @@ int build_split(Ctx& c, bool* exact) {
   return 0;
 }
 
+// FMT_VI assembly (see k_vi_collect).  ok = the matrix has at most VI_MAX distinct values; the
+// dictionary is the sorted set of their bit patterns, so indices do not depend on the order
+// the set was filled in.
+int build_vi(Ctx& c, bool* ok) {
+  *ok = false;
+  const bool table = table_law(c);
+  MCX_HIP(hipMemsetAsync(c.vi_keys, 0xff, VI_HASH * sizeof(unsigned long long), c.stream));
+  MCX_HIP(hipMemsetAsync(c.vi_ctl, 0, 2 * sizeof(unsigned), c.stream));
+  const dim3 grid(nblk(c.g.nown), 27);
+  if (table)
+    hipLaunchKernelGGL(k_vi_collect<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.vi_keys, c.vi_ctl);
+  else
+    hipLaunchKernelGGL(k_vi_collect<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.vi_keys, c.vi_ctl);
+  unsigned ctl[2];
+  std::vector<unsigned long long> keys(VI_HASH);
+  MCX_HIP(hipMemcpyAsync(ctl, c.vi_ctl, sizeof(ctl), hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipMemcpyAsync(keys.data(), c.vi_keys, VI_HASH * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                         c.stream));
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  if (ctl[1] || ctl[0] > (unsigned)VI_MAX) return 0;
+  std::vector<unsigned long long> vals;
+  for (unsigned long long k : keys)
+    if (k != VI_EMPTY) vals.push_back(k);
+  std::sort(vals.begin(), vals.end());
+  std::vector<unsigned char> slot(VI_HASH, 0);
+  for (int h = 0; h < VI_HASH; h++)
+    if (keys[h] != VI_EMPTY)
+      slot[h] = (unsigned char)(std::lower_bound(vals.begin(), vals.end(), keys[h]) - vals.begin());
+  std::vector<double> dict(VI_MAX, 0.);
+  for (size_t q = 0; q < vals.size(); q++) std::memcpy(&dict[q], &vals[q], sizeof(double));
+  MCX_HIP(hipMemcpyAsync(c.vi_slot, slot.data(), VI_HASH, hipMemcpyHostToDevice, c.stream));
+  MCX_HIP(hipMemcpyAsync(c.vi_dict, dict.data(), VI_MAX * sizeof(double), hipMemcpyHostToDevice, c.stream));
+  u32x4* I = reinterpret_cast<u32x4*>(c.vi_idx);
+  if (table)
+    hipLaunchKernelGGL(k_vi_pack<true>, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.vi_keys,
+                       c.vi_slot, I);
+  else
+    hipLaunchKernelGGL(k_vi_pack<false>, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.vi_keys,
+                       c.vi_slot, I);
+  // the host copies above must outlive the async uploads
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  c.vi_n = (int)vals.size();
+  *ok = true;
+  return 0;
+}
+
 void launch_jacobi(Ctx& c) {
-  if (c.fmt != FMT_V)
+  if (c.fmt == FMT_VI)
+    hipLaunchKernelGGL(k_jacobi_vi, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.vi_idx, c.vi_dict, c.dinv);
+  else if (c.fmt != FMT_V)
     hipLaunchKernelGGL(k_jacobi_sym, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.U, c.dinv);
   else
     hipLaunchKernelGGL(k_jacobi, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.V, c.dinv);
@@ -2222,6 +2472,19 @@ void launch_jacobi(Ctx& c) {
 void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
   const int nb = (int)spmv_grid_blocks(c);
   const SpmvTiling tl = spmv_tiling(c.g, c.spmv_subl);
+  if (c.fmt == FMT_VI) {
+    const u32x4* I = reinterpret_cast<const u32x4*>(c.vi_idx);
+    if (dot && gated)
+      hipLaunchKernelGGL((k_spmv_vi<true, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_dict, xpad, y,
+                         c.partials, c.cg, tl);
+    else if (dot)
+      hipLaunchKernelGGL((k_spmv_vi<true, false>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_dict, xpad, y,
+                         c.partials, c.cg, tl);
+    else
+      hipLaunchKernelGGL((k_spmv_vi<false, false>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_dict, xpad, y,
+                         c.partials, c.cg, tl);
+    return;
+  }
   if (c.fmt == FMT_SPLIT) {
     int ztx, zty;
     split_shape(c, ztx, zty);

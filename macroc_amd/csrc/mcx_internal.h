@@ -70,7 +70,13 @@ struct Ctx;
 // the AIJ matrix held exactly as its upper blocks U plus, per owned node, the bf16 correction
 // lower - mirror(upper) of the correction slots that are non-zero somewhere in the matrix
 // (every AIJ value reconstructs bit for bit; rows summed in the z-marching order).
-enum Fmt { FMT_V = 0, FMT_U = 1, FMT_SPLIT = 2 };
+// FMT_VI: the AIJ matrix held exactly as one byte per value, an index into a dictionary of the
+// matrix's distinct values (at most 256; value-indexed CSR, Kourtis et al. 2008), all 27
+// blocks per node in FMT_V's slot order — every row summed in the CPU AIJ order.
+enum Fmt { FMT_V = 0, FMT_U = 1, FMT_SPLIT = 2, FMT_VI = 3 };
+constexpr int VI_MAX = 256;     // dictionary entries (one index byte per value)
+constexpr int VI_HASH = 4096;   // open-addressing set of the distinct values (bit patterns)
+constexpr int VI_CHUNKS = 16;   // 16-B index chunks per node: 243 slots + 13 zero pad bytes
 
 // AIJ-split correction slots, passed by value: slot = nb*9 + r*3 + c of the row node's lower
 // block nb < 13 holds A(n, nb)[r][c] - U(m, 26-nb)[c][r], m = n + off(nb); nb = 13 (the
@@ -133,6 +139,16 @@ struct Ctx {
   uint16_t* D = nullptr;     // AIJ-split: bf16 corrections of the padded box [u_of/64][dsl.Lq][64] x 8
   int64_t D_bytes = 0;       // allocated bytes of D (grown to the active slots' quads)
   unsigned* d_mask = nullptr;  // AIJ-split assembly: [0..13] slot masks per lower block, [14] inexact
+  // value-indexed AIJ (FMT_VI): index bytes [ngroups][VI_CHUNKS][64] x 16 B, the dictionary
+  // (VI_MAX doubles, ascending bit pattern), the build's value set and its slot -> index map
+  unsigned char* vi_idx = nullptr;
+  double* vi_dict = nullptr;
+  unsigned long long* vi_keys = nullptr;  // [VI_HASH]
+  unsigned char* vi_slot = nullptr;       // [VI_HASH]
+  unsigned* vi_ctl = nullptr;             // [0] distinct values, [1] overflow
+  int vi_n = 0;                           // dictionary entries of the current matrix
+  int aij_vi = 1;            // aij: assemble in FMT_VI when the matrix has at most VI_MAX distinct values
+  bool vi_declined = false;  // a per-GP-tangent law overflowed the dictionary: skip the attempt
   int fmt = FMT_V;           // storage the matrix is currently assembled in
   bool assembled = false;    // a matrix has been assembled (mcx_assembly_jac)
   int aij_split = 1;         // aij: assemble in FMT_SPLIT when every correction is exact in bf16
@@ -228,6 +244,7 @@ void launch_element_ke(Ctx& c);        // Ke of a per-GP-tangent law
 void launch_gather_matrix(Ctx& c);
 void launch_gather_matrix_sym(Ctx& c);
 int build_split(Ctx& c, bool* exact);  // AIJ-split corrections from U (exact = usable)
+int build_vi(Ctx& c, bool* ok);        // value-indexed AIJ (ok = at most VI_MAX distinct values)
 void launch_jacobi(Ctx& c);
 void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated);
 void launch_update_u(Ctx& c);

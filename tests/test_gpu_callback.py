@@ -126,7 +126,7 @@ def step_and_compare(m, P, inject=None):
 def test_host_micropp_callbacks(grid):
     rtol = 1e-12
     P = O.Problem(*grid, rtol=rtol)
-    with M.Macroc(argv(*grid, rtol, ["-mat_aij_split", 0])) as m:
+    with M.Macroc(argv(*grid, rtol, ["-mat_aij_vi", 0, "-mat_aij_split", 0])) as m:
         law = HostMicropp(m.ngp, iso_C(E_DEF, NU_DEF))
         law.register(m)
         step_and_compare(m, P)
@@ -139,7 +139,8 @@ def test_host_micropp_callbacks(grid):
 
 
 def test_device_law_default_storage():
-    """A device law from another library, default AIJ-split storage (bit-exact matrix dump)."""
+    """A device law from another library, default AIJ storage: its per-GP tangents are all the
+    isotropic C, so the matrix is value-indexed (bit-exact matrix dump)."""
     grid, rtol = (8, 8, 8), 1e-12
     P = O.Problem(*grid, rtol=rtol)
     L = testlaw()
@@ -149,6 +150,7 @@ def test_device_law_default_storage():
         m.set_option("split_maxq", 30)
         m.set_device_law(law)
         step_and_compare(m, P)
+        assert m.get_info()["storage"] == 3
         m.update_vars()
         upd = C.c_int()
         assert L.testlaw_device_calls(C.byref(law), C.byref(upd)) == 1 and upd.value == 1
@@ -190,7 +192,7 @@ def test_external_law_multirank_box():
         P.apply_bc_u(P.get_displacement(ts))
     P.set_strains(); P.homogenize(); P.assembly_res(); P.assembly_jac()
     Cm = iso_C(E_DEF, NU_DEF)
-    args = argv(*grid, rtol, ["-da_processors_x", 2, "-mat_aij_split", 0])
+    args = argv(*grid, rtol, ["-da_processors_x", 2, "-mat_aij_vi", 0, "-mat_aij_split", 0])
     g = M.LocalGroup(2)
     out, errs = [None, None], []
 

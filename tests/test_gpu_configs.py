@@ -2,11 +2,12 @@
 oracle cannot run these grids in seconds, so its parity is held by the same code path at the
 small grids of test_gpu_parity.py / test_gpu_nonlinear.py).
 
-Config 3: 256^3, -ts 2, -ksp_rtol 1e-8, default AIJ storage (upper blocks + bf16 corrections):
+Config 3: 256^3, -ts 2, -ksp_rtol 1e-8, default AIJ storage (value-indexed: one byte per value):
   * CG/Jacobi iterations in the 2,700-2,950 window (the survey's independent scipy estimate is
     ~11.3 N = 2,900; the oracle restatement's count at 64^3 is 720, SURVEY §3.2);
   * converged on rtol (KSP_CONVERGED_RTOL) with the true residual |A du - b| / |b| <= 10 rtol;
-  * the storage is the exact split one (every AIJ value reconstructed bit for bit: 24 bf16 slots);
+  * the storage is the value-indexed one (at most 256 distinct values; the AIJ-split storage, 24
+    bf16 correction slots, solves the same system to the same iteration count);
   * symmetry x.(A y) == y.(A x) to rounding, linearity of the SpMV;
   * a repeated Newton step (u zeroed, same BC) reproduces du bit for bit (deterministic kernels).
 Config 5: 128^3, -micro_n 10, J2-plastic Gauss-point law, non-linear Newton (dt 0.01):
@@ -40,7 +41,7 @@ def test_config3_256_cubed():
 
         res, its, reason, du = step()
         info = m.get_info()
-        assert (info["storage"], info["split_slots"], info["split_bits"]) == (2, 24, 16)
+        assert info["storage"] == 3 and 0 < info["vi_values"] <= 256, info
         assert 2700 <= its <= 2950 and reason == 2, (its, reason)
         b = m.b()
         r = m.spmv(du) - b
@@ -54,6 +55,13 @@ def test_config3_256_cubed():
         assert np.linalg.norm(Axy - (Ax + 2.0 * Ay)) <= 1e-13 * np.linalg.norm(np.abs(Ax) + 2.0 * np.abs(Ay))
         res2, its2, reason2, du2 = step()
         assert res2 == res and its2 == its and np.array_equal(du2, du)
+        # the AIJ-split storage of the same matrix: 24 exact bf16 correction slots, same solve
+        m.set_option("aij_vi", 0)
+        res3, its3, reason3, du3 = step()
+        info = m.get_info()
+        assert (info["storage"], info["split_slots"], info["split_bits"]) == (2, 24, 16)
+        assert res3 == res and abs(its3 - its) <= 1 and reason3 == 2
+        assert np.linalg.norm(m.spmv(du3) - b) <= 10 * rtol * np.linalg.norm(b)
 
 
 def test_config5_nonlinear_128(capfd):

@@ -68,13 +68,20 @@ def newton_step(x_global_nat, options=()):
 @pytest.mark.parametrize("name", ["g1088_r2", "g888_r8", "g522_r3", "g534_r8"])
 def test_multirank_newton_step(name):
     """AIJ blocks in the CPU AIJ order (-mat_aij_split 0): SpMV bit-exact on any rank grid."""
-    _multirank(name, sbaij=False, extra=["-mat_aij_split", 0])
+    _multirank(name, sbaij=False, extra=["-mat_aij_vi", 0, "-mat_aij_split", 0])
+
+
+@pytest.mark.parametrize("name", ["g1088_r2", "g888_r8", "g522_r3", "g534_r8"])
+def test_multirank_aij_vi(name):
+    """Default AIJ storage for the elastic law: value-indexed (one byte per value + a per-rank
+    dictionary), rows in the CPU AIJ order: matrix and SpMV bit-exact on any rank grid."""
+    _multirank(name, sbaij=False, vi=True)
 
 
 @pytest.mark.parametrize("name", ["g1088_r2", "g888_r8", "g534_r8"])
 def test_multirank_aij_split(name):
-    """Default AIJ storage (upper blocks + bf16 corrections): matrix bit-exact, SpMV rounding."""
-    _multirank(name, sbaij=False, split=True)
+    """AIJ-split storage (upper blocks + bf16 corrections): matrix bit-exact, SpMV rounding."""
+    _multirank(name, sbaij=False, extra=["-mat_aij_vi", 0], split=True)
 
 
 @pytest.mark.parametrize("name", ["g1088_r2", "g888_r8"])
@@ -82,7 +89,7 @@ def test_multirank_sbaij(name):
     _multirank(name, sbaij=True)
 
 
-def _multirank(name, sbaij, extra=(), split=False):
+def _multirank(name, sbaij, extra=(), split=False, vi=False):
     fx = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     NX, NY, NZ = (int(v) for v in fx["grid"])
     nr = int(fx["nranks"])
@@ -118,6 +125,8 @@ def _multirank(name, sbaij, extra=(), split=False):
         dset.append(o["dir"])
         if split:
             assert o["info"]["storage"] == 2
+        if vi:
+            assert o["info"]["storage"] == 3 and 0 < o["info"]["vi_values"] <= 256
         if sbaij or split:  # z-marching kernels: whole-3-vector mirrored terms, rounding-level
             absrow = np.add.reduceat(np.abs(v1) * np.abs(x[ci1]), rp1[:-1])
             assert np.all(np.abs(o["y"] - y1[o["nat"]]) <= 1e-14 * absrow[o["nat"]] + 1e-300)
@@ -160,6 +169,8 @@ def test_multirank_full_tiles(grid, procs, mat):
     nr, rtol = px * py * pz, 1e-10
     argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
             "-da_processors_z", pz, "-ksp_rtol", repr(rtol), "-dm_mat_type", mat.split("-")[0]]
+    if mat.startswith("aij"):
+        argv += ["-mat_aij_vi", 0]  # the z-marching AIJ-split kernels
     # 8: phased 64x4; aij-tall: 64x16 AIJ-split tiles (internal x faces at every tile's lanes 0 / 63)
     # aij-dense: split_maxq 0 sends every correction to the dense second pass (k_split_dense)
     opts = {"aij": [("split_maxq", 30)], "aij-tall": [("split_maxq", 30), ("split_tx", 64), ("split_ty", 16)],

@@ -40,7 +40,7 @@ def test_newton_step_single_rank(name):
     NX, NY, NZ = (int(v) for v in fx["grid"])
     rtol = float(fx["rtol"])
     P = O.Problem(NX, NY, NZ, rtol=rtol)
-    with M.Macroc(argv_for(NX, NY, NZ, rtol, ["-mat_aij_split", 0])) as m:
+    with M.Macroc(argv_for(NX, NY, NZ, rtol, ["-mat_aij_vi", 0, "-mat_aij_split", 0])) as m:
         petsc, nat = m.owned_dofs()
         assert np.array_equal(petsc, fx["dof_map"][nat])
         assert np.array_equal(m.dump_dirichlet(), fx["dirichlet"])
@@ -88,15 +88,83 @@ def test_newton_step_single_rank(name):
 
 
 @pytest.mark.parametrize("name", SINGLE)
+def test_aij_vi_single_rank(name):
+    """Default AIJ storage for the elastic law: value-indexed (one index byte per value into a
+    dictionary of the matrix's distinct values).  Matrix dump and SpMV bit-exact with the
+    oracle's CPU AIJ (same row order as the AIJ blocks), the dictionary sorted and small, the
+    solve's residual history equal to the fixture's."""
+    fx = load(name)
+    NX, NY, NZ = (int(v) for v in fx["grid"])
+    rtol = float(fx["rtol"])
+    P = O.Problem(NX, NY, NZ, rtol=rtol)
+    with M.Macroc(argv_for(NX, NY, NZ, rtol)) as m:
+        for ts in (0, 1):
+            m.apply_bc_on_u(m.get_displacement(ts))
+            P.apply_bc_u(m.get_displacement(ts))
+        m.set_strains(); m.homogenize(); m.assembly_res()
+        P.set_strains(); P.homogenize(); P.assembly_res()
+        m.assembly_jac()
+        P.assembly_jac()
+        info = m.get_info()
+        rp, ci, v = m.dump_csr()
+        assert np.array_equal(v, P.A_values())
+        nval = len(np.unique(v.view(np.int64)))  # distinct bit patterns of the AIJ values
+        assert info["storage"] == 3 and nval <= info["vi_values"] <= nval + 1  # + the clipped blocks' 0
+        x = np.random.default_rng(42).uniform(-1, 1, m.n)
+        y = m.spmv(x)
+        assert np.array_equal(y, P.spmv(x))
+        assert np.array_equal(m.spmv(x), y)
+        its, rn, reason = m.solve_Ax()
+        assert abs(its - int(fx["its"])) <= 1
+        ref = fx["du"]
+        if np.linalg.norm(ref) > 0:
+            assert np.linalg.norm(m.du() - ref) <= du_tol(rtol) * np.linalg.norm(ref)
+            h = m.ksp_history()
+            k = min(len(h), len(fx["history"]), 20)
+            np.testing.assert_allclose(h[:k], fx["history"][:k], rtol=1e-9)
+        # the same matrix through -mat_aij_vi 0 -mat_aij_split 0 (AIJ blocks): identical products
+        m.set_option("aij_vi", 0)
+        m.set_option("aij_split", 0)
+        m.assembly_jac()
+        assert m.get_info()["storage"] == 0 and np.array_equal(m.spmv(x), y)
+
+
+def test_aij_vi_fallback_and_toggle():
+    """More than 256 distinct values (a plastic tangent) overflow the dictionary: the assembly
+    falls back to the AIJ-split storage, bit-exact; an elastic matrix is value-indexed again
+    once the option is re-enabled."""
+    NX, NY, NZ, dt = 12, 10, 12, 0.05
+    P = O.Problem(NX, NY, NZ, rtol=1e-10, law=1, dt=dt, bc_type=0)
+    P.apply_bc_u(P.get_displacement(1))
+    P.set_strains(); P.homogenize(); P.assembly_res(); P.assembly_jac(); P.solve(); P.update_u()
+    u = P.u()
+    P.set_strains(); P.homogenize(); P.assembly_jac()
+    argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-dt", dt, "-mat_law", "plastic", "-bc_type", 0]
+    with M.Macroc(argv) as m:
+        m.apply_bc_on_u(m.get_displacement(1))
+        m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
+        assert m.get_info()["storage"] == 3  # still elastic everywhere: one tangent, few values
+        m.solve_Ax(); m.update_u()
+        m.set_u(u)
+        m.set_strains(); m.homogenize(); m.assembly_jac()
+        info = m.get_info()
+        assert info["storage"] == 2 and info["vi_values"] == 0
+        assert np.array_equal(m.dump_csr()[2], P.A_values())
+    with pytest.raises(M.MacrocError):
+        with M.Macroc(["-da_grid_x", 6, "-da_grid_y", 6, "-da_grid_z", 6, "-dm_mat_type", "sbaij"]) as m:
+            m.set_option("aij_vi", 1)
+
+
+@pytest.mark.parametrize("name", SINGLE)
 def test_aij_split_single_rank(name):
-    """Default AIJ storage: upper blocks + bf16 lower corrections.  Every AIJ value is
+    """AIJ-split storage: upper blocks + bf16 lower corrections.  Every AIJ value is
     reconstructed bit for bit (matrix dump == oracle), the SpMV rows differ from the CPU order
     by rounding only (<= 1e-14 of sum |a_ij x_j|), the solve meets the north-star bar."""
     fx = load(name)
     NX, NY, NZ = (int(v) for v in fx["grid"])
     rtol = float(fx["rtol"])
     P = O.Problem(NX, NY, NZ, rtol=rtol)
-    with M.Macroc(argv_for(NX, NY, NZ, rtol)) as m:
+    with M.Macroc(argv_for(NX, NY, NZ, rtol, ["-mat_aij_vi", 0])) as m:
         m.set_option("split_maxq", 30)  # tiny grids are boundary-dominated: dense corrections
         for ts in (0, 1):
             m.apply_bc_on_u(m.get_displacement(ts))
@@ -325,7 +393,7 @@ def test_aij_split_tile_shapes(NX, NY, NZ):
     in one canonical order — results bitwise equal across shapes, rows within 1e-14 sum|a||x|
     of the oracle's CPU order."""
     P = O.Problem(NX, NY, NZ, rtol=1e-8)
-    with M.Macroc(argv_for(NX, NY, NZ, 1e-8)) as m:
+    with M.Macroc(argv_for(NX, NY, NZ, 1e-8, ["-mat_aij_vi", 0])) as m:
         m.set_option("split_maxq", 30)
         for ts in (0, 1):
             m.apply_bc_on_u(m.get_displacement(ts))

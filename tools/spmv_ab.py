@@ -18,11 +18,15 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--grid", default="256", help="N or NX,NY,NZ")
 ap.add_argument("--mat", default="aij", choices=["aij", "sbaij"])
 ap.add_argument("--split", type=int, default=1, help="aij: -mat_aij_split")
+ap.add_argument("--vi", type=int, default=1, help="aij: -mat_aij_vi")
 ap.add_argument("--variants", default="split_tx=0", help="';'-separated option sets 'name=value,name=value'")
 ap.add_argument("--base", default="split_tx=0,spmv_zblocks=0", help="options every variant starts from")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--lib", default="", help="another build of libmacroc_amd.so (e.g. the previous commit's)")
 a = ap.parse_args()
+if a.lib:
+    M.LIB_PATH = os.path.abspath(a.lib)
 
 
 def parse(spec):
@@ -31,7 +35,8 @@ def parse(spec):
 
 g = [int(v) for v in a.grid.split(",")]
 NX, NY, NZ = g if len(g) == 3 else g * 3
-m = M.Macroc(["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-dm_mat_type", a.mat, "-mat_aij_split", a.split])
+m = M.Macroc(["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-dm_mat_type", a.mat, "-mat_aij_split", a.split,
+              "-mat_aij_vi", a.vi])
 m.apply_bc_on_u(m.get_displacement(1))
 m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
 base = parse(a.base)
