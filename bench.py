@@ -239,7 +239,7 @@ def measure(argv, rank, world, comm_id, args, steps, warmup):
     return {"its": its, "tm": tm, "info": info, "check": check, "spmv_avg_ms": spmv_avg_ms, "spmv_bytes": spmv_bytes,
             "csr_bytes": csr_bytes, "storage": STORAGE_NAME[storage["storage"]], "storage_id": storage["storage"],
             "split_slots": storage["split_slots"], "split_bits": storage["split_bits"],
-            "vi_values": storage["vi_values"],
+            "vi_values": storage["vi_values"], "vi_bits": storage["vi_bits"], "vi_blocks": storage["vi_blocks"],
             "achieved": spmv_bytes / (spmv_avg_ms * 1e-3) / 1e9, "ms_step": dt / max(steps, 1) * 1e3,
             "warmup_s": t_warm}
 
@@ -340,7 +340,7 @@ def main():
                        "dofs": ndofs, "nnz": info["nnz_global"], "parallelism": f"dmda{px}x{py}x{pz}",
                        "mat_type": "aij" if args.mat_type.startswith("aij") else "sbaij", "storage": r["storage"],
                        "split_slots": r["split_slots"], "split_bits": r["split_bits"],
-                       "vi_values": r["vi_values"]},
+                       "vi_values": r["vi_values"], "vi_bits": r["vi_bits"], "vi_blocks": r["vi_blocks"]},
             "cg_its": its,
             "ms_per_cg_iter": tm["solve_ms"] / max(its, 1),
             # CG iterations grow ~linearly with the global grid edge (720 at 64^3, 2814 at 256^3),

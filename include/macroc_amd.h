@@ -128,7 +128,11 @@ typedef struct {
      nex*ney*nez; Gauss point gpi = ie*8 + gp.  One rank: DMDAGetElements' own order.  Several
      ranks: the rank's PETSc elements plus the upper ghost layer (owner computes). */
   int64_t ex0, ey0, ez0, nex, ney, nez;
-  int vi_values;                /* value-indexed AIJ: dictionary entries (distinct matrix values) */
+  int vi_values;                /* value-indexed AIJ: distinct matrix values */
+  int vi_bits;                  /* value-indexed AIJ: 4 = a nibble per value into its slot's dictionary
+                                   (every slot takes <= 16 values), 8 = a byte into one dictionary */
+  int vi_blocks;                /* value-indexed AIJ, block mode: distinct 3x3 blocks (one index byte per
+                                   block into a dictionary of them), 0 when values are indexed one by one */
 } mcx_info;
 
 typedef struct {

@@ -54,7 +54,7 @@ static int free_ctx(Ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
-  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->eps, c->sig, c->ctan, c->Ke,
+  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf, c->halo.d_bnd};
   for (void* p : ptrs)
@@ -79,16 +79,19 @@ static int free_ctx(Ctx* c) {
 
 // largest SpMV grid over the selectable kernels (mcx_set_option may switch between them)
 static int64_t max_spmv_blocks(Ctx& c) {
-  const int keep = c.spmv_kernel, keep_fmt = c.fmt;
+  const int keep = c.spmv_kernel, keep_fmt = c.fmt, keep_bits = c.vi_bits;
   int64_t m = 0;
-  for (int f : {FMT_V, FMT_U, FMT_SPLIT})
-    for (int k = 0; k <= 11; k++) {
-      c.fmt = f;
-      c.spmv_kernel = k;
-      m = std::max(m, spmv_grid_blocks(c));
-    }
+  for (int f : {FMT_V, FMT_U, FMT_SPLIT, FMT_VI})
+    for (int k = 0; k <= 11; k++)
+      for (int bits : {4, 8}) {
+        c.fmt = f;
+        c.spmv_kernel = k;
+        c.vi_bits = bits;
+        m = std::max(m, spmv_grid_blocks(c));
+      }
   c.spmv_kernel = keep;
   c.fmt = keep_fmt;
+  c.vi_bits = keep_bits;
   return m;
 }
 
@@ -484,6 +487,8 @@ static void fill_info(const Ctx& c, mcx_info* in) {
   in->split_slots = c.fmt == FMT_SPLIT ? c.dsl.L : 0;
   in->split_bits = c.fmt == FMT_SPLIT ? (c.dsl.wide ? 32 : 16) : 0;
   in->vi_values = c.fmt == FMT_VI ? c.vi_n : 0;
+  in->vi_bits = c.fmt == FMT_VI ? c.vi_bits : 0;
+  in->vi_blocks = c.fmt == FMT_VI && c.vi_block ? c.vi_nblocks : 0;
   in->ex0 = g.ex0;
   in->ey0 = g.ey0;
   in->ez0 = g.ez0;
@@ -756,11 +761,13 @@ static int ensure_VI(Ctx& c) {
   if (c.vi_idx) return 0;
   const int64_t idx_bytes = c.ngroups * VI_CHUNKS * 64 * 16;
   MCX_HIP(hipMalloc(&c.vi_idx, idx_bytes));
-  MCX_HIP(hipMalloc(&c.vi_dict, VI_MAX * sizeof(double)));
-  MCX_HIP(hipMalloc(&c.vi_keys, VI_HASH * sizeof(unsigned long long)));
-  MCX_HIP(hipMalloc(&c.vi_slot, VI_HASH));
-  MCX_HIP(hipMalloc(&c.vi_ctl, 2 * sizeof(unsigned)));
-  c.device_bytes += idx_bytes + VI_MAX * sizeof(double) + VI_HASH * 9 + 8;
+  const int64_t nd = std::max(VI_MAX, NSLOT * 16), nk = 2 * VI_HASH + NSLOT * 32;
+  MCX_HIP(hipMalloc(&c.vi_dict, nd * sizeof(double)));
+  MCX_HIP(hipMalloc(&c.vi_bdict, VI_MAX * VIB_STRIDE * sizeof(double)));
+  MCX_HIP(hipMalloc(&c.vi_keys, nk * sizeof(unsigned long long)));
+  MCX_HIP(hipMalloc(&c.vi_slot, nk));
+  MCX_HIP(hipMalloc(&c.vi_ctl, (5 + NSLOT) * sizeof(unsigned)));
+  c.device_bytes += idx_bytes + nd * 8 + VI_MAX * VIB_STRIDE * 8 + nk * 9 + (5 + NSLOT) * 4;
   return 0;
 }
 
@@ -1110,9 +1117,10 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
   std::vector<double> dict;
   if (vals && c.fmt == FMT_VI) {
     Ih.resize((size_t)c.ngroups * VI_CHUNKS * 64 * 16);
-    dict.resize(VI_MAX);
+    dict.resize(c.vi_block ? VI_MAX * VIB_STRIDE : std::max(VI_MAX, NSLOT * 16));
     MCX_HIP(hipMemcpyAsync(Ih.data(), c.vi_idx, Ih.size(), hipMemcpyDeviceToHost, c.stream));
-    MCX_HIP(hipMemcpyAsync(dict.data(), c.vi_dict, VI_MAX * sizeof(double), hipMemcpyDeviceToHost, c.stream));
+    MCX_HIP(hipMemcpyAsync(dict.data(), c.vi_block ? c.vi_bdict : c.vi_dict, dict.size() * sizeof(double),
+                           hipMemcpyDeviceToHost, c.stream));
     MCX_HIP(hipStreamSynchronize(c.stream));
   } else if (vals) {
     V.resize(up ? c.npgroups * UPAIR * 128 : c.ngroups * NPAIR * 128);
@@ -1170,7 +1178,14 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
             else v = uval(pc, 6 + 9 * (nb - 14) + r * 3 + cc);
           } else if (vals && c.fmt == FMT_VI) {
             const int s = nb * 9 + r * 3 + cc;
-            v = dict[Ih[(((n >> 6) * VI_CHUNKS + (s >> 4)) * 64 + (n & 63)) * 16 + (s & 15)]];
+            if (c.vi_block) {  // byte nb of 2 chunks of 16 B: the block's dictionary entry
+              v = dict[Ih[(((n >> 6) * 2 + (nb >> 4)) * 64 + (n & 63)) * 16 + (nb & 15)] * VIB_STRIDE + r * 3 + cc];
+            } else if (c.vi_bits == 8) {
+              v = dict[Ih[(((n >> 6) * VI_CHUNKS + (s >> 4)) * 64 + (n & 63)) * 16 + (s & 15)]];
+            } else {  // nibble s of 8 chunks of 16 B, low nibble first
+              const unsigned char byte = Ih[(((n >> 6) * 8 + (s >> 5)) * 64 + (n & 63)) * 16 + ((s & 31) >> 1)];
+              v = dict[s * 16 + ((s & 1) ? byte >> 4 : byte & 15)];
+            }
           } else if (vals) {
             int s = nb * 9 + r * 3 + cc;
             v = V[(n >> 6) * (NPAIR * 128) + (int64_t)(s >> 1) * 128 + 2 * (n & 63) + (s & 1)];
@@ -1264,9 +1279,12 @@ int mcx_get_timing(void* ctx, mcx_timing* t) {
   *t = c.t;
   // algorithmic bytes of one SpMV in this format: the stencil-block values actually present
   // (AIJ nonzeros of the owned rows x 8 B), x read once, y written once
-  // (value-indexed: one index byte per nonzero; the 13 pad bytes per node it also loads are not counted)
-  t->spmv_bytes_per_launch = (c.fmt == FMT_V ? c.nnz_local * 8 : (c.fmt == FMT_VI ? c.nnz_local : c.nupper_local * 8)) +
-                             2 * 3 * (int64_t)c.g.nown * 8;
+  // (value-indexed: vi_bits per nonzero; the pad up to whole 16-B chunks per node is not counted)
+  t->spmv_bytes_per_launch =
+      (c.fmt == FMT_V    ? c.nnz_local * 8
+       : c.fmt == FMT_VI ? (c.vi_block ? c.nnz_local / 9 : (c.nnz_local * c.vi_bits + 7) / 8)
+                         : c.nupper_local * 8) +
+      2 * 3 * (int64_t)c.g.nown * 8;
   if (c.fmt == FMT_SPLIT) t->spmv_bytes_per_launch += (int64_t)c.g.nown * c.dsl.Lq * 16;
   return 0;
 }
@@ -1305,7 +1323,7 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     return 0;
   }
   if (!std::strcmp(name, "split_dbg")) {
-    c.split_dbg = std::max(0, std::min(2, (int)value));
+    c.split_dbg = std::max(0, std::min(3, (int)value));
     return 0;
   }
   if (!std::strcmp(name, "split_tx")) {
@@ -1338,6 +1356,27 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.split_ty = v;
     if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
       set_error("split_ty: partials buffer too small");
+      return 2;
+    }
+    return 0;
+  }
+  if (!std::strcmp(name, "vi_bits")) {  // takes effect at the next mcx_assembly_jac
+    const int v = (int)value;
+    if (v != 4 && v != 8) {
+      set_error("vi_bits: 4 (per-slot nibbles where every slot has <= 16 values) or 8");
+      return 2;
+    }
+    c.vi_bits_max = v;
+    return 0;
+  }
+  if (!std::strcmp(name, "vi_block")) {  // takes effect at the next mcx_assembly_jac
+    c.vi_block_on = value != 0.;
+    return 0;
+  }
+  if (!std::strcmp(name, "vi_stage")) {
+    c.vi_stage = value != 0.;
+    if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
+      set_error("vi_stage: partials buffer too small");
       return 2;
     }
     return 0;

@@ -1534,13 +1534,18 @@ __global__ __launch_bounds__(TPB) void k_split_dense(Geo g, const uint16_t* __re
 
 // ---------------------------------------------------------------------------- value-indexed AIJ
 // FMT_VI.  The assembled AIJ values of the elastic law take few distinct values (the stencil of
-// a uniform grid, its boundary variants and the Dirichlet 0 / 1 entries: 129 at 12^3, the same
-// set at any size), so the matrix is held exactly as one index byte per value into a dictionary
-// of them: 243 bytes per node instead of 1,944 (value-indexed CSR, Kourtis, Goumas & Koziris,
-// CF'08).  Built at every assembly in two passes over the on-the-fly blocks (matrix_block):
-// k_vi_collect gathers the distinct values (a per-block LDS set, then a global set); the host
-// sorts them into the dictionary; k_vi_pack writes the index bytes.  More than VI_MAX distinct
-// values (a per-GP tangent) = overflow: the context falls back to AIJ-split / AIJ blocks.
+// a uniform grid, its boundary variants and the Dirichlet 0 / 1 entries: 129 at 12^3, 89 at
+// 256^3), and any one slot S = nb*9 + r*3 + c of a node's 27 blocks takes at most 12 of them
+// (12^3 .. 40^3, tests/test_gpu_parity.py).  So the matrix is held exactly as small indices into
+// dictionaries of its values (value-indexed CSR, Kourtis, Goumas & Koziris, CF'08):
+//   vi_bits 4: one nibble per value into the slot's own dictionary (<= 16 entries per slot):
+//              128 B per node (243 nibbles + pad) instead of 1,944;
+//   vi_bits 8: one byte per value into one dictionary of <= 256 entries: 256 B per node.
+// Built at every assembly in two passes over the on-the-fly blocks (matrix_block): k_vi_collect
+// gathers the distinct values (per block and slot in LDS, then per slot and overall in global
+// sets); the host sorts them into the dictionaries (so indices do not depend on the order the
+// sets were filled in); k_vi_pack writes the indices.  More than 256 distinct values (a per-GP
+// tangent) = overflow: the context falls back to AIJ-split / AIJ blocks.
 constexpr unsigned long long VI_EMPTY = ~0ull;  // a NaN payload arithmetic does not produce
 
 __device__ __forceinline__ unsigned vi_hash(unsigned long long k) {
@@ -1550,22 +1555,57 @@ __device__ __forceinline__ unsigned vi_hash(unsigned long long k) {
   return (unsigned)k;
 }
 
-// pass 1: thread = (owned node, block nb); ctl[0] = distinct values, ctl[1] = overflow
+// index of slot S in a node's chunks: NIB 8 = byte S of 16 x 16 B, NIB 4 = nibble S of 8 x 16 B
+template <int NIB>
+__device__ __forceinline__ unsigned vi_index(const u32x4* w, int S) {
+  if constexpr (NIB == 8) return (w[S >> 4][(S >> 2) & 3] >> (8 * (S & 3))) & 255u;
+  else return (w[S >> 5][(S >> 3) & 3] >> (4 * (S & 7))) & 15u;
+}
+// dictionary entry of that index: one shared table (8) or the slot's own 16 entries (4)
+template <int NIB>
+__device__ __forceinline__ int vi_entry(int S, unsigned id) {
+  return NIB == 8 ? (int)id : S * 16 + (int)id;
+}
+template <int NIB>
+constexpr int vi_chunks() { return NIB == 8 ? 16 : 8; }
+
+// insert key into an open-addressing set of SIZE entries; returns true when it was new, probe
+// budget exhausted = *full
+template <int SIZE>
+__device__ __forceinline__ bool vi_insert(unsigned long long* set, unsigned long long key, bool* full) {
+  unsigned h = vi_hash(key) & (SIZE - 1);
+  for (int probe = 0; probe < SIZE; probe++) {
+    const unsigned long long cur = __hip_atomic_load(&set[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == key) return false;
+    if (cur == VI_EMPTY) {
+      const unsigned long long old = atomicCAS(&set[h], VI_EMPTY, key);
+      if (old == VI_EMPTY) return true;
+      if (old == key) return false;
+    }
+    h = (h + 1) & (SIZE - 1);
+  }
+  *full = true;
+  return false;
+}
+
+// pass 1: thread = (owned node, block nb), block = 256 nodes x one nb (9 slots).  ctl[0] =
+// distinct values, ctl[1] = more than VI_MAX (no value-indexed storage), ctl[2] = some slot has
+// more than 16 (no nibble indices), ctl[3 + S] = distinct values of slot S; skeys[S][32] = the
+// slot's set, keys[VI_HASH] = the whole matrix's
 template <bool TABLE>
 __global__ __launch_bounds__(TPB) void k_vi_collect(Geo g, Material mat, const double* __restrict__ Ke,
-                                                    unsigned long long* __restrict__ keys, unsigned* __restrict__ ctl) {
-  constexpr int LS = 1024;  // block set: at most VI_MAX + 1 keys are ever inserted
-  __shared__ unsigned long long s_keys[LS];
-  __shared__ unsigned s_cnt, s_over;
-  for (int t = threadIdx.x; t < LS; t += TPB) s_keys[t] = VI_EMPTY;
-  if (threadIdx.x == 0) {
-    s_cnt = 0;
-    s_over = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
+                                                    unsigned long long* __restrict__ keys,
+                                                    unsigned long long* __restrict__ skeys, unsigned* __restrict__ ctl) {
+  constexpr int LS = 64;  // per-slot block set (a slot takes <= 16 values, else nibbles are out)
+  __shared__ unsigned long long s_keys[9][LS];
+  __shared__ unsigned s_over;
+  for (int t = threadIdx.x; t < 9 * LS; t += TPB) (&s_keys[0][0])[t] = VI_EMPTY;
+  if (threadIdx.x == 0) s_over = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   if (s_over) return;  // uniform: the dictionary already overflowed
   const int n = blockIdx.x * TPB + threadIdx.x;
   const int nb = blockIdx.y;
+  bool full = false;
   if (n < g.nown) {
     int i, j, k;
     node_ijk(g, n, i, j, k);
@@ -1574,60 +1614,42 @@ __global__ __launch_bounds__(TPB) void k_vi_collect(Geo g, Material mat, const d
 #pragma unroll
     for (int q = 0; q < 9; q++) {
       const unsigned long long key = (unsigned long long)__double_as_longlong(val[q]);
-      if (key == VI_EMPTY) s_over = 1;
-      if (s_over) break;
-      unsigned h = vi_hash(key) & (LS - 1);
-      for (int probe = 0; probe < LS; probe++) {
-        const unsigned long long cur = s_keys[h];
-        if (cur == key) break;
-        if (cur == VI_EMPTY) {
-          const unsigned long long old = atomicCAS(&s_keys[h], VI_EMPTY, key);
-          if (old == VI_EMPTY) {
-            if (atomicAdd(&s_cnt, 1u) >= (unsigned)VI_MAX) s_over = 1;
-            break;
-          }
-          if (old == key) break;
-        }
-        h = (h + 1) & (LS - 1);
-      }
+      if (key == VI_EMPTY) full = true;
+      else vi_insert<LS>(s_keys[q], key, &full);
     }
   }
+  if (full) s_over = 1;
   __syncthreads();
   if (s_over) {
     if (threadIdx.x == 0) atomicOr(&ctl[1], 1u);
     return;
   }
-  for (int t = threadIdx.x; t < LS; t += TPB) {
-    const unsigned long long key = s_keys[t];
+  for (int t = threadIdx.x; t < 9 * LS; t += TPB) {
+    const int q = t / LS;
+    const unsigned long long key = s_keys[q][t % LS];
     if (key == VI_EMPTY) continue;
-    unsigned h = vi_hash(key) & (VI_HASH - 1);
-    int probe = 0;
-    for (; probe < VI_HASH; probe++) {
-      const unsigned long long cur = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (cur == key) break;
-      if (cur == VI_EMPTY) {
-        const unsigned long long old = atomicCAS(&keys[h], VI_EMPTY, key);
-        if (old == VI_EMPTY) {
-          if (atomicAdd(&ctl[0], 1u) >= (unsigned)VI_MAX) atomicOr(&ctl[1], 1u);
-          break;
-        }
-        if (old == key) break;
-      }
-      h = (h + 1) & (VI_HASH - 1);
-    }
-    if (probe == VI_HASH) atomicOr(&ctl[1], 1u);
+    bool gfull = false;
+    if (vi_insert<VI_HASH>(keys, key, &gfull) && atomicAdd(&ctl[0], 1u) >= (unsigned)VI_MAX) atomicOr(&ctl[1], 1u);
+    if (gfull) atomicOr(&ctl[1], 1u);
+    const int S = nb * 9 + q;
+    if (__hip_atomic_load(&ctl[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) continue;
+    bool sfull = false;
+    if (vi_insert<32>(skeys + S * 32, key, &sfull) && atomicAdd(&ctl[3 + S], 1u) >= 16u) atomicOr(&ctl[2], 1u);
+    if (sfull) atomicOr(&ctl[2], 1u);
   }
 }
 
-// pass 2: thread = owned node; its 27 blocks in slot order S = nb*9 + r*3 + c, each value's
-// dictionary index (set staged in LDS) packed into 16-B chunks [n/64][S/16][n%64]
-template <bool TABLE>
+// pass 2: thread = owned node; its 27 blocks in slot order, each value's index (the sets and
+// their index maps staged in LDS) packed into 16-B chunks [n/64][chunk][n%64]
+template <bool TABLE, int NIB>
 __global__ __launch_bounds__(TPB) void k_vi_pack(Geo g, Material mat, const double* __restrict__ Ke,
                                                  const unsigned long long* __restrict__ keys,
                                                  const unsigned char* __restrict__ slot, u32x4* __restrict__ I) {
-  __shared__ unsigned long long s_keys[VI_HASH];
-  __shared__ unsigned char s_slot[VI_HASH];
-  for (int t = threadIdx.x; t < VI_HASH; t += TPB) {
+  constexpr int NK = NIB == 8 ? VI_HASH : NSLOT * 32;  // one set, or 32 entries per slot
+  constexpr int CH = vi_chunks<NIB>(), PER = 128 / NIB;  // chunks per node, indices per chunk
+  __shared__ unsigned long long s_keys[NK];
+  __shared__ unsigned char s_slot[NK];
+  for (int t = threadIdx.x; t < NK; t += TPB) {
     s_keys[t] = keys[t];
     s_slot[t] = slot[t];
   }
@@ -1636,7 +1658,7 @@ __global__ __launch_bounds__(TPB) void k_vi_pack(Geo g, Material mat, const doub
   if (n >= g.nown) return;
   int i, j, k;
   node_ijk(g, n, i, j, k);
-  u32x4* dst = I + (int64_t)(n >> 6) * (VI_CHUNKS * 64) + (n & 63);
+  u32x4* dst = I + (int64_t)(n >> 6) * (CH * 64) + (n & 63);
   unsigned w0 = 0, w1 = 0, w2 = 0, w3 = 0;
   for (int nb = 0; nb < 27; nb++) {
     double val[9];
@@ -1644,17 +1666,19 @@ __global__ __launch_bounds__(TPB) void k_vi_pack(Geo g, Material mat, const doub
 #pragma unroll
     for (int q = 0; q < 9; q++) {
       const unsigned long long key = (unsigned long long)__double_as_longlong(val[q]);
-      unsigned h = vi_hash(key) & (VI_HASH - 1);
-      for (int probe = 0; probe < VI_HASH && s_keys[h] != key; probe++) h = (h + 1) & (VI_HASH - 1);
-      const unsigned idx = s_slot[h];
-      const int S = nb * 9 + q, b = S & 15, sh = 8 * (b & 3);
-      if ((b >> 2) == 0) w0 |= idx << sh;
-      else if ((b >> 2) == 1) w1 |= idx << sh;
-      else if ((b >> 2) == 2) w2 |= idx << sh;
+      const int S = nb * 9 + q;
+      const int base = NIB == 8 ? 0 : S * 32, size = NIB == 8 ? VI_HASH : 32;
+      unsigned h = vi_hash(key) & (size - 1);
+      for (int probe = 0; probe < size && s_keys[base + h] != key; probe++) h = (h + 1) & (size - 1);
+      const unsigned idx = s_slot[base + h];
+      const int b = S % PER, word = b / (PER / 4), sh = NIB * (b % (PER / 4));
+      if (word == 0) w0 |= idx << sh;
+      else if (word == 1) w1 |= idx << sh;
+      else if (word == 2) w2 |= idx << sh;
       else w3 |= idx << sh;
-      if (b == 15 || S == NSLOT - 1) {  // uniform: chunk complete (the last one padded with zeros)
+      if (b == PER - 1 || S == NSLOT - 1) {  // uniform: chunk complete (the last one padded with zeros)
         u32x4 v = {w0, w1, w2, w3};
-        dst[(S >> 4) * 64] = v;
+        dst[(S / PER) * 64] = v;
         w0 = w1 = w2 = w3 = 0;
       }
     }
@@ -1662,35 +1686,41 @@ __global__ __launch_bounds__(TPB) void k_vi_pack(Geo g, Material mat, const doub
 }
 
 // PCSetUp_Jacobi on FMT_VI
-__global__ void k_jacobi_vi(Geo g, const unsigned char* __restrict__ I, const double* __restrict__ dict,
+template <int NIB>
+__global__ void k_jacobi_vi(Geo g, const u32x4* __restrict__ I, const double* __restrict__ dict,
                             double* __restrict__ dinv) {
+  constexpr int CH = vi_chunks<NIB>();
   const int n = blockIdx.x * TPB + threadIdx.x;
   if (n >= g.nown) return;
-  const unsigned char* ib = I + ((int64_t)(n >> 6) * (VI_CHUNKS * 64) + (n & 63)) * 16;
+  u32x4 w[CH];
+  const u32x4* ip = I + (int64_t)(n >> 6) * (CH * 64) + (n & 63);
+#pragma unroll
+  for (int q = 0; q < CH; q++) w[q] = ip[q * 64];
 #pragma unroll
   for (int r = 0; r < 3; r++) {
     const int S = 13 * 9 + r * 4;
-    double d = dict[ib[(S >> 4) * 64 * 16 + (S & 15)]];
+    double d = dict[vi_entry<NIB>(S, vi_index<NIB>(w, S))];
     if (d != 0.0) d = 1.0 / d;
     if (d == 0.0) d = 1.0;
     dinv[3 * n + r] = d;
   }
 }
 
-// y = A x on FMT_VI: k_spmv with the 122 16-B value pairs replaced by 16 16-B index chunks (256 B
-// per node) and the values read from the dictionary in LDS (interior lanes of a wave share an
+// y = A x on FMT_VI, x gathered: k_spmv with the 122 16-B value pairs replaced by 16 (8) 16-B
+// index chunks and the values read from the dictionary in LDS (interior lanes of a wave share an
 // index: LDS broadcast).  Same node sweep (XCD slabs), same slot order and products as k_spmv, so
-// y is bit-identical to the CPU AIJ product.
-template <bool DOT, bool GATED>
+// y is bit-identical to the CPU AIJ product.  DBG (timing-only diagnostics, wrong products):
+// bit 0 = no dictionary lookups (the index is the value), bit 1 = no x gathers.
+template <bool DOT, bool GATED, int NIB, int DBG = 0>
 __global__ __launch_bounds__(TPB) void k_spmv_vi(Geo g, const u32x4* __restrict__ I, const double* __restrict__ dict,
                                                  const double* __restrict__ x, double* __restrict__ y,
                                                  double* __restrict__ part, const CgState* __restrict__ cg,
                                                  SpmvTiling tl) {
-  static_assert(TPB == VI_MAX, "one dictionary entry per thread");
-  __shared__ double tab[VI_MAX];
+  constexpr int CH = vi_chunks<NIB>(), NT = NIB == 8 ? VI_MAX : NSLOT * 16;
+  __shared__ double tab[NT];
   __shared__ double sh[TPB / 64];
   if (GATED && cg->reason) return;
-  tab[threadIdx.x] = dict[threadIdx.x];
+  for (int t = threadIdx.x; t < NT; t += TPB) tab[t] = dict[t];
   __syncthreads();
   int i = 0, j = 0, k = 0;
   const int n = spmv_node(g, tl.TX, tl.LPB, tl.nxc, tl.jgroups, tl.subl, i, j, k);
@@ -1698,16 +1728,25 @@ __global__ __launch_bounds__(TPB) void k_spmv_vi(Geo g, const u32x4* __restrict_
   if (n >= 0) {
     const int PX = g.PX, PXY = g.PX * g.PY;
     const int pc = (i + 1) + (j + 1) * PX + (k + 1) * PXY;
-    const u32x4* ip = I + (int64_t)(n >> 6) * (VI_CHUNKS * 64) + (n & 63);
-    u32x4 w[VI_CHUNKS];
+    const u32x4* ip = I + (int64_t)(n >> 6) * (CH * 64) + (n & 63);
+    u32x4 w[CH];
 #pragma unroll
-    for (int q = 0; q < VI_CHUNKS; q++) w[q] = __builtin_nontemporal_load(ip + q * 64);
+    for (int q = 0; q < CH; q++) w[q] = __builtin_nontemporal_load(ip + q * 64);
     double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
 #pragma unroll
     for (int nb = 0; nb < 27; nb++) {
       const int off = (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
       const double* xp = x + 3 * (int64_t)(pc + off);
-      const double xv[3] = {xp[0], xp[1], xp[2]};
+      double xv[3];
+      if (DBG & 2) {
+        xv[0] = (double)(pc + off);
+        xv[1] = xv[0] + 0.5;
+        xv[2] = xv[0] + 0.25;
+      } else {
+        xv[0] = xp[0];
+        xv[1] = xp[1];
+        xv[2] = xp[2];
+      }
       if (nb == 13) {
         xc0 = xv[0];
         xc1 = xv[1];
@@ -1716,7 +1755,8 @@ __global__ __launch_bounds__(TPB) void k_spmv_vi(Geo g, const u32x4* __restrict_
 #pragma unroll
       for (int q = 0; q < 9; q++) {
         const int S = nb * 9 + q, r = q / 3, cc = q % 3;
-        const double v = tab[(w[S >> 4][(S >> 2) & 3] >> (8 * (S & 3))) & 255u];
+        const unsigned id = vi_index<NIB>(w, S);
+        const double v = (DBG & 1) ? (double)id : tab[vi_entry<NIB>(S, id)];
         if (r == 0) y0 += v * xv[cc];
         else if (r == 1) y1 += v * xv[cc];
         else y2 += v * xv[cc];
@@ -1729,6 +1769,413 @@ __global__ __launch_bounds__(TPB) void k_spmv_vi(Geo g, const u32x4* __restrict_
   }
   if (DOT) {
     double s = block_sum<TPB>(dot, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+  }
+}
+
+// ---- block-indexed: one byte per 3x3 block.  A block position nb takes at most 21 distinct
+// blocks (the diagonal; <= 11 elsewhere; 187 in all at 12^3 .. 40^3), so each node's 27 blocks
+// are held as 27 bytes (+5 pad: 32 B per node) indexing one dictionary of blocks (<= 256 x 9
+// values).  A block's key is its position and its 9 per-slot nibbles (nb << 36 | nibbles), so
+// it is exact; built from the nibble dictionaries by two more passes (k_vib_collect, k_vib_pack).
+// per-slot nibble of value key in slot S (sets staged in LDS: 32 entries per slot)
+__device__ __forceinline__ unsigned vi_nibble(const unsigned long long* skeys, const unsigned char* smap, int S,
+                                              unsigned long long key) {
+  unsigned h = vi_hash(key) & 31u;
+  for (int probe = 0; probe < 32 && skeys[S * 32 + h] != key; probe++) h = (h + 1) & 31u;
+  return smap[S * 32 + h];
+}
+
+// pass 3: thread = (owned node, nb): the block's key into a per-block LDS set, then the global
+// block set bkeys[VI_HASH]; ctl[0] = distinct blocks, ctl[1] = more than VI_MAX
+template <bool TABLE>
+__global__ __launch_bounds__(TPB) void k_vib_collect(Geo g, Material mat, const double* __restrict__ Ke,
+                                                     const unsigned long long* __restrict__ skeys,
+                                                     const unsigned char* __restrict__ smap,
+                                                     unsigned long long* __restrict__ bkeys, unsigned* __restrict__ ctl) {
+  constexpr int LS = 64;
+  __shared__ unsigned long long s_set[LS];
+  __shared__ unsigned long long s_keys[9 * 32];
+  __shared__ unsigned char s_map[9 * 32];
+  __shared__ unsigned s_over;
+  const int nb = blockIdx.y;
+  for (int t = threadIdx.x; t < 9 * 32; t += TPB) {
+    s_keys[t] = skeys[nb * 9 * 32 + t];
+    s_map[t] = smap[nb * 9 * 32 + t];
+  }
+  for (int t = threadIdx.x; t < LS; t += TPB) s_set[t] = VI_EMPTY;
+  if (threadIdx.x == 0) s_over = 0;
+  __syncthreads();
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  bool full = false;
+  if (n < g.nown) {
+    int i, j, k;
+    node_ijk(g, n, i, j, k);
+    double val[9];
+    matrix_block<TABLE>(g, mat, Ke, g.xs + i, g.ys + j, g.zs + k, nb % 3 - 1, (nb / 3) % 3 - 1, nb / 9 - 1, val);
+    unsigned long long key = (unsigned long long)nb << 36;
+#pragma unroll
+    for (int q = 0; q < 9; q++)
+      key |= (unsigned long long)vi_nibble(s_keys, s_map, q, (unsigned long long)__double_as_longlong(val[q]))
+             << (4 * q);
+    vi_insert<LS>(s_set, key, &full);
+  }
+  if (full) s_over = 1;
+  __syncthreads();
+  if (s_over) {
+    if (threadIdx.x == 0) atomicOr(&ctl[1], 1u);
+    return;
+  }
+  for (int t = threadIdx.x; t < LS; t += TPB) {
+    const unsigned long long key = s_set[t];
+    if (key == VI_EMPTY) continue;
+    bool gfull = false;
+    if (vi_insert<VI_HASH>(bkeys, key, &gfull) && atomicAdd(&ctl[0], 1u) >= (unsigned)VI_MAX) atomicOr(&ctl[1], 1u);
+    if (gfull) atomicOr(&ctl[1], 1u);
+  }
+}
+
+// pass 4: thread = (owned node, nb): the block's byte index, byte nb of the node's 32
+// ([n/64][2][64] x 16 B)
+template <bool TABLE>
+__global__ __launch_bounds__(TPB) void k_vib_pack(Geo g, Material mat, const double* __restrict__ Ke,
+                                                  const unsigned long long* __restrict__ skeys,
+                                                  const unsigned char* __restrict__ smap,
+                                                  const unsigned long long* __restrict__ bkeys,
+                                                  const unsigned char* __restrict__ bmap, unsigned char* __restrict__ I) {
+  __shared__ unsigned long long s_keys[9 * 32];
+  __shared__ unsigned char s_map[9 * 32];
+  __shared__ unsigned long long s_bkeys[VI_HASH];
+  __shared__ unsigned char s_bmap[VI_HASH];
+  const int nb = blockIdx.y;
+  for (int t = threadIdx.x; t < 9 * 32; t += TPB) {
+    s_keys[t] = skeys[nb * 9 * 32 + t];
+    s_map[t] = smap[nb * 9 * 32 + t];
+  }
+  for (int t = threadIdx.x; t < VI_HASH; t += TPB) {
+    s_bkeys[t] = bkeys[t];
+    s_bmap[t] = bmap[t];
+  }
+  __syncthreads();
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  double val[9];
+  matrix_block<TABLE>(g, mat, Ke, g.xs + i, g.ys + j, g.zs + k, nb % 3 - 1, (nb / 3) % 3 - 1, nb / 9 - 1, val);
+  unsigned long long key = (unsigned long long)nb << 36;
+#pragma unroll
+  for (int q = 0; q < 9; q++)
+    key |= (unsigned long long)vi_nibble(s_keys, s_map, q, (unsigned long long)__double_as_longlong(val[q])) << (4 * q);
+  unsigned h = vi_hash(key) & (VI_HASH - 1);
+  for (int probe = 0; probe < VI_HASH && s_bkeys[h] != key; probe++) h = (h + 1) & (VI_HASH - 1);
+  I[(((int64_t)(n >> 6) * 2 + (nb >> 4)) * 64 + (n & 63)) * 16 + (nb & 15)] = s_bmap[h];
+}
+
+__global__ void k_jacobi_vib(Geo g, const unsigned char* __restrict__ I, const double* __restrict__ bdict,
+                             double* __restrict__ dinv) {
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  const int id = I[(((int64_t)(n >> 6) * 2 + 0) * 64 + (n & 63)) * 16 + 13];
+#pragma unroll
+  for (int r = 0; r < 3; r++) {
+    double d = bdict[id * VIB_STRIDE + r * 4];
+    if (d != 0.0) d = 1.0 / d;
+    if (d == 0.0) d = 1.0;
+    dinv[3 * n + r] = d;
+  }
+}
+
+// y = A x on block-indexed FMT_VI: 2 16-B index chunks per node (27 block bytes), each block's
+// 9 values from the dictionary in LDS (4 x 16-B + 8-B reads), x gathered.  Same slot order and
+// products as k_spmv: bit-identical to the CPU AIJ product.
+template <bool DOT, bool GATED>
+__global__ __launch_bounds__(TPB) void k_spmv_vib(Geo g, const u32x4* __restrict__ I,
+                                                  const double* __restrict__ bdict, const double* __restrict__ x,
+                                                  double* __restrict__ y, double* __restrict__ part,
+                                                  const CgState* __restrict__ cg, SpmvTiling tl) {
+  __shared__ double2 tab[VI_MAX * VIB_STRIDE / 2];
+  __shared__ double sh[TPB / 64];
+  if (GATED && cg->reason) return;
+  for (int t = threadIdx.x; t < VI_MAX * VIB_STRIDE / 2; t += TPB) tab[t] = reinterpret_cast<const double2*>(bdict)[t];
+  __syncthreads();
+  int i = 0, j = 0, k = 0;
+  const int n = spmv_node(g, tl.TX, tl.LPB, tl.nxc, tl.jgroups, tl.subl, i, j, k);
+  double dot = 0.;
+  if (n >= 0) {
+    const int PX = g.PX, PXY = g.PX * g.PY;
+    const int pc = (i + 1) + (j + 1) * PX + (k + 1) * PXY;
+    const u32x4* ip = I + (int64_t)(n >> 6) * (2 * 64) + (n & 63);
+    const u32x4 w0 = __builtin_nontemporal_load(ip), w1 = __builtin_nontemporal_load(ip + 64);
+    double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+#pragma unroll
+    for (int nb = 0; nb < 27; nb++) {
+      const int off = (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
+      const double* xp = x + 3 * (int64_t)(pc + off);
+      const double xv[3] = {xp[0], xp[1], xp[2]};
+      if (nb == 13) {
+        xc0 = xv[0];
+        xc1 = xv[1];
+        xc2 = xv[2];
+      }
+      const unsigned word = nb < 16 ? w0[nb >> 2] : w1[(nb - 16) >> 2];
+      const unsigned id = (word >> (8 * (nb & 3))) & 255u;
+      const double2* e = tab + id * (VIB_STRIDE / 2);
+      const double2 a01 = e[0], a23 = e[1], a45 = e[2], a67 = e[3], a8 = e[4];
+      const double a[9] = {a01.x, a01.y, a23.x, a23.y, a45.x, a45.y, a67.x, a67.y, a8.x};
+#pragma unroll
+      for (int q = 0; q < 9; q++) {
+        const int r = q / 3, cc = q % 3;
+        if (r == 0) y0 += a[q] * xv[cc];
+        else if (r == 1) y1 += a[q] * xv[cc];
+        else y2 += a[q] * xv[cc];
+      }
+    }
+    __builtin_nontemporal_store(y0, &y[3 * n + 0]);
+    __builtin_nontemporal_store(y1, &y[3 * n + 1]);
+    __builtin_nontemporal_store(y2, &y[3 * n + 2]);
+    if (DOT) dot = xc0 * y0 + xc1 * y1 + xc2 * y2;
+  }
+  if (DOT) {
+    double s = block_sum<TPB>(dot, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+  }
+}
+
+// y = A x on block-indexed FMT_VI with x staged in LDS, z-marching: k_spmv_vim's ring of three x
+// planes (rows j0-1 .. j0+TY, prefetched in registers one plane ahead) with the block dictionary
+// in LDS beside it.  The gathered kernel (k_spmv_vib) spends most of its time in the 81 8-B x
+// loads per node at a 24-B lane stride; here x comes from LDS and HBM streams 32 B of indices
+// per node.  Same slot order and products as k_spmv: bit-identical to the CPU AIJ product.
+template <bool DOT, bool GATED, int TX, int TY>
+__global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __restrict__ I,
+                                                       const double* __restrict__ bdict, const double* __restrict__ x,
+                                                       double* __restrict__ y, double* __restrict__ part,
+                                                       const CgState* __restrict__ cg, ZTiling zt) {
+  constexpr int T = TX * TY, RL = 3 * (TX + 2), PR = TY + 2, PLANE = PR * RL;  // doubles per staged plane
+  constexpr int NL = (PLANE + T - 1) / T;                                      // x loads per thread per plane
+  __shared__ double xs[3][PLANE];
+  __shared__ double2 tab[VI_MAX * VIB_STRIDE / 2];
+  __shared__ double sh[T / 64];
+  if (GATED && cg->reason) return;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, t8 = b >> 3;
+  const int slab = (zt.nty + 7) >> 3;
+  const int ty0 = xcd * slab;
+  const int nty_here = min(slab, zt.nty - ty0);
+  const int per = max(nty_here, 0) * zt.ntx * zt.nzc;
+  if (t8 >= per) {  // whole block idle (uniform): still write the partial
+    if (DOT && threadIdx.x == 0) part[blockIdx.x] = 0.;
+    return;
+  }
+  const int txi = t8 % zt.ntx, r8 = t8 / zt.ntx;  // x tiles fastest, then the slab's tile rows, then z-chunks
+  const int tyi = ty0 + r8 % nty_here, zc = r8 / nty_here;
+  const int i0 = txi * TX, j0 = tyi * TY;
+  const int k0 = zc * zt.kc, k1 = min(g.nz, k0 + zt.kc);
+  const int me = threadIdx.x, lx = me % TX, ly = me / TX;
+  const int i = i0 + lx, j = j0 + ly;
+  const bool inxy = i < g.nx && j < g.ny;
+  const int PX = g.PX, PXY = g.PX * g.PY;
+  const int len = 3 * min(TX + 2, g.nx + 2 - i0);  // doubles of a staged row that exist in the padded box
+  const int rows = min(TY + 2, g.ny + 2 - j0);      // staged rows (j0-1 ..) that exist (padded j <= ny)
+  auto xload = [&](int p, int m) -> double {        // x of node plane p (-1 .. nz), staged element me + m T
+    const int e = me + m * T;
+    const int rr = e / RL, o = e - rr * RL;
+    if (e >= PLANE || o >= len || rr >= rows) return 0.;
+    return x[3 * (int64_t)(i0 + (j0 + rr) * PX + (p + 1) * PXY) + o];
+  };
+  auto xstore = [&](int slot, int m, double v) {
+    const int e = me + m * T;
+    if (e < PLANE) xs[slot][e] = v;
+  };
+  auto iload = [&](int k, u32x4& w0, u32x4& w1) {
+    if (inxy) {
+      const int n = i + g.nx * (j + g.ny * k);
+      const u32x4* ip = I + (int64_t)(n >> 6) * (2 * 64) + (n & 63);
+      w0 = __builtin_nontemporal_load(ip);
+      w1 = __builtin_nontemporal_load(ip + 64);
+    }
+  };
+  for (int t = me; t < VI_MAX * VIB_STRIDE / 2; t += T) tab[t] = reinterpret_cast<const double2*>(bdict)[t];
+#pragma unroll
+  for (int s = 0; s < 3; s++)  // prologue: planes k0-1, k0, k0+1 in ring slots 0, 1, 2
+#pragma unroll
+    for (int m = 0; m < NL; m++) xstore(s, m, xload(k0 - 1 + s, m));
+  u32x4 c0 = {0u, 0u, 0u, 0u}, c1 = c0, n0 = c0, n1 = c0;
+  iload(k0, c0, c1);
+  __syncthreads();
+  double dot = 0.;
+  for (int k = k0; k < k1; k++) {
+    const bool more = k + 1 < k1;
+    double xr[NL];
+    if (more) {  // in flight during this plane: x of plane k+2, indices of plane k+1
+#pragma unroll
+      for (int m = 0; m < NL; m++) xr[m] = xload(k + 2, m);
+      iload(k + 1, n0, n1);
+    }
+    if (inxy) {
+      double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+#pragma unroll
+      for (int nb = 0; nb < 27; nb++) {
+        const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
+        const double* xp = xs[(k + dz - k0 + 1) % 3] + (ly + 1 + dy) * RL + 3 * (lx + 1 + dx);
+        const double xv[3] = {xp[0], xp[1], xp[2]};
+        if (nb == 13) {
+          xc0 = xv[0];
+          xc1 = xv[1];
+          xc2 = xv[2];
+        }
+        const unsigned word = nb < 16 ? c0[nb >> 2] : c1[(nb - 16) >> 2];
+        const unsigned id = (word >> (8 * (nb & 3))) & 255u;
+        const double2* e = tab + id * (VIB_STRIDE / 2);
+        const double2 a01 = e[0], a23 = e[1], a45 = e[2], a67 = e[3], a8 = e[4];
+        const double a[9] = {a01.x, a01.y, a23.x, a23.y, a45.x, a45.y, a67.x, a67.y, a8.x};
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+          const int r = q / 3, cc = q % 3;
+          if (r == 0) y0 += a[q] * xv[cc];
+          else if (r == 1) y1 += a[q] * xv[cc];
+          else y2 += a[q] * xv[cc];
+        }
+      }
+      const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
+      __builtin_nontemporal_store(y0, &y[3 * n + 0]);
+      __builtin_nontemporal_store(y1, &y[3 * n + 1]);
+      __builtin_nontemporal_store(y2, &y[3 * n + 2]);
+      if (DOT) dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
+    }
+    if (more) {  // uniform
+      __syncthreads();  // plane k-1's slot is free
+#pragma unroll
+      for (int m = 0; m < NL; m++) xstore((k + 2 - k0 + 1) % 3, m, xr[m]);
+      c0 = n0;
+      c1 = n1;
+      __syncthreads();
+    }
+  }
+  if (DOT) {
+    double s = block_sum<T>(dot, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+  }
+}
+
+// y = A x on FMT_VI with x staged in LDS, z-marching.  k_spmv_vi's 81 x gathers per node (8 B
+// at a 24-B lane stride: a third of every fetched line used) are a third of its time
+// (profiles/r02_vi_dbg.log: 1.14 ms, 0.78 without them); staging one plane per block and launch
+// was slower still (1.39 ms: one 113-KB block per CU waits on its own staging,
+// profiles/r02_ab_vis_*.log).  Here a 1024-thread block owns a TX x TY node tile and marches it
+// up a z-chunk: LDS holds a ring of three x planes (rows j0-1 .. j0+TY, TX+2 nodes each, as
+// contiguous in the padded box), and while plane k is computed the registers already carry plane
+// k+2's x (coalesced 8-B loads, 1.5 x per owned node at TY = 4) and plane k+1's index chunks,
+// written to the ring after the step's barrier.  Same slot order and products as k_spmv:
+// bit-identical to the CPU AIJ product.
+template <bool DOT, bool GATED, int TX, int TY, int NIB>
+__global__ __launch_bounds__(TX * TY) void k_spmv_vim(Geo g, const u32x4* __restrict__ I,
+                                                      const double* __restrict__ dict, const double* __restrict__ x,
+                                                      double* __restrict__ y, double* __restrict__ part,
+                                                      const CgState* __restrict__ cg, ZTiling zt) {
+  constexpr int T = TX * TY, RL = 3 * (TX + 2), PR = TY + 2, PLANE = PR * RL;  // doubles per staged plane
+  constexpr int NL = (PLANE + T - 1) / T;                                      // x loads per thread per plane
+  constexpr int CH = vi_chunks<NIB>(), NT = NIB == 8 ? VI_MAX : NSLOT * 16;
+  __shared__ double xs[3][PLANE];
+  __shared__ double tab[NT];
+  __shared__ double sh[T / 64];
+  if (GATED && cg->reason) return;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, t8 = b >> 3;
+  const int slab = (zt.nty + 7) >> 3;
+  const int ty0 = xcd * slab;
+  const int nty_here = min(slab, zt.nty - ty0);
+  const int per = max(nty_here, 0) * zt.ntx * zt.nzc;
+  if (t8 >= per) {  // whole block idle (uniform): still write the partial
+    if (DOT && threadIdx.x == 0) part[blockIdx.x] = 0.;
+    return;
+  }
+  const int txi = t8 % zt.ntx, r8 = t8 / zt.ntx;  // x tiles fastest, then the slab's tile rows, then z-chunks
+  const int tyi = ty0 + r8 % nty_here, zc = r8 / nty_here;
+  const int i0 = txi * TX, j0 = tyi * TY;
+  const int k0 = zc * zt.kc, k1 = min(g.nz, k0 + zt.kc);
+  const int me = threadIdx.x, lx = me % TX, ly = me / TX;
+  const int i = i0 + lx, j = j0 + ly;
+  const bool inxy = i < g.nx && j < g.ny;
+  const int PX = g.PX, PXY = g.PX * g.PY;
+  const int len = 3 * min(TX + 2, g.nx + 2 - i0);  // doubles of a staged row that exist in the padded box
+  const int rows = min(TY + 2, g.ny + 2 - j0);      // staged rows (j0-1 ..) that exist (padded j <= ny)
+  // x of node plane p (-1 .. nz): staged element e = rr * RL + o of padded row j0+rr, plane p+1
+  auto xload = [&](int p, int m) -> double {
+    const int e = me + m * T;
+    const int rr = e / RL, o = e - rr * RL;
+    if (e >= PLANE || o >= len || rr >= rows) return 0.;
+    return x[3 * (int64_t)(i0 + (j0 + rr) * PX + (p + 1) * PXY) + o];
+  };
+  auto xstore = [&](int slot, int m, double v) {
+    const int e = me + m * T;
+    if (e < PLANE) xs[slot][e] = v;
+  };
+  auto iload = [&](int k, u32x4 (&w)[CH]) {
+    if (inxy) {
+      const int n = i + g.nx * (j + g.ny * k);
+      const u32x4* ip = I + (int64_t)(n >> 6) * (CH * 64) + (n & 63);
+#pragma unroll
+      for (int q = 0; q < CH; q++) w[q] = __builtin_nontemporal_load(ip + q * 64);
+    }
+  };
+  for (int t = me; t < NT; t += T) tab[t] = dict[t];
+  // prologue: planes k0-1, k0, k0+1 in ring slots 0, 1, 2 (plane p in slot (p - k0 + 1) % 3)
+#pragma unroll
+  for (int s = 0; s < 3; s++)
+#pragma unroll
+    for (int m = 0; m < NL; m++) xstore(s, m, xload(k0 - 1 + s, m));
+  u32x4 cur[CH], nxt[CH];
+  iload(k0, cur);
+  __syncthreads();
+  double dot = 0.;
+  for (int k = k0; k < k1; k++) {
+    const bool more = k + 1 < k1;
+    double xr[NL];
+    if (more) {  // in flight during this plane: x of plane k+2 (the padded ghost plane at most), indices of k+1
+#pragma unroll
+      for (int m = 0; m < NL; m++) xr[m] = xload(k + 2, m);
+      iload(k + 1, nxt);
+    }
+    if (inxy) {
+      double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+#pragma unroll
+      for (int nb = 0; nb < 27; nb++) {
+        const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
+        const double* xp = xs[(k + dz - k0 + 1) % 3] + (ly + 1 + dy) * RL + 3 * (lx + 1 + dx);
+        const double xv[3] = {xp[0], xp[1], xp[2]};
+        if (nb == 13) {
+          xc0 = xv[0];
+          xc1 = xv[1];
+          xc2 = xv[2];
+        }
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+          const int S = nb * 9 + q, r = q / 3, cc = q % 3;
+          const double v = tab[vi_entry<NIB>(S, vi_index<NIB>(cur, S))];
+          if (r == 0) y0 += v * xv[cc];
+          else if (r == 1) y1 += v * xv[cc];
+          else y2 += v * xv[cc];
+        }
+      }
+      const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
+      __builtin_nontemporal_store(y0, &y[3 * n + 0]);
+      __builtin_nontemporal_store(y1, &y[3 * n + 1]);
+      __builtin_nontemporal_store(y2, &y[3 * n + 2]);
+      if (DOT) dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
+    }
+    if (more) {  // uniform
+      __syncthreads();  // plane k-1's slot is free
+#pragma unroll
+      for (int m = 0; m < NL; m++) xstore((k + 2 - k0 + 1) % 3, m, xr[m]);
+#pragma unroll
+      for (int q = 0; q < CH; q++) cur[q] = nxt[q];
+      __syncthreads();
+    }
+  }
+  if (DOT) {
+    double s = block_sum<T>(dot, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = s;
   }
 }
@@ -2270,7 +2717,31 @@ static void split_shape(const Ctx& c, int& ztx, int& zty) {
   if (!built) zty = 4;  // the launcher instantiates only these shapes
 }
 
+// FMT_VI with x staged in LDS (k_spmv_vim): 1024-thread tiles TX x TY marching z-chunks, one
+// resident round of blocks (one per CU: the ring and the dictionaries fill the LDS)
+static void vis_shape(const Ctx& c, int& tx, int& ty) {
+  tx = c.g.nx >= 256 ? 256 : (c.g.nx >= 128 ? 128 : 64);
+  ty = 1024 / tx;
+}
+
+static ZTiling vis_tiling(const Ctx& c) {
+  int tx, ty;
+  vis_shape(c, tx, ty);
+  ZTiling t;
+  t.ntx = (c.g.nx + tx - 1) / tx;
+  t.nty = (c.g.ny + ty - 1) / ty;
+  const int tiles = t.ntx * t.nty, want = c.spmv_zblocks > 0 ? c.spmv_zblocks : c.g.ncu;
+  t.nzc = std::max(1, std::min(c.g.nz, (want + tiles - 1) / tiles));
+  t.kc = (c.g.nz + t.nzc - 1) / t.nzc;
+  t.nzc = (c.g.nz + t.kc - 1) / t.kc;
+  return t;
+}
+
 int64_t spmv_grid_blocks(const Ctx& c) {
+  if (c.fmt == FMT_VI && c.vi_stage && c.vi_bits == 4) {
+    const ZTiling t = vis_tiling(c);
+    return 8 * (int64_t)(((t.nty + 7) / 8) * t.ntx * t.nzc);
+  }
   if (c.fmt == FMT_SPLIT || (c.fmt == FMT_U && c.spmv_kernel >= 1)) {
     int ztx, zty;
     if (c.fmt == FMT_SPLIT) split_shape(c, ztx, zty);
@@ -2420,69 +2891,213 @@ int build_split(Ctx& c, bool* exact) {
 int build_vi(Ctx& c, bool* ok) {
   *ok = false;
   const bool table = table_law(c);
-  MCX_HIP(hipMemsetAsync(c.vi_keys, 0xff, VI_HASH * sizeof(unsigned long long), c.stream));
-  MCX_HIP(hipMemsetAsync(c.vi_ctl, 0, 2 * sizeof(unsigned), c.stream));
+  MCX_HIP(hipMemsetAsync(c.vi_keys, 0xff, (VI_HASH + NSLOT * 32) * sizeof(unsigned long long), c.stream));
+  MCX_HIP(hipMemsetAsync(c.vi_ctl, 0, (3 + NSLOT) * sizeof(unsigned), c.stream));
+  unsigned long long* skeys = c.vi_keys + VI_HASH;
   const dim3 grid(nblk(c.g.nown), 27);
   if (table)
-    hipLaunchKernelGGL(k_vi_collect<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.vi_keys, c.vi_ctl);
+    hipLaunchKernelGGL(k_vi_collect<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.vi_keys, skeys, c.vi_ctl);
   else
-    hipLaunchKernelGGL(k_vi_collect<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.vi_keys, c.vi_ctl);
-  unsigned ctl[2];
-  std::vector<unsigned long long> keys(VI_HASH);
-  MCX_HIP(hipMemcpyAsync(ctl, c.vi_ctl, sizeof(ctl), hipMemcpyDeviceToHost, c.stream));
-  MCX_HIP(hipMemcpyAsync(keys.data(), c.vi_keys, VI_HASH * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+    hipLaunchKernelGGL(k_vi_collect<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.vi_keys, skeys, c.vi_ctl);
+  std::vector<unsigned> ctl(3 + NSLOT);
+  std::vector<unsigned long long> keys(VI_HASH + NSLOT * 32);
+  MCX_HIP(hipMemcpyAsync(ctl.data(), c.vi_ctl, ctl.size() * sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipMemcpyAsync(keys.data(), c.vi_keys, keys.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                          c.stream));
   MCX_HIP(hipStreamSynchronize(c.stream));
   if (ctl[1] || ctl[0] > (unsigned)VI_MAX) return 0;
-  std::vector<unsigned long long> vals;
-  for (unsigned long long k : keys)
-    if (k != VI_EMPTY) vals.push_back(k);
-  std::sort(vals.begin(), vals.end());
-  std::vector<unsigned char> slot(VI_HASH, 0);
-  for (int h = 0; h < VI_HASH; h++)
-    if (keys[h] != VI_EMPTY)
-      slot[h] = (unsigned char)(std::lower_bound(vals.begin(), vals.end(), keys[h]) - vals.begin());
-  std::vector<double> dict(VI_MAX, 0.);
-  for (size_t q = 0; q < vals.size(); q++) std::memcpy(&dict[q], &vals[q], sizeof(double));
-  MCX_HIP(hipMemcpyAsync(c.vi_slot, slot.data(), VI_HASH, hipMemcpyHostToDevice, c.stream));
-  MCX_HIP(hipMemcpyAsync(c.vi_dict, dict.data(), VI_MAX * sizeof(double), hipMemcpyHostToDevice, c.stream));
+  const int bits = (!ctl[2] && c.vi_bits_max == 4) ? 4 : 8;
+  // dictionaries: sorted bit patterns (the whole matrix's, or each slot's), and the index of
+  // every occupied set entry
+  const int nsets = bits == 8 ? 1 : NSLOT, ssize = bits == 8 ? VI_HASH : 32, dsize = bits == 8 ? VI_MAX : 16;
+  const unsigned long long* kk = bits == 8 ? keys.data() : keys.data() + VI_HASH;
+  std::vector<unsigned char> slot(nsets * ssize, 0);
+  std::vector<double> dict(nsets * dsize, 0.);
+  for (int st = 0; st < nsets; st++) {
+    std::vector<unsigned long long> vals;
+    for (int h = 0; h < ssize; h++)
+      if (kk[st * ssize + h] != VI_EMPTY) vals.push_back(kk[st * ssize + h]);
+    std::sort(vals.begin(), vals.end());
+    for (int h = 0; h < ssize; h++)
+      if (kk[st * ssize + h] != VI_EMPTY)
+        slot[st * ssize + h] =
+            (unsigned char)(std::lower_bound(vals.begin(), vals.end(), kk[st * ssize + h]) - vals.begin());
+    for (size_t q = 0; q < vals.size(); q++) std::memcpy(&dict[st * dsize + q], &vals[q], sizeof(double));
+  }
+  MCX_HIP(hipMemcpyAsync(c.vi_slot, slot.data(), slot.size(), hipMemcpyHostToDevice, c.stream));
+  MCX_HIP(hipMemcpyAsync(c.vi_dict, dict.data(), dict.size() * sizeof(double), hipMemcpyHostToDevice, c.stream));
+  c.vi_block = false;
+  if (bits == 4 && c.vi_block_on) {  // one byte per 3x3 block when the blocks are few (k_vib_collect)
+    unsigned long long* bkeys = c.vi_keys + VI_HASH + NSLOT * 32;
+    unsigned char* bmap = c.vi_slot + NSLOT * 32;
+    unsigned* bctl = c.vi_ctl + 3 + NSLOT;
+    MCX_HIP(hipMemsetAsync(bkeys, 0xff, VI_HASH * sizeof(unsigned long long), c.stream));
+    MCX_HIP(hipMemsetAsync(bctl, 0, 2 * sizeof(unsigned), c.stream));
+    if (table)
+      hipLaunchKernelGGL(k_vib_collect<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, skeys, c.vi_slot, bkeys,
+                         bctl);
+    else
+      hipLaunchKernelGGL(k_vib_collect<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, skeys, c.vi_slot, bkeys,
+                         bctl);
+    unsigned bc[2];
+    std::vector<unsigned long long> bk(VI_HASH);
+    MCX_HIP(hipMemcpyAsync(bc, bctl, sizeof(bc), hipMemcpyDeviceToHost, c.stream));
+    MCX_HIP(hipMemcpyAsync(bk.data(), bkeys, VI_HASH * sizeof(unsigned long long), hipMemcpyDeviceToHost, c.stream));
+    MCX_HIP(hipStreamSynchronize(c.stream));
+    if (!bc[1] && bc[0] <= (unsigned)VI_MAX) {
+      std::vector<unsigned long long> bv;
+      for (unsigned long long k : bk)
+        if (k != VI_EMPTY) bv.push_back(k);
+      std::sort(bv.begin(), bv.end());
+      std::vector<unsigned char> bm(VI_HASH, 0);
+      for (int h = 0; h < VI_HASH; h++)
+        if (bk[h] != VI_EMPTY) bm[h] = (unsigned char)(std::lower_bound(bv.begin(), bv.end(), bk[h]) - bv.begin());
+      std::vector<double> bd((size_t)VI_MAX * VIB_STRIDE, 0.);
+      for (size_t b = 0; b < bv.size(); b++) {
+        const int nb = (int)(bv[b] >> 36);
+        for (int q = 0; q < 9; q++) bd[b * VIB_STRIDE + q] = dict[(nb * 9 + q) * 16 + ((bv[b] >> (4 * q)) & 15)];
+      }
+      MCX_HIP(hipMemcpyAsync(bmap, bm.data(), VI_HASH, hipMemcpyHostToDevice, c.stream));
+      MCX_HIP(hipMemcpyAsync(c.vi_bdict, bd.data(), bd.size() * sizeof(double), hipMemcpyHostToDevice, c.stream));
+      if (table)
+        hipLaunchKernelGGL(k_vib_pack<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, skeys, c.vi_slot, bkeys,
+                           bmap, c.vi_idx);
+      else
+        hipLaunchKernelGGL(k_vib_pack<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, skeys, c.vi_slot, bkeys,
+                           bmap, c.vi_idx);
+      MCX_HIP(hipStreamSynchronize(c.stream));
+      c.vi_n = (int)ctl[0];
+      c.vi_bits = 4;
+      c.vi_nblocks = (int)bv.size();
+      c.vi_block = true;
+      *ok = true;
+      return 0;
+    }
+  }
   u32x4* I = reinterpret_cast<u32x4*>(c.vi_idx);
-  if (table)
-    hipLaunchKernelGGL(k_vi_pack<true>, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.vi_keys,
-                       c.vi_slot, I);
+  const dim3 pg(nblk(c.g.nown));
+  if (bits == 8 && table)
+    hipLaunchKernelGGL((k_vi_pack<true, 8>), pg, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.vi_keys, c.vi_slot, I);
+  else if (bits == 8)
+    hipLaunchKernelGGL((k_vi_pack<false, 8>), pg, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.vi_keys, c.vi_slot, I);
+  else if (table)
+    hipLaunchKernelGGL((k_vi_pack<true, 4>), pg, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, skeys, c.vi_slot, I);
   else
-    hipLaunchKernelGGL(k_vi_pack<false>, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.vi_keys,
-                       c.vi_slot, I);
+    hipLaunchKernelGGL((k_vi_pack<false, 4>), pg, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, skeys, c.vi_slot, I);
   // the host copies above must outlive the async uploads
   MCX_HIP(hipStreamSynchronize(c.stream));
-  c.vi_n = (int)vals.size();
+  c.vi_n = (int)ctl[0];
+  c.vi_bits = bits;
   *ok = true;
   return 0;
 }
 
 void launch_jacobi(Ctx& c) {
-  if (c.fmt == FMT_VI)
-    hipLaunchKernelGGL(k_jacobi_vi, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.vi_idx, c.vi_dict, c.dinv);
+  if (c.fmt == FMT_VI && c.vi_block)
+    hipLaunchKernelGGL(k_jacobi_vib, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.vi_idx, c.vi_bdict, c.dinv);
+  else if (c.fmt == FMT_VI && c.vi_bits == 4)
+    hipLaunchKernelGGL(k_jacobi_vi<4>, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g,
+                       reinterpret_cast<const u32x4*>(c.vi_idx), c.vi_dict, c.dinv);
+  else if (c.fmt == FMT_VI)
+    hipLaunchKernelGGL(k_jacobi_vi<8>, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g,
+                       reinterpret_cast<const u32x4*>(c.vi_idx), c.vi_dict, c.dinv);
   else if (c.fmt != FMT_V)
     hipLaunchKernelGGL(k_jacobi_sym, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.U, c.dinv);
   else
     hipLaunchKernelGGL(k_jacobi, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.V, c.dinv);
 }
 
+template <int NIB>
+static void launch_spmv_vi(Ctx& c, const double* xpad, double* y, bool dot, bool gated, int nb, const SpmvTiling& tl) {
+  const u32x4* I = reinterpret_cast<const u32x4*>(c.vi_idx);
+  if (NIB == 4 && c.vi_stage) {  // x staged in LDS, 1024-node tiles marching z-chunks
+    const ZTiling zt = vis_tiling(c);
+    int tx, ty;
+    vis_shape(c, tx, ty);
+#define MCX_VIS(TXV, TYV)                                                                                            \
+  do {                                                                                                              \
+    if (dot && gated)                                                                                               \
+      hipLaunchKernelGGL((k_spmv_vim<true, true, TXV, TYV, NIB>), dim3(nb), dim3(1024), 0, c.stream, c.g, I,         \
+                         c.vi_dict, xpad, y, c.partials, c.cg, zt);                                                 \
+    else if (dot)                                                                                                   \
+      hipLaunchKernelGGL((k_spmv_vim<true, false, TXV, TYV, NIB>), dim3(nb), dim3(1024), 0, c.stream, c.g, I,        \
+                         c.vi_dict, xpad, y, c.partials, c.cg, zt);                                                 \
+    else                                                                                                            \
+      hipLaunchKernelGGL((k_spmv_vim<false, false, TXV, TYV, NIB>), dim3(nb), dim3(1024), 0, c.stream, c.g, I,       \
+                         c.vi_dict, xpad, y, c.partials, c.cg, zt);                                                 \
+  } while (0)
+    if constexpr (NIB == 4) {
+      if (tx == 256) MCX_VIS(256, 4);
+      else if (tx == 128) MCX_VIS(128, 8);
+      else MCX_VIS(64, 16);
+    }
+#undef MCX_VIS
+    return;
+  }
+  if (c.split_dbg) {  // timing-only diagnostics of the gathered kernel (wrong products)
+    if (c.split_dbg == 1)
+      hipLaunchKernelGGL((k_spmv_vi<false, false, NIB, 1>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_dict, xpad,
+                         y, c.partials, c.cg, tl);
+    else if (c.split_dbg == 2)
+      hipLaunchKernelGGL((k_spmv_vi<false, false, NIB, 2>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_dict, xpad,
+                         y, c.partials, c.cg, tl);
+    else
+      hipLaunchKernelGGL((k_spmv_vi<false, false, NIB, 3>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_dict, xpad,
+                         y, c.partials, c.cg, tl);
+    return;
+  }
+  if (dot && gated)
+    hipLaunchKernelGGL((k_spmv_vi<true, true, NIB>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_dict, xpad, y,
+                       c.partials, c.cg, tl);
+  else if (dot)
+    hipLaunchKernelGGL((k_spmv_vi<true, false, NIB>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_dict, xpad, y,
+                       c.partials, c.cg, tl);
+  else
+    hipLaunchKernelGGL((k_spmv_vi<false, false, NIB>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_dict, xpad, y,
+                       c.partials, c.cg, tl);
+}
+
 void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
   const int nb = (int)spmv_grid_blocks(c);
   const SpmvTiling tl = spmv_tiling(c.g, c.spmv_subl);
-  if (c.fmt == FMT_VI) {
+  if (c.fmt == FMT_VI && c.vi_block) {
     const u32x4* I = reinterpret_cast<const u32x4*>(c.vi_idx);
+    if (c.vi_stage) {  // x staged in LDS, 1024-node tiles marching z-chunks
+      const ZTiling zt = vis_tiling(c);
+      int tx, ty;
+      vis_shape(c, tx, ty);
+#define MCX_VIBM(TXV, TYV)                                                                                          \
+  do {                                                                                                             \
+    if (dot && gated)                                                                                              \
+      hipLaunchKernelGGL((k_spmv_vibm<true, true, TXV, TYV>), dim3(nb), dim3(1024), 0, c.stream, c.g, I, c.vi_bdict, \
+                         xpad, y, c.partials, c.cg, zt);                                                           \
+    else if (dot)                                                                                                  \
+      hipLaunchKernelGGL((k_spmv_vibm<true, false, TXV, TYV>), dim3(nb), dim3(1024), 0, c.stream, c.g, I,            \
+                         c.vi_bdict, xpad, y, c.partials, c.cg, zt);                                               \
+    else                                                                                                           \
+      hipLaunchKernelGGL((k_spmv_vibm<false, false, TXV, TYV>), dim3(nb), dim3(1024), 0, c.stream, c.g, I,           \
+                         c.vi_bdict, xpad, y, c.partials, c.cg, zt);                                               \
+  } while (0)
+      if (tx == 256) MCX_VIBM(256, 4);
+      else if (tx == 128) MCX_VIBM(128, 8);
+      else MCX_VIBM(64, 16);
+#undef MCX_VIBM
+      return;
+    }
     if (dot && gated)
-      hipLaunchKernelGGL((k_spmv_vi<true, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_dict, xpad, y,
+      hipLaunchKernelGGL((k_spmv_vib<true, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_bdict, xpad, y,
                          c.partials, c.cg, tl);
     else if (dot)
-      hipLaunchKernelGGL((k_spmv_vi<true, false>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_dict, xpad, y,
+      hipLaunchKernelGGL((k_spmv_vib<true, false>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_bdict, xpad, y,
                          c.partials, c.cg, tl);
     else
-      hipLaunchKernelGGL((k_spmv_vi<false, false>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_dict, xpad, y,
+      hipLaunchKernelGGL((k_spmv_vib<false, false>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_bdict, xpad, y,
                          c.partials, c.cg, tl);
+    return;
+  }
+  if (c.fmt == FMT_VI) {
+    if (c.vi_bits == 4) launch_spmv_vi<4>(c, xpad, y, dot, gated, nb, tl);
+    else launch_spmv_vi<8>(c, xpad, y, dot, gated, nb, tl);  // byte indices: gathered x (the ring spills)
     return;
   }
   if (c.fmt == FMT_SPLIT) {

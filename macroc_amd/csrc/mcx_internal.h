@@ -70,13 +70,15 @@ struct Ctx;
 // the AIJ matrix held exactly as its upper blocks U plus, per owned node, the bf16 correction
 // lower - mirror(upper) of the correction slots that are non-zero somewhere in the matrix
 // (every AIJ value reconstructs bit for bit; rows summed in the z-marching order).
-// FMT_VI: the AIJ matrix held exactly as one byte per value, an index into a dictionary of the
-// matrix's distinct values (at most 256; value-indexed CSR, Kourtis et al. 2008), all 27
-// blocks per node in FMT_V's slot order — every row summed in the CPU AIJ order.
+// FMT_VI: the AIJ matrix held exactly as small indices into dictionaries of its distinct values
+// (value-indexed CSR, Kourtis et al. 2008): a nibble per value into the slot's own dictionary
+// (every slot takes at most 16 values) or a byte per value into one dictionary (at most 256),
+// all 27 blocks per node in FMT_V's slot order — every row summed in the CPU AIJ order.
 enum Fmt { FMT_V = 0, FMT_U = 1, FMT_SPLIT = 2, FMT_VI = 3 };
 constexpr int VI_MAX = 256;     // dictionary entries (one index byte per value)
 constexpr int VI_HASH = 4096;   // open-addressing set of the distinct values (bit patterns)
 constexpr int VI_CHUNKS = 16;   // 16-B index chunks per node: 243 slots + 13 zero pad bytes
+constexpr int VIB_STRIDE = 10;  // doubles per dictionary block (9 values + pad: 16-B aligned)
 
 // AIJ-split correction slots, passed by value: slot = nb*9 + r*3 + c of the row node's lower
 // block nb < 13 holds A(n, nb)[r][c] - U(m, 26-nb)[c][r], m = n + off(nb); nb = 13 (the
@@ -143,11 +145,19 @@ struct Ctx {
   // (VI_MAX doubles, ascending bit pattern), the build's value set and its slot -> index map
   unsigned char* vi_idx = nullptr;
   double* vi_dict = nullptr;
-  unsigned long long* vi_keys = nullptr;  // [VI_HASH]
-  unsigned char* vi_slot = nullptr;       // [VI_HASH]
-  unsigned* vi_ctl = nullptr;             // [0] distinct values, [1] overflow
-  int vi_n = 0;                           // dictionary entries of the current matrix
+  unsigned long long* vi_keys = nullptr;  // [VI_HASH] the value set, [NSLOT][32] the slots' sets, [VI_HASH] the block set
+  unsigned char* vi_slot = nullptr;       // index of every set entry ([VI_HASH] or [NSLOT][32]), then the blocks'
+  unsigned* vi_ctl = nullptr;             // [0] distinct values, [1] > VI_MAX, [2] a slot > 16, [3 + S] per slot, blocks'
+                                          // [3 + NSLOT] count, [4 + NSLOT] > VI_MAX
+  int vi_n = 0;                           // distinct values of the current matrix
+  int vi_bits = 8;                        // 4: per-slot nibble indices, 8: one byte per value
+  int vi_bits_max = 4;                    // option vi_bits: 8 = never use nibble indices
+  bool vi_block = false;                  // one byte per 3x3 block into a dictionary of blocks (k_spmv_vib)
+  int vi_block_on = 1;                    // option vi_block: try the block dictionary (needs nibbles)
+  int vi_nblocks = 0;                     // distinct blocks of the current matrix (block mode)
+  double* vi_bdict = nullptr;             // [VI_MAX][VIB_STRIDE] dictionary blocks
   int aij_vi = 1;            // aij: assemble in FMT_VI when the matrix has at most VI_MAX distinct values
+  int vi_stage = 1;          // FMT_VI SpMV: 1 = x staged in LDS per tile (k_spmv_vis), 0 = gathered (k_spmv_vi)
   bool vi_declined = false;  // a per-GP-tangent law overflowed the dictionary: skip the attempt
   int fmt = FMT_V;           // storage the matrix is currently assembled in
   bool assembled = false;    // a matrix has been assembled (mcx_assembly_jac)

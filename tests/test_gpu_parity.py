@@ -114,6 +114,25 @@ def test_aij_vi_single_rank(name):
         y = m.spmv(x)
         assert np.array_equal(y, P.spmv(x))
         assert np.array_equal(m.spmv(x), y)
+        # every slot takes <= 16 values and every block position few blocks: one byte per 3x3 block
+        assert info["vi_bits"] == 4 and 0 < info["vi_blocks"] <= 256
+        m.set_option("vi_block", 0)  # per-slot nibble indices: the same matrix and products
+        m.assembly_jac()
+        assert m.get_info()["vi_blocks"] == 0 and np.array_equal(m.dump_csr()[2], v)
+        assert np.array_equal(m.spmv(x), y)
+        m.set_option("vi_stage", 0)  # x gathered instead of staged in LDS: the same products
+        assert np.array_equal(m.spmv(x), y)
+        m.set_option("vi_stage", 1)
+        m.set_option("spmv_zblocks", 1)  # one z-chunk per tile: the staged ring marches every plane
+        assert np.array_equal(m.spmv(x), y)
+        m.set_option("spmv_zblocks", 0)
+        m.set_option("vi_bits", 8)  # one byte per value into one dictionary: the same matrix and products
+        m.assembly_jac()
+        assert m.get_info()["vi_bits"] == 8 and np.array_equal(m.dump_csr()[2], v)
+        assert np.array_equal(m.spmv(x), y)
+        m.set_option("vi_bits", 4)
+        m.set_option("vi_block", 1)
+        m.assembly_jac()
         its, rn, reason = m.solve_Ax()
         assert abs(its - int(fx["its"])) <= 1
         ref = fx["du"]

@@ -19,6 +19,8 @@ ap.add_argument("--grid", default="256", help="N or NX,NY,NZ")
 ap.add_argument("--mat", default="aij", choices=["aij", "sbaij"])
 ap.add_argument("--split", type=int, default=1, help="aij: -mat_aij_split")
 ap.add_argument("--vi", type=int, default=1, help="aij: -mat_aij_vi")
+ap.add_argument("--vi-bits", type=int, default=4, help="aij value-indexed: 4 (per-slot nibbles) or 8 (bytes)")
+ap.add_argument("--vi-block", type=int, default=1, help="aij value-indexed: 1 = one byte per 3x3 block when possible")
 ap.add_argument("--variants", default="split_tx=0", help="';'-separated option sets 'name=value,name=value'")
 ap.add_argument("--base", default="split_tx=0,spmv_zblocks=0", help="options every variant starts from")
 ap.add_argument("--rounds", type=int, default=5)
@@ -37,6 +39,9 @@ g = [int(v) for v in a.grid.split(",")]
 NX, NY, NZ = g if len(g) == 3 else g * 3
 m = M.Macroc(["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-dm_mat_type", a.mat, "-mat_aij_split", a.split,
               "-mat_aij_vi", a.vi])
+if a.mat == "aij" and a.vi:
+    m.set_option("vi_bits", a.vi_bits)
+    m.set_option("vi_block", a.vi_block)
 m.apply_bc_on_u(m.get_displacement(1))
 m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
 base = parse(a.base)
