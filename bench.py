@@ -50,7 +50,15 @@ STORAGE_NAME = {0: "aij-blocks", 1: "sbaij", 2: "aij-split", 3: "aij-vi"}
 KERNEL_NAME = {0: "k_spmv (AIJ stencil blocks, CPU AIJ row order)",
                1: "k_spmv_symp (SBAIJ phased z-marching tiles)",
                2: "k_spmv_symp<AIJS> (AIJ-split: upper blocks + bf16 lower corrections, z-marching)",
-               3: "k_spmv_vi (value-indexed AIJ: index bytes + dictionary in LDS, CPU AIJ row order)"}
+               3: "k_spmv_vi (value-indexed AIJ: index bytes + dictionary in LDS, CPU AIJ row order)",
+               # value-indexed, one byte per 3x3 block (vi_blocks > 0): z-marching x ring in LDS
+               # where a tile marches >= 4 planes (k_spmv_vibm), else x gathered (k_spmv_vib)
+               "3b": "k_spmv_vibm (block-indexed AIJ: one byte per 3x3 block, block dictionary + x ring in "
+                     "LDS, CPU AIJ row order)"}
+
+
+def kernel_name(r):
+    return KERNEL_NAME["3b" if r["storage_id"] == 3 and r["vi_blocks"] else r["storage_id"]]
 
 
 def log(*a):
@@ -305,7 +313,7 @@ def main():
         vr = measure(argv + STORAGE_ARGS[v], rank, world, new_comm_id(), args, 1, 1)
         variants.append({
             "mat_type": v, "value": ndofs / (vr["ms_step"] * 1e-3), "ms_per_step": vr["ms_step"], "steps": 1,
-            "warmup": 1, "storage": vr["storage"], "kernel": KERNEL_NAME[vr["storage_id"]], "cg_its": vr["its"],
+            "warmup": 1, "storage": vr["storage"], "kernel": kernel_name(vr), "cg_its": vr["its"],
             "ms_per_cg_iter": vr["tm"]["solve_ms"] / max(vr["its"], 1), "spmv_avg_ms": vr["spmv_avg_ms"],
             "spmv_bytes_per_launch": vr["spmv_bytes"], "spmv_achieved_GBs": vr["achieved"],
             "spmv_frac": vr["achieved"] / PEAK_HBM_GBS, "spmv_traffic": pmc_traffic(vr["storage"], NX, NY, NZ),
@@ -351,7 +359,7 @@ def main():
             "device_gb": info["device_bytes"] / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": pmc_traffic(r["storage"], NX, NY, NZ),
-                         "kernel": KERNEL_NAME[r["storage_id"]], "bytes_per_launch": spmv_bytes,
+                         "kernel": kernel_name(r), "bytes_per_launch": spmv_bytes,
                          "avg_launch_ms": spmv_avg_ms, "launches_timed": tm["spmv_launches"],
                          # the same launch priced at PETSc AIJ bytes (what the reference's MatMult streams)
                          "csr_bytes_per_launch": r["csr_bytes"], "csr_achieved": csr_achieved,

@@ -144,7 +144,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   if ((rc = dalloc(c, &c.u_pad, npad)) || (rc = dalloc(c, &c.p_pad, npad)) || (rc = dalloc(c, &c.b, nown3)) ||
       (rc = dalloc(c, &c.du, nown3)) || (rc = dalloc(c, &c.r, nown3)) || (rc = dalloc(c, &c.z, nown3)) ||
       (rc = dalloc(c, &c.w, nown3)) || (rc = dalloc(c, &c.dinv, nown3)) || (rc = dalloc(c, &c.tmp, nown3)) ||
-      ((c.o.mat_type == MCX_MAT_SBAIJ || c.aij_split) && (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))) ||
+      (c.o.mat_type == MCX_MAT_SBAIJ && (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))) ||
       (c.o.mat_type == MCX_MAT_AIJ && !c.aij_split && (rc = dalloc(c, &c.V, c.ngroups * NPAIR * 128))) ||
       (rc = dalloc(c, &c.eps, 6 * 8 * E)) || (rc = dalloc(c, &c.sig, 6 * 8 * E)) ||
       (rc = dalloc(c, &c.partials, c.partials_cap = 4 * std::max(max_spmv_blocks(c), node_blocks(c)) + 64)) ||
@@ -758,9 +758,8 @@ static int ensure_V(Ctx& c) {
 
 // the value-indexed storage, allocated on first use
 static int ensure_VI(Ctx& c) {
-  if (c.vi_idx) return 0;
-  const int64_t idx_bytes = c.ngroups * VI_CHUNKS * 64 * 16;
-  MCX_HIP(hipMalloc(&c.vi_idx, idx_bytes));
+  if (c.vi_dict) return 0;
+  const int64_t idx_bytes = 0;  // the index array is sized by build_vi to the mode it picks
   const int64_t nd = std::max(VI_MAX, NSLOT * 16), nk = 2 * VI_HASH + NSLOT * 32;
   MCX_HIP(hipMalloc(&c.vi_dict, nd * sizeof(double)));
   MCX_HIP(hipMalloc(&c.vi_bdict, VI_MAX * VIB_STRIDE * sizeof(double)));
@@ -794,6 +793,7 @@ int mcx_assembly_jac(void* ctx) {
     launch_gather_matrix_sym(c);
     c.fmt = FMT_U;
   } else if (c.aij_split && !c.split_declined) {
+    if (!c.U && (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))) return rc;  // first AIJ-split assembly
     launch_gather_matrix_sym(c);
     bool exact = false;
     if ((rc = build_split(c, &exact))) return rc;
@@ -1116,7 +1116,7 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
   std::vector<unsigned char> Ih;
   std::vector<double> dict;
   if (vals && c.fmt == FMT_VI) {
-    Ih.resize((size_t)c.ngroups * VI_CHUNKS * 64 * 16);
+    Ih.resize((size_t)c.vi_idx_bytes);
     dict.resize(c.vi_block ? VI_MAX * VIB_STRIDE : std::max(VI_MAX, NSLOT * 16));
     MCX_HIP(hipMemcpyAsync(Ih.data(), c.vi_idx, Ih.size(), hipMemcpyDeviceToHost, c.stream));
     MCX_HIP(hipMemcpyAsync(dict.data(), c.vi_block ? c.vi_bdict : c.vi_dict, dict.size() * sizeof(double),
@@ -1374,7 +1374,7 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     return 0;
   }
   if (!std::strcmp(name, "vi_stage")) {
-    c.vi_stage = value != 0.;
+    c.vi_stage = value < 0. ? -1 : (value != 0. ? 1 : 0);
     if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
       set_error("vi_stage: partials buffer too small");
       return 2;
@@ -1392,7 +1392,7 @@ int mcx_set_option(void* ctx, const char* name, double value) {
   }
   if (!std::strcmp(name, "aij_split")) {  // takes effect at the next mcx_assembly_jac
     c.split_declined = false;
-    if (value != 0. && (!c.U || !c.d_mask)) {
+    if (value != 0. && !c.d_mask) {
       set_error("aij_split: context created with -mat_aij_split 0 (no split storage)");
       return 2;
     }

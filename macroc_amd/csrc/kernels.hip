@@ -2737,8 +2737,16 @@ static ZTiling vis_tiling(const Ctx& c) {
   return t;
 }
 
+// staged (z-marching) value-indexed SpMV: forced by option vi_stage 0 / 1, else where a block
+// marches at least 4 planes (256^3: 0.49 vs 0.66 ms gathered, 128^3 0.073 vs 0.090; 64^3, one
+// plane per block: 0.024 vs 0.012; profiles/r02_vibm_ab*.log)
+bool vi_staged(const Ctx& c) {
+  if (c.vi_stage >= 0) return c.vi_stage != 0;
+  return vis_tiling(c).kc >= 4;
+}
+
 int64_t spmv_grid_blocks(const Ctx& c) {
-  if (c.fmt == FMT_VI && c.vi_stage && c.vi_bits == 4) {
+  if (c.fmt == FMT_VI && vi_staged(c) && c.vi_bits == 4) {
     const ZTiling t = vis_tiling(c);
     return 8 * (int64_t)(((t.nty + 7) / 8) * t.ntx * t.nzc);
   }
@@ -2888,6 +2896,22 @@ int build_split(Ctx& c, bool* exact) {
 // FMT_VI assembly (see k_vi_collect).  ok = the matrix has at most VI_MAX distinct values; the
 // dictionary is the sorted set of their bit patterns, so indices do not depend on the order
 // the set was filled in.
+// the index array at bytes_per_node x the owned node groups (grown, never shrunk)
+static int ensure_vi_idx(Ctx& c, int64_t bytes_per_node) {
+  const int64_t need = c.ngroups * 64 * bytes_per_node;
+  if (need <= c.vi_idx_bytes) return 0;
+  if (c.vi_idx) {
+    MCX_HIP(hipStreamSynchronize(c.stream));
+    MCX_HIP(hipFree(c.vi_idx));
+    c.device_bytes -= c.vi_idx_bytes;
+    c.vi_idx = nullptr;
+  }
+  MCX_HIP(hipMalloc(&c.vi_idx, need));
+  c.vi_idx_bytes = need;
+  c.device_bytes += need;
+  return 0;
+}
+
 int build_vi(Ctx& c, bool* ok) {
   *ok = false;
   const bool table = table_law(c);
@@ -2959,6 +2983,7 @@ int build_vi(Ctx& c, bool* ok) {
       }
       MCX_HIP(hipMemcpyAsync(bmap, bm.data(), VI_HASH, hipMemcpyHostToDevice, c.stream));
       MCX_HIP(hipMemcpyAsync(c.vi_bdict, bd.data(), bd.size() * sizeof(double), hipMemcpyHostToDevice, c.stream));
+      if (int rc = ensure_vi_idx(c, 32)) return rc;
       if (table)
         hipLaunchKernelGGL(k_vib_pack<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, skeys, c.vi_slot, bkeys,
                            bmap, c.vi_idx);
@@ -2974,6 +2999,7 @@ int build_vi(Ctx& c, bool* ok) {
       return 0;
     }
   }
+  if (int rc = ensure_vi_idx(c, bits == 8 ? 256 : 128)) return rc;
   u32x4* I = reinterpret_cast<u32x4*>(c.vi_idx);
   const dim3 pg(nblk(c.g.nown));
   if (bits == 8 && table)
@@ -3010,7 +3036,7 @@ void launch_jacobi(Ctx& c) {
 template <int NIB>
 static void launch_spmv_vi(Ctx& c, const double* xpad, double* y, bool dot, bool gated, int nb, const SpmvTiling& tl) {
   const u32x4* I = reinterpret_cast<const u32x4*>(c.vi_idx);
-  if (NIB == 4 && c.vi_stage) {  // x staged in LDS, 1024-node tiles marching z-chunks
+  if (NIB == 4 && vi_staged(c)) {  // x staged in LDS, 1024-node tiles marching z-chunks
     const ZTiling zt = vis_tiling(c);
     int tx, ty;
     vis_shape(c, tx, ty);
@@ -3062,7 +3088,7 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
   const SpmvTiling tl = spmv_tiling(c.g, c.spmv_subl);
   if (c.fmt == FMT_VI && c.vi_block) {
     const u32x4* I = reinterpret_cast<const u32x4*>(c.vi_idx);
-    if (c.vi_stage) {  // x staged in LDS, 1024-node tiles marching z-chunks
+    if (vi_staged(c)) {  // x staged in LDS, 1024-node tiles marching z-chunks
       const ZTiling zt = vis_tiling(c);
       int tx, ty;
       vis_shape(c, tx, ty);

@@ -144,6 +144,7 @@ struct Ctx {
   // value-indexed AIJ (FMT_VI): index bytes [ngroups][VI_CHUNKS][64] x 16 B, the dictionary
   // (VI_MAX doubles, ascending bit pattern), the build's value set and its slot -> index map
   unsigned char* vi_idx = nullptr;
+  int64_t vi_idx_bytes = 0;               // allocated bytes of vi_idx (grown to the mode's 32 / 128 / 256 B per node)
   double* vi_dict = nullptr;
   unsigned long long* vi_keys = nullptr;  // [VI_HASH] the value set, [NSLOT][32] the slots' sets, [VI_HASH] the block set
   unsigned char* vi_slot = nullptr;       // index of every set entry ([VI_HASH] or [NSLOT][32]), then the blocks'
@@ -157,7 +158,7 @@ struct Ctx {
   int vi_nblocks = 0;                     // distinct blocks of the current matrix (block mode)
   double* vi_bdict = nullptr;             // [VI_MAX][VIB_STRIDE] dictionary blocks
   int aij_vi = 1;            // aij: assemble in FMT_VI when the matrix has at most VI_MAX distinct values
-  int vi_stage = 1;          // FMT_VI SpMV: 1 = x staged in LDS per tile (k_spmv_vis), 0 = gathered (k_spmv_vi)
+  int vi_stage = -1;         // FMT_VI SpMV: 1 = x staged in LDS, z-marching tiles; 0 = x gathered; -1 = by grid (vi_staged)
   bool vi_declined = false;  // a per-GP-tangent law overflowed the dictionary: skip the attempt
   int fmt = FMT_V;           // storage the matrix is currently assembled in
   bool assembled = false;    // a matrix has been assembled (mcx_assembly_jac)
@@ -271,6 +272,7 @@ void launch_copy_pad_to_owned(Ctx& c, const double* pad, double* owned);
 int64_t spmv_grid_blocks(const Ctx& c);
 int64_t spmv_nparts(const Ctx& c);   // partial sums the CG's SpMV leaves (its own grid, or the dense pass's)
 int64_t node_blocks(const Ctx& c);
+bool vi_staged(const Ctx& c);
 int dirichlet_mask_host(const Geo& g, int gi, int gj, int gk);
 
 }  // namespace mcx

@@ -126,6 +126,8 @@ def test_aij_vi_single_rank(name):
         m.set_option("spmv_zblocks", 1)  # one z-chunk per tile: the staged ring marches every plane
         assert np.array_equal(m.spmv(x), y)
         m.set_option("spmv_zblocks", 0)
+        assert np.array_equal(m.spmv(x), y)
+        m.set_option("vi_stage", -1)
         m.set_option("vi_bits", 8)  # one byte per value into one dictionary: the same matrix and products
         m.assembly_jac()
         assert m.get_info()["vi_bits"] == 8 and np.array_equal(m.dump_csr()[2], v)
@@ -133,6 +135,13 @@ def test_aij_vi_single_rank(name):
         m.set_option("vi_bits", 4)
         m.set_option("vi_block", 1)
         m.assembly_jac()
+        assert m.get_info()["vi_blocks"] > 0
+        for stage, zblocks in ((0, 0), (1, 0), (1, 1)):  # block dictionary: gathered x, staged x, marching
+            m.set_option("vi_stage", stage)
+            m.set_option("spmv_zblocks", zblocks)
+            assert np.array_equal(m.spmv(x), y), (stage, zblocks)
+        m.set_option("vi_stage", -1)
+        m.set_option("spmv_zblocks", 0)
         its, rn, reason = m.solve_Ax()
         assert abs(its - int(fx["its"])) <= 1
         ref = fx["du"]

@@ -1,5 +1,5 @@
 #!/bin/bash
-# tools/pmc_spmv.sh STORAGE GRID (aij-split | aij-blocks | sbaij) — HBM traffic of the CG SpMV kernel from rocprofv3 PMC counters:
+# tools/pmc_spmv.sh STORAGE GRID (aij-vi | aij-split | aij-blocks | sbaij) — HBM traffic of the CG SpMV kernel from rocprofv3 PMC counters:
 # FETCH_SIZE and WRITE_SIZE in separate passes (they do not fit one pass on gfx950), kernel
 # trace only (no sys/runtime tracing beside --pmc), one bench step at GRID^3.  Results are
 # parsed by tools/pmc_parse.py into gpurun_out/pmc/ and profiles/pmc_spmv.json.
@@ -7,7 +7,8 @@ set -euo pipefail
 MAT=${1:-aij-split}
 G=${2:-256}
 case $MAT in
-  aij-split) RE='k_spmv_symp'; BM=aij ;;
+  aij-vi) RE='k_spmv_vib'; BM=aij ;;
+  aij-split) RE='k_spmv_symp'; BM=aij-split ;;
   aij-blocks) RE='k_spmv<'; BM=aij-blocks ;;
   sbaij) RE='k_spmv_sym'; BM=sbaij ;;
 esac

@@ -9,5 +9,4 @@ mkdir -p gpurun_out
 timeout -k 10 420 python3 bench.py > gpurun_out/${TAG}_bench_default.json 2> gpurun_out/${TAG}_bench_default.log
 timeout -k 10 480 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run --output-format csv -- \
   python3 bench.py > gpurun_out/${TAG}_bench_default_under_rocprof.json 2> gpurun_out/${TAG}_bench_rocprof.log
-bash tools/pmc_spmv.sh aij-split 256
-bash tools/pmc_spmv.sh sbaij 256
+bash tools/pmc_spmv.sh aij-vi 256
