@@ -2028,8 +2028,9 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
         const unsigned word = nb < 16 ? c0[nb >> 2] : c1[(nb - 16) >> 2];
         const unsigned id = (word >> (8 * (nb & 3))) & 255u;
         const double2* e = tab + id * (VIB_STRIDE / 2);
-        const double2 a01 = e[0], a23 = e[1], a45 = e[2], a67 = e[3], a8 = e[4];
-        const double a[9] = {a01.x, a01.y, a23.x, a23.y, a45.x, a45.y, a67.x, a67.y, a8.x};
+        const double2 a01 = e[0], a23 = e[1], a45 = e[2], a67 = e[3];
+        const double a8 = reinterpret_cast<const double*>(e)[8];  // 8 B, not the padded 16: 18 LDS cycles per block
+        const double a[9] = {a01.x, a01.y, a23.x, a23.y, a45.x, a45.y, a67.x, a67.y, a8};
 #pragma unroll
         for (int q = 0; q < 9; q++) {
           const int r = q / 3, cc = q % 3;
