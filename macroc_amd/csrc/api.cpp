@@ -1373,6 +1373,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.vi_block_on = value != 0.;
     return 0;
   }
+  if (!std::strcmp(name, "vi_xread")) {
+    c.vi_xread = value != 0.;
+    return 0;
+  }
   if (!std::strcmp(name, "vi_stage")) {
     c.vi_stage = value < 0. ? -1 : (value != 0. ? 1 : 0);
     if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {

@@ -158,6 +158,7 @@ struct Ctx {
   int vi_nblocks = 0;                     // distinct blocks of the current matrix (block mode)
   double* vi_bdict = nullptr;             // [VI_MAX][VIB_STRIDE] dictionary blocks
   int aij_vi = 1;            // aij: assemble in FMT_VI when the matrix has at most VI_MAX distinct values
+  int vi_xread = 1;          // staged block-indexed SpMV: x as unpaired 8-B LDS reads (option vi_xread; 0: compiler's pairs)
   int vi_stage = -1;         // FMT_VI SpMV: 1 = x staged in LDS, z-marching tiles; 0 = x gathered; -1 = by grid (vi_staged)
   bool vi_declined = false;  // a per-GP-tangent law overflowed the dictionary: skip the attempt
   int fmt = FMT_V;           // storage the matrix is currently assembled in

@@ -136,10 +136,13 @@ def test_aij_vi_single_rank(name):
         m.set_option("vi_block", 1)
         m.assembly_jac()
         assert m.get_info()["vi_blocks"] > 0
-        for stage, zblocks in ((0, 0), (1, 0), (1, 1)):  # block dictionary: gathered x, staged x, marching
+        # block dictionary: gathered x, staged x, marching; x read from LDS unpaired or paired
+        for stage, zblocks, xread in ((0, 0, 1), (1, 0, 1), (1, 1, 1), (1, 0, 0), (1, 1, 0)):
             m.set_option("vi_stage", stage)
             m.set_option("spmv_zblocks", zblocks)
-            assert np.array_equal(m.spmv(x), y), (stage, zblocks)
+            m.set_option("vi_xread", xread)
+            assert np.array_equal(m.spmv(x), y), (stage, zblocks, xread)
+        m.set_option("vi_xread", 1)
         m.set_option("vi_stage", -1)
         m.set_option("spmv_zblocks", 0)
         its, rn, reason = m.solve_Ax()
