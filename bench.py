@@ -83,6 +83,24 @@ def pmc_traffic(mat_type, NX, NY, NZ):
         return None
 
 
+def lds_limiter(mat_type, NX, NY, NZ):
+    """LDS-array busy fraction of the headline SpMV kernel from the committed rocprofv3 SQ counter
+    passes (profiles/pmc_vibm.json, tools/pmc_vibm.sh: SQ_LDS_IDX_ACTIVE per CU / SQ_BUSY_CYCLES per
+    shader engine), or None.  The value-indexed kernel streams only ~80 B per node from HBM; its
+    limiter is the LDS (x ring + block dictionary reads), which this reports beside the HBM roofline."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_vibm.json")
+    try:
+        with open(path) as f:
+            e = json.load(f).get(f"{mat_type}:{NX}x{NY}x{NZ}")
+        if not e:
+            return None
+        return {"resource": "LDS", "busy_frac": e["lds_busy_frac"], "kernel": e["kernel"],
+                "valu_insts_per_wave_plane": e["valu_insts_per_wave_plane"],
+                "lds_insts_per_wave_plane": e["lds_insts_per_wave_plane"], "source": "profiles/pmc_vibm.json"}
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def host_cores():
     """CPUs this process may really use: the affinity mask, capped by a cgroup v2 CPU quota."""
     n = len(os.sched_getaffinity(0))
@@ -363,7 +381,8 @@ def main():
                          "avg_launch_ms": spmv_avg_ms, "launches_timed": tm["spmv_launches"],
                          # the same launch priced at PETSc AIJ bytes (what the reference's MatMult streams)
                          "csr_bytes_per_launch": r["csr_bytes"], "csr_achieved": csr_achieved,
-                         "csr_frac": csr_achieved / PEAK_HBM_GBS},
+                         "csr_frac": csr_achieved / PEAK_HBM_GBS,
+                         "limiter": lds_limiter(r["storage"], NX, NY, NZ)},
             "cpu_baseline": cpu,
             "check": check,
             "variants": variants,
