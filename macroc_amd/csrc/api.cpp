@@ -54,7 +54,7 @@ static int free_ctx(Ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
-  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
+  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf, c->halo.d_bnd};
   for (void* p : ptrs)
@@ -143,7 +143,8 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   // AIJ-split corrections D are sized by build_split to the active slots
   if ((rc = dalloc(c, &c.u_pad, npad)) || (rc = dalloc(c, &c.p_pad, npad)) || (rc = dalloc(c, &c.b, nown3)) ||
       (rc = dalloc(c, &c.du, nown3)) || (rc = dalloc(c, &c.r, nown3)) || (rc = dalloc(c, &c.z, nown3)) ||
-      (rc = dalloc(c, &c.w, nown3)) || (rc = dalloc(c, &c.dinv, nown3)) || (rc = dalloc(c, &c.tmp, nown3)) ||
+      (rc = dalloc(c, &c.w, nown3)) || (rc = dalloc(c, &c.dinv, nown3)) ||
+      (rc = dalloc(c, &c.jix, (int64_t)g.nown)) || (rc = dalloc(c, &c.jdd, 3 * VI_MAX)) || (rc = dalloc(c, &c.tmp, nown3)) ||
       (c.o.mat_type == MCX_MAT_SBAIJ && (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))) ||
       (c.o.mat_type == MCX_MAT_AIJ && !c.aij_split && (rc = dalloc(c, &c.V, c.ngroups * NPAIR * 128))) ||
       (rc = dalloc(c, &c.eps, 6 * 8 * E)) || (rc = dalloc(c, &c.sig, 6 * 8 * E)) ||
@@ -1401,6 +1402,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
       return 2;
     }
     c.aij_split = value != 0.;
+    return 0;
+  }
+  if (!std::strcmp(name, "cg_dix")) {
+    c.cg_dix = value != 0.;
     return 0;
   }
   if (!std::strcmp(name, "cg_nt")) {

@@ -1872,18 +1872,28 @@ __global__ __launch_bounds__(TPB) void k_vib_pack(Geo g, Material mat, const dou
   I[(((int64_t)(n >> 6) * 2 + (nb >> 4)) * 64 + (n & 63)) * 16 + (nb & 15)] = s_bmap[h];
 }
 
+__device__ __forceinline__ double jacobi_inv(double d) {
+  if (d != 0.0) d = 1.0 / d;
+  if (d == 0.0) d = 1.0;
+  return d;
+}
+
+// dinv per owned DOF, and jix[n] = the node's diagonal-block index (block 13 = offset 0,0,0)
 __global__ void k_jacobi_vib(Geo g, const unsigned char* __restrict__ I, const double* __restrict__ bdict,
-                             double* __restrict__ dinv) {
+                             double* __restrict__ dinv, unsigned char* __restrict__ jix) {
   const int n = blockIdx.x * TPB + threadIdx.x;
   if (n >= g.nown) return;
   const int id = I[(((int64_t)(n >> 6) * 2 + 0) * 64 + (n & 63)) * 16 + 13];
+  jix[n] = (unsigned char)id;
 #pragma unroll
-  for (int r = 0; r < 3; r++) {
-    double d = bdict[id * VIB_STRIDE + r * 4];
-    if (d != 0.0) d = 1.0 / d;
-    if (d == 0.0) d = 1.0;
-    dinv[3 * n + r] = d;
-  }
+  for (int r = 0; r < 3; r++) dinv[3 * n + r] = jacobi_inv(bdict[id * VIB_STRIDE + r * 4]);
+}
+
+// the dictionary's inverse diagonals [VI_MAX][3] (same values as k_jacobi_vib's dinv)
+__global__ void k_jacobi_vib_dict(const double* __restrict__ bdict, double* __restrict__ jdd) {
+  const int t = blockIdx.x * TPB + threadIdx.x;
+  if (t >= 3 * VI_MAX) return;
+  jdd[t] = jacobi_inv(bdict[(t / 3) * VIB_STRIDE + (t % 3) * 4]);
 }
 
 // y = A x on block-indexed FMT_VI: 2 16-B index chunks per node (27 block bytes), each block's
@@ -2324,8 +2334,28 @@ __device__ __forceinline__ void st(double* p, double v) {
   else *p = v;
 }
 
-template <bool NT>
+// Jacobi inverse diagonal of DOF 3n+d.  DIX (block-indexed value storage): dinv is the
+// dictionary's inverse diagonals [VI_MAX][3] and jix the owned nodes' diagonal-block index (one
+// byte per node instead of 24 B of dinv); the values are k_jacobi_vib's, so z = r * dinv is
+// bit-identical either way.
+template <bool DIX>
+__device__ __forceinline__ double jac_inv(const double* __restrict__ dinv, const unsigned char* __restrict__ jix,
+                                          int n, int d) {
+  if constexpr (DIX) return dinv[3 * jix[n] + d];
+  else return dinv[3 * n + d];
+}
+
+// z of DOF q = 3n+d: stored z, or (DIX) recomputed from r (the update kernel then writes no z)
+template <bool DIX>
+__device__ __forceinline__ double z_of(const double* __restrict__ z, const double* __restrict__ dinv,
+                                       const unsigned char* __restrict__ jix, int n, int d) {
+  if constexpr (DIX) return z[3 * n + d] * jac_inv<true>(dinv, jix, n, d);
+  else return z[3 * n + d];
+}
+
+template <bool NT, bool DIX>
 __device__ __forceinline__ void pupdate_node(const Geo& g, int n, const double* __restrict__ z,
+                                             const double* __restrict__ dinv, const unsigned char* __restrict__ jix,
                                              double* __restrict__ ppad, double* __restrict__ x,
                                              const CgState* __restrict__ cg) {
   int i, j, k;
@@ -2333,7 +2363,7 @@ __device__ __forceinline__ void pupdate_node(const Geo& g, int n, const double* 
   const int pc = pad_of(g, i, j, k);
   if (cg->i == 0) {
 #pragma unroll
-    for (int d = 0; d < 3; d++) st<NT>(&ppad[3 * pc + d], z[3 * n + d]);
+    for (int d = 0; d < 3; d++) st<NT>(&ppad[3 * pc + d], z_of<DIX>(z, dinv, jix, n, d));
   } else {
     const double bc = cg->bcoef, a = cg->alpha;
 #pragma unroll
@@ -2341,7 +2371,7 @@ __device__ __forceinline__ void pupdate_node(const Geo& g, int n, const double* 
       const int q = 3 * n + d;
       const double pv = ppad[3 * pc + d];
       st<NT>(&x[q], x[q] + a * pv);
-      st<NT>(&ppad[3 * pc + d], z[q] + bc * pv);
+      st<NT>(&ppad[3 * pc + d], z_of<DIX>(z, dinv, jix, n, d) + bc * pv);
     }
   }
 }
@@ -2353,8 +2383,9 @@ __device__ __forceinline__ bool sent_node(const Geo& g, int i, int j, int k) {
 }
 
 // SKIP_SENT: the sent nodes were updated before the halo exchange (k_cg_pupdate_list)
-template <bool NT, bool SKIP_SENT = false>
-__global__ void k_cg_pupdate(Geo g, const double* __restrict__ z, double* __restrict__ ppad,
+template <bool NT, bool DIX, bool SKIP_SENT = false>
+__global__ void k_cg_pupdate(Geo g, const double* __restrict__ z, const double* __restrict__ dinv,
+                             const unsigned char* __restrict__ jix, double* __restrict__ ppad,
                              double* __restrict__ x, const CgState* __restrict__ cg) {
   if (cg->reason) return;
   int n = blockIdx.x * TPB + threadIdx.x;
@@ -2364,17 +2395,18 @@ __global__ void k_cg_pupdate(Geo g, const double* __restrict__ z, double* __rest
     node_ijk(g, n, i, j, k);
     if (sent_node(g, i, j, k)) return;
   }
-  pupdate_node<NT>(g, n, z, ppad, x, cg);
+  pupdate_node<NT, DIX>(g, n, z, dinv, jix, ppad, x, cg);
 }
 
-template <bool NT>
-__global__ void k_cg_pupdate_list(Geo g, const double* __restrict__ z, double* __restrict__ ppad,
+template <bool NT, bool DIX>
+__global__ void k_cg_pupdate_list(Geo g, const double* __restrict__ z, const double* __restrict__ dinv,
+                                  const unsigned char* __restrict__ jix, double* __restrict__ ppad,
                                   double* __restrict__ x, const CgState* __restrict__ cg,
                                   const int* __restrict__ list, int64_t cnt) {
   if (cg->reason) return;
   const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (t >= cnt) return;
-  pupdate_node<NT>(g, list[t], z, ppad, x, cg);
+  pupdate_node<NT, DIX>(g, list[t], z, dinv, jix, ppad, x, cg);
 }
 
 // the last iteration's x += alpha p (when that iteration reached its update)
@@ -2395,9 +2427,10 @@ __global__ void k_cg_xfinal(Geo g, const double* __restrict__ ppad, double* __re
 // 1024-thread blocks: a quarter of the partials for k_reduce (one block reads them all)
 static constexpr int UTPB = 1024;
 
-template <bool NT>
+template <bool NT, bool DIX>
 __global__ __launch_bounds__(UTPB) void k_cg_update(Geo g, const double* __restrict__ w,
                                                    const double* __restrict__ dinv,
+                                                   const unsigned char* __restrict__ jix,
                                                    double* __restrict__ r, double* __restrict__ z,
                                                    double* __restrict__ part, int nparts,
                                                    const CgState* __restrict__ cg) {
@@ -2412,8 +2445,8 @@ __global__ __launch_bounds__(UTPB) void k_cg_update(Geo g, const double* __restr
       const int q = 3 * n + d;
       const double rv = r[q] + ma * w[q];
       st<NT>(&r[q], rv);
-      const double zv = rv * dinv[q];
-      st<NT>(&z[q], zv);
+      const double zv = rv * jac_inv<DIX>(dinv, jix, n, d);
+      if (!DIX) st<NT>(&z[q], zv);
       zz += zv * zv;
       zr += zv * rv;
     }
@@ -2437,9 +2470,10 @@ __device__ void cg_logic_beta(CgState* s, double zz, double zr, double* hist);
 
 // r += (-a) w; z = D^-1 r; partials z.z, z.r — with alpha from the SpMV's p.w partials
 // (k_reduce's RED_ALPHA step, same summation tree for npw <= UTPB)
-template <bool NT>
+template <bool NT, bool DIX>
 __global__ __launch_bounds__(UTPB) void k_cg_update_fa(Geo g, const double* __restrict__ w,
-                                                      const double* __restrict__ dinv, double* __restrict__ r,
+                                                      const double* __restrict__ dinv,
+                                                      const unsigned char* __restrict__ jix, double* __restrict__ r,
                                                       double* __restrict__ z, double* __restrict__ part, int nparts,
                                                       const double* __restrict__ part_pw, int npw,
                                                       const CgState* __restrict__ cg_in, CgState* __restrict__ cg_out) {
@@ -2467,8 +2501,8 @@ __global__ __launch_bounds__(UTPB) void k_cg_update_fa(Geo g, const double* __re
       const int q = 3 * n + d;
       const double rv = r[q] + ma * w[q];
       st<NT>(&r[q], rv);
-      const double zv = rv * dinv[q];
-      st<NT>(&z[q], zv);
+      const double zv = rv * jac_inv<DIX>(dinv, jix, n, d);
+      if (!DIX) st<NT>(&z[q], zv);
       zz += zv * zv;
       zr += zv * rv;
     }
@@ -2501,8 +2535,10 @@ __device__ __forceinline__ double sum1024_by256(const double* __restrict__ v, in
 }
 
 // p update with beta from the update's z.z / z.r partials (k_reduce's RED_BETA step)
-template <bool NT>
+template <bool NT, bool DIX>
 __global__ __launch_bounds__(TPB) void k_cg_pupdate_fb(Geo g, const double* __restrict__ z,
+                                                      const double* __restrict__ dinv,
+                                                      const unsigned char* __restrict__ jix,
                                                       double* __restrict__ ppad, double* __restrict__ x,
                                                       const double* __restrict__ part, int nparts,
                                                       const CgState* __restrict__ cg_in, CgState* __restrict__ cg_out,
@@ -2530,7 +2566,7 @@ __global__ __launch_bounds__(TPB) void k_cg_pupdate_fb(Geo g, const double* __re
     const int q = 3 * n + d;
     const double pv = ppad[3 * pc + d];
     st<NT>(&x[q], x[q] + a * pv);
-    st<NT>(&ppad[3 * pc + d], z[q] + bc * pv);
+    st<NT>(&ppad[3 * pc + d], z_of<DIX>(z, dinv, jix, n, d) + bc * pv);
   }
 }
 
@@ -3037,8 +3073,11 @@ int build_vi(Ctx& c, bool* ok) {
 
 void launch_jacobi(Ctx& c) {
   if (c.fmt == FMT_VI && c.vi_block)
-    hipLaunchKernelGGL(k_jacobi_vib, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.vi_idx, c.vi_bdict, c.dinv);
-  else if (c.fmt == FMT_VI && c.vi_bits == 4)
+  {
+    hipLaunchKernelGGL(k_jacobi_vib, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.vi_idx, c.vi_bdict, c.dinv,
+                       c.jix);
+    hipLaunchKernelGGL(k_jacobi_vib_dict, dim3(nblk(3 * VI_MAX)), dim3(TPB), 0, c.stream, c.vi_bdict, c.jdd);
+  } else if (c.fmt == FMT_VI && c.vi_bits == 4)
     hipLaunchKernelGGL(k_jacobi_vi<4>, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g,
                        reinterpret_cast<const u32x4*>(c.vi_idx), c.vi_dict, c.dinv);
   else if (c.fmt == FMT_VI)
@@ -3301,27 +3340,48 @@ void launch_cg_xfinal(Ctx& c) {
   hipLaunchKernelGGL(k_cg_xfinal, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.p_pad, c.du, c.cg);
 }
 
+// CG vector kernels' Jacobi form: DIX (block-indexed value storage, option cg_dix) reads one
+// diagonal-block index byte per node and recomputes z = D^-1 r from r where it is used, so the
+// update writes no z and reads no dinv vector (two fewer vectors per iteration)
+static bool cg_dix(const Ctx& c) { return c.cg_dix && c.fmt == FMT_VI && c.vi_block; }
+
+// instantiate CALL with constexpr NT (non-temporal stores) and DX (DIX) from run-time flags
+#define MCX_NT_DIX(ntv, dixv, CALL)                      \
+  do {                                                   \
+    if ((ntv) && (dixv)) {                               \
+      constexpr bool NT = true, DX = true;               \
+      CALL;                                              \
+    } else if (ntv) {                                    \
+      constexpr bool NT = true, DX = false;              \
+      CALL;                                              \
+    } else if (dixv) {                                   \
+      constexpr bool NT = false, DX = true;              \
+      CALL;                                              \
+    } else {                                             \
+      constexpr bool NT = false, DX = false;             \
+      CALL;                                              \
+    }                                                    \
+  } while (0)
+
 void launch_cg_pupdate(Ctx& c, int part) {
   const unsigned nbn = nblk(c.g.nown);
+  const bool dix = cg_dix(c);
+  const double* zs = dix ? c.r : c.z;
+  const double* jd = dix ? c.jdd : c.dinv;
   if (part == 1) {
     if (!c.halo.nbnd) return;
     const unsigned nb = nblk(c.halo.nbnd);
-    if (c.cg_nt)
-      hipLaunchKernelGGL(k_cg_pupdate_list<true>, dim3(nb), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg,
-                         c.halo.d_bnd, c.halo.nbnd);
-    else
-      hipLaunchKernelGGL(k_cg_pupdate_list<false>, dim3(nb), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg,
-                         c.halo.d_bnd, c.halo.nbnd);
+    MCX_NT_DIX(c.cg_nt, dix,
+               hipLaunchKernelGGL((k_cg_pupdate_list<NT, DX>), dim3(nb), dim3(TPB), 0, c.stream, c.g, zs, jd, c.jix,
+                                  c.p_pad, c.du, c.cg, c.halo.d_bnd, c.halo.nbnd));
   } else if (part == 2) {
-    if (c.cg_nt)
-      hipLaunchKernelGGL((k_cg_pupdate<true, true>), dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg);
-    else
-      hipLaunchKernelGGL((k_cg_pupdate<false, true>), dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg);
+    MCX_NT_DIX(c.cg_nt, dix,
+               hipLaunchKernelGGL((k_cg_pupdate<NT, DX, true>), dim3(nbn), dim3(TPB), 0, c.stream, c.g, zs, jd, c.jix,
+                                  c.p_pad, c.du, c.cg));
   } else {
-    if (c.cg_nt)
-      hipLaunchKernelGGL((k_cg_pupdate<true>), dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg);
-    else
-      hipLaunchKernelGGL((k_cg_pupdate<false>), dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du, c.cg);
+    MCX_NT_DIX(c.cg_nt, dix,
+               hipLaunchKernelGGL((k_cg_pupdate<NT, DX>), dim3(nbn), dim3(TPB), 0, c.stream, c.g, zs, jd, c.jix,
+                                  c.p_pad, c.du, c.cg));
   }
 }
 
@@ -3340,13 +3400,13 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) 
   // folds save 1.6 % (profiles/r02_cg_ab_fuse{64,256}.log)
   const bool fa = fused(c) && nbu <= 1024, fb = fa;
   int rc;
+  const bool dix = cg_dix(c);
+  const double* zs = dix ? c.r : c.z;
+  const double* jd = dix ? c.jdd : c.dinv;
   if (fb && !first) {
-    if (c.cg_nt)
-      hipLaunchKernelGGL(k_cg_pupdate_fb<true>, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad, c.du,
-                         c.partials2, nbu, A, c.cg, c.hist);
-    else
-      hipLaunchKernelGGL(k_cg_pupdate_fb<false>, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.z, c.p_pad,
-                         c.du, c.partials2, nbu, A, c.cg, c.hist);
+    MCX_NT_DIX(c.cg_nt, dix,
+               hipLaunchKernelGGL((k_cg_pupdate_fb<NT, DX>), dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, zs, jd,
+                                  c.jix, c.p_pad, c.du, c.partials2, nbu, A, c.cg, c.hist));
   } else if (c.nranks > 1 && c.overlap && c.halo.nbnd) {
     // the sent nodes' p first, then their exchange overlaps the interior p update
     launch_cg_pupdate(c, 1);
@@ -3361,23 +3421,17 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) 
   launch_spmv(c, c.p_pad, c.w, true, true);
   if (ev1) MCX_HIP(hipEventRecord(ev1, c.stream));
   if (fa) {
-    if (c.cg_nt)
-      hipLaunchKernelGGL(k_cg_update_fa<true>, dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, c.dinv, c.r, c.z,
-                         c.partials2, nbu, c.partials, nbs, c.cg, A);
-    else
-      hipLaunchKernelGGL(k_cg_update_fa<false>, dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, c.dinv, c.r, c.z,
-                         c.partials2, nbu, c.partials, nbs, c.cg, A);
+    MCX_NT_DIX(c.cg_nt, dix,
+               hipLaunchKernelGGL((k_cg_update_fa<NT, DX>), dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, jd, c.jix,
+                                  c.r, c.z, c.partials2, nbu, c.partials, nbs, c.cg, A));
     if (!fb || last) return reduce_and_logic(c, 2, nbu, RED_BETA, true, c.partials2, A);
     return 0;
   }
   rc = reduce_and_logic(c, 1, nbs, RED_ALPHA, true, c.partials, c.cg);
   if (rc) return rc;
-  if (c.cg_nt)
-    hipLaunchKernelGGL(k_cg_update<true>, dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, c.dinv, c.r, c.z,
-                       c.partials2, nbu, c.cg);
-  else
-    hipLaunchKernelGGL(k_cg_update<false>, dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, c.dinv, c.r, c.z,
-                       c.partials2, nbu, c.cg);
+  MCX_NT_DIX(c.cg_nt, dix,
+             hipLaunchKernelGGL((k_cg_update<NT, DX>), dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, jd, c.jix, c.r,
+                                c.z, c.partials2, nbu, c.cg));
   return reduce_and_logic(c, 2, nbu, RED_BETA, true, c.partials2, c.cg);
 }
 

@@ -136,6 +136,9 @@ struct Ctx {
   double* z = nullptr;
   double* w = nullptr;
   double* dinv = nullptr;    // Jacobi inverse diagonal
+  unsigned char* jix = nullptr;  // block-indexed storage: each owned node's diagonal-block index
+  double* jdd = nullptr;         // block-indexed storage: the dictionary's inverse diagonals [VI_MAX][3]
+  int cg_dix = 1;                // CG kernels: Jacobi from jix/jdd, z recomputed from r (option cg_dix)
   double* V = nullptr;       // aij stencil-block matrix, AoSoA [ngroups][NPAIR][64] double2
   double* U = nullptr;       // sbaij upper stencil blocks over the padded box [npgroups][UPAIR][64] double2
   uint16_t* D = nullptr;     // AIJ-split: bf16 corrections of the padded box [u_of/64][dsl.Lq][64] x 8
