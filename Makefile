@@ -13,7 +13,7 @@ MPI_DIR ?= /opt/conda
 MPI_FLAGS = -I$(MPI_DIR)/include -Wl,-rpath-link,/usr/lib/x86_64-linux-gnu $(MPI_DIR)/lib/libmpi.so -Wl,-rpath,$(MPI_DIR)/lib
 TESTLAW = tests/libmcx_testlaw.so
 
-all: $(LIB) oracle driver driver-mpi testlaw
+all: $(LIB) oracle driver driver-mpi testlaw asan
 
 build/%.o: macroc_amd/csrc/% $(HDR)
 	@mkdir -p build
@@ -50,4 +50,31 @@ clean:
 	rm -rf build $(LIB) macroc_amd/driver/macroc_amd macroc_amd/driver/macroc_amd_mpi $(TESTLAW) tests/macroc_amd_micropp
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle driver driver-mpi testlaw clean
+# Host sanitizer build: every library source with AddressSanitizer + UBSan on the
+# host side only (-Xarch_host; device code is compiled as in the product build) linked with the C
+# driver into one executable, and the oracle's CLI under the same sanitizers (gcc).  No GPU is
+# touched: tests/test_asan.py runs the driver's -plan_only (mcx_plan / mcx_plan_halo: DMDA
+# decomposition, halo plans) on 1-8 rank grids and the oracle's time loop, and fails on any
+# sanitizer report.
+ASAN_DIR = build/asan
+ASAN_HOST = -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=all \
+            -Xarch_host -fno-omit-frame-pointer
+ASAN_OBJ = $(patsubst macroc_amd/csrc/%,$(ASAN_DIR)/%.o,$(SRC))
+ASAN_EXE = $(ASAN_DIR)/macroc_amd_asan
+ASAN_ORACLE = $(ASAN_DIR)/macroc_oracle_asan
+
+asan: $(ASAN_EXE) $(ASAN_ORACLE)
+$(ASAN_DIR)/%.o: macroc_amd/csrc/% $(HDR)
+	@mkdir -p $(ASAN_DIR)
+	$(HIPCC) -O1 -g -std=c++17 -fPIC -ffp-contract=off --offload-arch=$(ARCH) -Wall -Wno-unused-function $(ASAN_HOST) -c $< -o $@
+$(ASAN_DIR)/main.c.o: macroc_amd/driver/main.c include/macroc_amd.h
+	@mkdir -p $(ASAN_DIR)
+	$(HIPCC) -x c -O1 -g -std=gnu11 -Iinclude $(ASAN_HOST) -c $< -o $@
+$(ASAN_EXE): $(ASAN_OBJ) $(ASAN_DIR)/main.c.o
+	$(HIPCC) --offload-arch=$(ARCH) $(ASAN_HOST) -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+$(ASAN_ORACLE): oracle/main.c oracle/oracle.c oracle/oracle.h
+	@mkdir -p $(ASAN_DIR)
+	gcc -O1 -g -ffp-contract=off -fopenmp -std=gnu11 -fsanitize=address,undefined -fno-sanitize-recover=all \
+	  -fno-omit-frame-pointer -o $@ oracle/main.c oracle/oracle.c -lm
+
+.PHONY: all oracle driver driver-mpi testlaw asan clean

@@ -133,6 +133,9 @@ typedef struct {
                                    (every slot takes <= 16 values), 8 = a byte into one dictionary */
   int vi_blocks;                /* value-indexed AIJ, block mode: distinct 3x3 blocks (one index byte per
                                    block into a dictionary of them), 0 when values are indexed one by one */
+  int spmv_tx, spmv_ty, spmv_kc; /* SpMV of the last assembled storage when it is a z-marching tile kernel:
+                                   tile width (x nodes), height (y rows) and planes per z-chunk; 0 for the
+                                   gathered (one-node-per-thread) kernels */
 } mcx_info;
 
 typedef struct {

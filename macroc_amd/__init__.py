@@ -75,6 +75,7 @@ class Info(C.Structure):
         ("ex0", C.c_int64), ("ey0", C.c_int64), ("ez0", C.c_int64), ("nex", C.c_int64), ("ney", C.c_int64),
         ("nez", C.c_int64),
         ("vi_values", C.c_int), ("vi_bits", C.c_int), ("vi_blocks", C.c_int),
+        ("spmv_tx", C.c_int), ("spmv_ty", C.c_int), ("spmv_kc", C.c_int),
     ]
 
     def as_dict(self):

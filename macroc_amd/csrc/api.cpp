@@ -490,6 +490,7 @@ static void fill_info(const Ctx& c, mcx_info* in) {
   in->vi_values = c.fmt == FMT_VI ? c.vi_n : 0;
   in->vi_bits = c.fmt == FMT_VI ? c.vi_bits : 0;
   in->vi_blocks = c.fmt == FMT_VI && c.vi_block ? c.vi_nblocks : 0;
+  if (c.device >= 0) spmv_tile(c, &in->spmv_tx, &in->spmv_ty, &in->spmv_kc);
   in->ex0 = g.ex0;
   in->ey0 = g.ey0;
   in->ez0 = g.ez0;

@@ -80,6 +80,9 @@ int halo_start(Ctx& c, double* xpad) {
     for (int q : h.nbr_rank) MCX_HIP(hipStreamWaitEvent(c.stream, g->ev_halo_done[q], 0));
     launch_pack(c, xpad);
     MCX_HIP(hipEventRecord(g->ev_packed[c.rank], c.stream));
+    // the copies below overwrite my receive buffer: order them after my compute stream's last
+    // reader of it (the previous halo's k_unpack), as the RCCL branch does
+    MCX_HIP(hipStreamWaitEvent(c.comm_stream, g->ev_packed[c.rank], 0));
     group_barrier(g);
     for (size_t t = 0; t < h.nbr_rank.size(); t++) {
       const Ctx& q = *g->members[h.nbr_rank[t]];

@@ -2814,6 +2814,18 @@ int64_t spmv_grid_blocks(const Ctx& c) {
   if (c.spmv_subl < 0) return (int64_t)c.g.nz * t.jgroups * t.nxc;
   return 8 * (int64_t)t.per_xcd;
 }
+void spmv_tile(const Ctx& c, int* tx, int* ty, int* kc) {
+  *tx = *ty = *kc = 0;
+  if (c.fmt == FMT_VI && vi_staged(c) && c.vi_bits == 4) {
+    vis_shape(c, *tx, *ty);
+    *kc = vis_tiling(c).kc;
+  } else if (c.fmt == FMT_SPLIT || (c.fmt == FMT_U && c.spmv_kernel >= 1)) {
+    if (c.fmt == FMT_SPLIT) split_shape(c, *tx, *ty);
+    else z_shape(c.spmv_kernel, *tx, *ty);
+    *kc = z_tiling(c.g, *tx, *ty, c.spmv_zblocks).kc;
+  }
+}
+
 int64_t spmv_nparts(const Ctx& c) {
   if (c.fmt == FMT_SPLIT && c.dsl.dense) return node_blocks(c);
   return spmv_grid_blocks(c);

@@ -277,6 +277,8 @@ int64_t spmv_grid_blocks(const Ctx& c);
 int64_t spmv_nparts(const Ctx& c);   // partial sums the CG's SpMV leaves (its own grid, or the dense pass's)
 int64_t node_blocks(const Ctx& c);
 bool vi_staged(const Ctx& c);
+// z-marching SpMV tile of the current storage (tx, ty, planes per chunk); all 0 for gathered kernels
+void spmv_tile(const Ctx& c, int* tx, int* ty, int* kc);
 int dirichlet_mask_host(const Geo& g, int gi, int gj, int gk);
 
 }  // namespace mcx

@@ -83,7 +83,7 @@ class HostMicropp:
                       lambda: 0, lambda: -1.0)
 
 
-def testlaw():
+def _testlaw():
     L = C.CDLL(TESTLAW)
     L.testlaw_elastic_device.argtypes = [C.POINTER(M.DeviceLaw), C.c_double, C.c_double]
     L.testlaw_device_calls.argtypes = [C.POINTER(M.DeviceLaw), C.POINTER(C.c_int)]
@@ -143,7 +143,7 @@ def test_device_law_default_storage():
     isotropic C, so the matrix is value-indexed (bit-exact matrix dump)."""
     grid, rtol = (8, 8, 8), 1e-12
     P = O.Problem(*grid, rtol=rtol)
-    L = testlaw()
+    L = _testlaw()
     law = M.DeviceLaw()
     assert L.testlaw_elastic_device(C.byref(law), E_DEF, NU_DEF) == 0
     with M.Macroc(argv(*grid, rtol)) as m:

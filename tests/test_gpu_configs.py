@@ -55,6 +55,16 @@ def test_config3_256_cubed():
         assert np.linalg.norm(Axy - (Ax + 2.0 * Ay)) <= 1e-13 * np.linalg.norm(np.abs(Ax) + 2.0 * np.abs(Ay))
         res2, its2, reason2, du2 = step()
         assert res2 == res and its2 == its and np.array_equal(du2, du)
+        assert (m.get_info()["spmv_tx"], m.get_info()["spmv_ty"]) == (256, 4)  # the headline instantiation
+        # the same 256^3 matrix as AIJ stencil blocks (-mat_aij_vi 0 -mat_aij_split 0: every value
+        # stored, rows in the CPU AIJ order, bit-exact with the oracle at small grids): the
+        # value-indexed product is bit for bit the same
+        m.set_option("aij_vi", 0)
+        m.set_option("aij_split", 0)
+        m.assembly_jac()
+        assert m.get_info()["storage"] == 0
+        assert np.array_equal(m.spmv(x), Ax)
+        m.set_option("aij_split", 1)
         # the AIJ-split storage of the same matrix: 24 exact bf16 correction slots, same solve
         m.set_option("aij_vi", 0)
         res3, its3, reason3, du3 = step()
@@ -86,3 +96,74 @@ def test_config5_nonlinear_128(capfd):
                 assert b < a / 5, res
             assert all(1200 <= k <= 1700 for k in out["ksp_its"]), out["ksp_its"]
         assert 0 < counts[1] < counts[2], counts
+
+
+def test_config4_512_cubed_2x2x2_in_process():
+    """BASELINE config 4's workload (512^3, -da_processors_x 2 -y 2 -z 2: 256^3 nodes per
+    subdomain; tests/CMakeLists.txt:26-28, src/init.c:85-93) on ONE MI355X: the eight subdomain
+    contexts run as host threads over the in-process transport (the RCCL transport differs only in
+    the calls that move the bytes; two RCCL ranks cannot share one GPU).  Every rank assembles
+    its own value-indexed storage and dictionary; the CG runs the full halo plan (7 neighbours per
+    rank) and the all-reduced scalars.  Checks: iterations in the 5,400-5,900 window (the
+    survey's ~11.3 N estimate), KSP_CONVERGED_RTOL, the true residual |A du - b| <= 10 rtol |b|,
+    and du in natural order against a one-rank 512^3 solve of the same system run after it.
+    The per-iteration time of the 8-context run is printed (not a scaling number: the eight
+    subdomains share one GPU)."""
+    import time
+
+    from test_gpu_multirank import run_group
+
+    N, rtol = 512, 1e-8
+    base = ["-da_grid_x", N, "-da_grid_y", N, "-da_grid_z", N, "-ts", 2, "-ksp_rtol", repr(rtol)]
+    argv = base + ["-da_processors_x", 2, "-da_processors_y", 2, "-da_processors_z", 2]
+
+    def fn(m):
+        m.set_timing(True)
+        m.apply_bc_on_u(m.get_displacement(1))
+        m.set_strains()
+        m.homogenize()
+        res = m.assembly_res()
+        m.assembly_jac()
+        its, rn, reason = m.solve_Ax()
+        tm = m.timing()
+        info = m.get_info()
+        b, du = m.b(), m.du()
+        r = m.spmv(du) - b
+        _, nat = m.owned_dofs()
+        return dict(res=res, its=its, reason=reason, info=info, solve_ms=tm["solve_ms"], nat=nat, du=du,
+                    rr=float(r @ r), bb=float(b @ b))
+
+    t0 = time.time()
+    print("\nconfig4: 8 in-process subdomain contexts ...", flush=True)
+    out = run_group(argv, 8, fn, timeout=900)
+    t8 = time.time() - t0
+    print(f"config4: 8-context solve done in {t8:.1f} s, its {out[0]['its']}; one-rank 512^3 ...", flush=True)
+    its = out[0]["its"]
+    ndofs = 3 * N ** 3
+    du8 = np.zeros(ndofs)
+    for o in out:
+        info = o["info"]
+        assert (info["nx"], info["ny"], info["nz"]) == (256, 256, 256)
+        assert info["storage"] == 3 and 0 < info["vi_blocks"] <= 256, info
+        assert o["its"] == its and o["reason"] == 2 and o["res"] == out[0]["res"]
+        du8[o["nat"]] = o["du"]
+    assert 5400 <= its <= 5900, its
+    rr, bb = sum(o["rr"] for o in out), sum(o["bb"] for o in out)
+    assert rr ** 0.5 <= 10 * rtol * bb ** 0.5, (rr ** 0.5, bb ** 0.5)
+    ms8 = max(o["solve_ms"] for o in out) / its
+    del out
+    t0 = time.time()
+    with M.Macroc(base) as m:
+        m.apply_bc_on_u(m.get_displacement(1))
+        m.set_strains()
+        m.homogenize()
+        res1 = m.assembly_res()
+        m.assembly_jac()
+        its1, rn1, reason1 = m.solve_Ax()
+        du1 = m.du()  # one rank: PETSc order == natural order
+    t1 = time.time() - t0
+    rel = np.linalg.norm(du8 - du1) / np.linalg.norm(du1)
+    print(f"\nconfig4 in-process 2x2x2: its {its}, {ms8:.3f} ms per CG iteration (8 contexts on one GPU), "
+          f"{t8:.1f} s; one rank 512^3: its {its1}, {t1:.1f} s; |du8 - du1| / |du1| = {rel:.3e}")
+    assert reason1 == 2 and abs(its1 - its) <= 0.01 * its
+    assert rel <= 1e-8, rel

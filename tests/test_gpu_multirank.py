@@ -252,3 +252,71 @@ def test_rccl_transport_one_rank():
     (r0, i0, c0, d0, f0, n0), (r1, i1, c1, d1, f1, n1) = outs
     assert (i0, c0, f0, n0) == (i1, c1, f1, n1) and np.array_equal(d0, d1)
     assert abs(r0 - r1) <= 1e-15 * r0
+
+
+@pytest.mark.parametrize("grid,procs", [((516, 5, 4), (2, 1, 1)), ((260, 9, 10), (1, 1, 2))])
+def test_multirank_vi_production_tiles(grid, procs):
+    """The value-indexed SpMV's 256x4 tiles on decomposed subdomains (258 = 256 + 2 wide, an
+    internal x face at a partial tile's last lane; or a z split with internal z faces at the
+    chunk ends): every rank's matrix rows and SpMV bit-exact with the one-rank oracle (MATAIJ
+    MatMult, src/init.c:85-93), du within the north-star bar at rtol 1e-12."""
+    NX, NY, NZ = grid
+    px, py, pz = procs
+    rtol = 1e-12
+    argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
+            "-da_processors_z", pz, "-ksp_rtol", repr(rtol)]
+    ref = O.Problem(NX, NY, NZ, rtol=rtol)
+    ref.newton_step1()
+    v1 = ref.A_values()
+    rp1, ci1 = ref.csr()
+    x = np.random.default_rng(23).uniform(-1, 1, ref.ndofs)
+    y1 = ref.spmv(x)
+    out = run_group(argv, px * py * pz, newton_step(x, [("vi_stage", 1)]))
+    du = np.zeros(ref.ndofs)
+    for o in out:
+        info = o["info"]
+        assert info["storage"] == 3 and info["vi_blocks"] > 0 and (info["spmv_tx"], info["spmv_ty"]) == (256, 4), info
+        assert np.array_equal(o["y"], y1[o["nat"]])
+        for q in range(0, len(o["nat"]), 7):  # rows bit-exact (every 7th: the dump is large)
+            row = o["nat"][q]
+            assert np.array_equal(np.sort(o["v"][o["rp"][q]:o["rp"][q + 1]].view(np.int64)),
+                                  np.sort(v1[rp1[row]:rp1[row + 1]].view(np.int64)))
+        du[o["nat"]] = o["du"]
+    assert np.linalg.norm(du - ref.du()) <= 1e-10 * np.linalg.norm(ref.du())
+
+
+def test_back_to_back_halos():
+    """Halo exchanges with no all-reduce between them (set_strains twice, then SpMVs back to
+    back): each exchange's device copies into a rank's receive buffer are ordered after that
+    rank's previous unpack, so every product is the one-rank oracle's, bit for bit."""
+    NX, NY, NZ = 20, 12, 10
+    argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", 2, "-da_processors_y", 2,
+            "-da_processors_z", 2]
+    ref = O.Problem(NX, NY, NZ)
+    ref.apply_bc_u(ref.get_displacement(1))
+    ref.set_strains(); ref.homogenize(); ref.assembly_res(); ref.assembly_jac()
+    rng = np.random.default_rng(31)
+    xs = [rng.uniform(-1, 1, ref.ndofs) for _ in range(4)]
+    ys = [ref.spmv(x) for x in xs]
+
+    def fn(m):
+        m.apply_bc_on_u(m.get_displacement(1))
+        m.set_strains()
+        e1 = m.strain()
+        m.set_strains()
+        e2 = m.strain()
+        m.homogenize()
+        m.assembly_res()
+        m.assembly_jac()
+        _, nat = m.owned_dofs()
+        out = [m.spmv(x[nat]) for x in xs]
+        return dict(nat=nat, same=np.array_equal(e1, e2), b=m.b(), y=out)
+
+    out = run_group(argv, 8, fn)
+    b = np.zeros(ref.ndofs)
+    for o in out:
+        assert o["same"]
+        b[o["nat"]] = o["b"]
+        for y, yr in zip(o["y"], ys):
+            assert np.array_equal(y, yr[o["nat"]])
+    assert np.array_equal(b, ref.b())

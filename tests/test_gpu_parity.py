@@ -446,3 +446,36 @@ def test_aij_split_tile_shapes(NX, NY, NZ):
             ys.append(y)
         for y in ys[1:]:
             assert np.array_equal(y, ys[0])
+
+
+@pytest.mark.parametrize("NX,NY,NZ,tile", [(260, 6, 5, (256, 4)), (130, 9, 6, (128, 8))])
+def test_aij_vi_production_tiles(NX, NY, NZ, tile):
+    """The headline kernel at the tile shapes it runs at full size (k_spmv_vibm 256x4 from nx 256
+    on, 128x8 from nx 128 on), with partial tiles in x (260 = 256 + 4, 130 = 128 + 2) and y
+    (6 = 4 + 2 rows, 9 = 8 + 1): matrix dump and SpMV bit-exact with the oracle's CPU AIJ
+    (MatMult_SeqAIJ order, the MATAIJ matrix of src/init.c:92 applied by KSPSolve,
+    src/assembly.c:179-192) for several z-chunkings, the solve within the north-star bar."""
+    rtol = 1e-12
+    P = O.Problem(NX, NY, NZ, rtol=rtol)
+    with M.Macroc(argv_for(NX, NY, NZ, rtol)) as m:
+        m.set_option("vi_stage", 1)  # the grid is too flat for the default rule (>= 4 planes per chunk)
+        for ts in (0, 1):
+            m.apply_bc_on_u(m.get_displacement(ts))
+            P.apply_bc_u(P.get_displacement(ts))
+        m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
+        P.set_strains(); P.homogenize(); P.assembly_res(); P.assembly_jac()
+        info = m.get_info()
+        assert info["storage"] == 3 and info["vi_blocks"] > 0, info
+        assert (info["spmv_tx"], info["spmv_ty"]) == tile, info
+        assert np.array_equal(m.dump_csr()[2], P.A_values())
+        x = np.random.default_rng(17).uniform(-1, 1, m.n)
+        y_ref = P.spmv(x)
+        for zblocks in (0, 1, 2, 3 * NZ):  # chunks of 1, NZ, NZ/2, ... planes per tile
+            m.set_option("spmv_zblocks", zblocks)
+            assert np.array_equal(m.spmv(x), y_ref), zblocks
+        m.set_option("spmv_zblocks", 1)  # every tile marches all planes: the prefetch ring end to end
+        assert m.get_info()["spmv_kc"] == NZ
+        its, rn, reason = m.solve_Ax()
+        out = P.solve()
+        assert reason == out["reason"] and abs(its - out["its"]) <= 1
+        assert np.linalg.norm(m.du() - P.du()) <= 1e-10 * np.linalg.norm(P.du())
