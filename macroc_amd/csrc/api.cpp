@@ -55,11 +55,14 @@ static int free_ctx(Ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
   void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
+                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf, c->halo.d_bnd};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->h_cg) (void)hipHostFree(c->h_cg);
+  for (void* h : {(void*)c->h_vib_keys, (void*)c->h_vib_map, (void*)c->h_vib_dict})
+    if (h) (void)hipHostFree(h);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->ev_a) (void)hipEventDestroy(c->ev_a);
   if (c->ev_b) (void)hipEventDestroy(c->ev_b);
@@ -150,7 +153,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
       (rc = dalloc(c, &c.eps, 6 * 8 * E)) || (rc = dalloc(c, &c.sig, 6 * 8 * E)) ||
       (rc = dalloc(c, &c.partials, c.partials_cap = 4 * std::max(max_spmv_blocks(c), node_blocks(c)) + 64)) ||
       (rc = dalloc(c, &c.red, 16)) || (rc = dalloc(c, &c.red_loc, 16)) || (rc = dalloc(c, &c.cg, 2)) ||
-      (rc = dalloc(c, &c.hist, (int64_t)o->ksp_max_it + 2)))
+      (rc = dalloc(c, &c.hist, (int64_t)o->ksp_max_it + 2)) || (rc = dalloc(c, &c.ke_uni, 576)))
     return rc;
   // per-GP tangent: only laws that hand one over (the isotropic elastic C is a kernel argument)
   c.partials2 = c.partials + c.partials_cap / 2;
@@ -768,7 +771,14 @@ static int ensure_VI(Ctx& c) {
   MCX_HIP(hipMalloc(&c.vi_keys, nk * sizeof(unsigned long long)));
   MCX_HIP(hipMalloc(&c.vi_slot, nk));
   MCX_HIP(hipMalloc(&c.vi_ctl, (5 + NSLOT) * sizeof(unsigned)));
-  c.device_bytes += idx_bytes + nd * 8 + VI_MAX * VIB_STRIDE * 8 + nk * 9 + (5 + NSLOT) * 4;
+  MCX_HIP(hipMalloc(&c.vib_keys, (NSLOT * VB_GSV + VI_HASH) * sizeof(unsigned long long)));
+  MCX_HIP(hipMalloc(&c.vib_ctl, 4 * sizeof(unsigned)));
+  MCX_HIP(hipHostMalloc((void**)&c.h_vib_keys, (NSLOT * VB_GSV + VI_HASH + 2) * sizeof(unsigned long long),
+                        hipHostMallocDefault));
+  MCX_HIP(hipHostMalloc((void**)&c.h_vib_map, VI_HASH, hipHostMallocDefault));
+  MCX_HIP(hipHostMalloc((void**)&c.h_vib_dict, VI_MAX * VIB_STRIDE * sizeof(double), hipHostMallocDefault));
+  c.device_bytes += idx_bytes + nd * 8 + VI_MAX * VIB_STRIDE * 8 + nk * 9 + (5 + NSLOT) * 4 +
+                    (NSLOT * VB_GSV + VI_HASH) * 8 + 16;
   return 0;
 }
 
@@ -778,6 +788,7 @@ int mcx_assembly_jac(void* ctx) {
   PhaseTimer t(c, PH_JAC);
   int rc;
   if (c.mat.law != MCX_LAW_ELASTIC) launch_element_ke(c);  // per-GP tangent: element matrices first
+  else launch_elastic_ke(c);  // one material, one element shape: one element matrix
   if (c.o.mat_type == MCX_MAT_AIJ && c.aij_vi && !c.vi_declined) {
     // value-indexed AIJ when the matrix has at most VI_MAX distinct values (the elastic law's
     // matrices); otherwise the next storage below
@@ -1373,6 +1384,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
   }
   if (!std::strcmp(name, "vi_block")) {  // takes effect at the next mcx_assembly_jac
     c.vi_block_on = value != 0.;
+    return 0;
+  }
+  if (!std::strcmp(name, "vib_onepass")) {  // takes effect at the next mcx_assembly_jac
+    c.vib_onepass = value != 0.;
     return 0;
   }
   if (!std::strcmp(name, "vi_xread")) {

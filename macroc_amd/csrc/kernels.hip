@@ -531,11 +531,27 @@ __global__ __launch_bounds__(TPB) void k_element_ke(Geo g, const double* __restr
   else ke_body<0>(g, le, a, ctan, Ke);
 }
 
+// The isotropic elastic law has one tangent C for every Gauss point, and the uniform grid one
+// element shape (unit-cube B, one wg), so every element's matrix is the same 24x24 Ke: its 64
+// blocks (a, bn) are evaluated once per assembly by ke_block — the arithmetic each element's
+// on-the-fly evaluation would repeat, so the assembled values are bit-identical — into
+// ke_uni[(a*8 + bn)*9 + r*3 + c], which matrix_block<false> then sums (a, bn wave-uniform: scalar
+// loads).  Round 2 re-evaluated ke_block for every element block of every assembled block.
+__global__ void k_elastic_ke(Geo g, Material mat, double* __restrict__ keu) {
+  const int t = threadIdx.x;
+  if (t >= 64) return;
+  double ke[9];
+  ke_block(g, mat, t >> 3, t & 7, ke);
+#pragma unroll
+  for (int q = 0; q < 9; q++) keu[t * 9 + q] = ke[q];
+}
+
 // One 3x3 block A(node g, node g+d) of the assembled matrix (MatSetValuesLocal(ADD) +
 // MatAssembly + MatZeroRowsColumns(diag = 1), src/assembly.c:106-112, src/bcs.c:341-347):
 // 0 + Ke_e1 + Ke_e2 + ... over the shared elements in ascending element order (the reference's
-// insertion order on one rank), each element block computed on the fly (elastic) or read from
-// the element matrices Ke (TABLE: laws with a per-GP tangent), then the Dirichlet rows / columns.
+// insertion order on one rank), each element block read from the elastic law's one element
+// matrix (Ke = ke_uni) or from the element matrices (TABLE: laws with a per-GP tangent, Ke =
+// [576][nelem]), then the Dirichlet rows / columns.
 template <bool TABLE>
 __device__ __forceinline__ void matrix_block(const Geo& g, const Material& mat, const double* __restrict__ Ke,
                                              int gi, int gj, int gk, int dx, int dy, int dz, double (&val)[9]) {
@@ -559,11 +575,10 @@ __device__ __forceinline__ void matrix_block(const Geo& g, const Material& mat, 
           const double* src = Ke + (int64_t)((a * 8 + bn) * 9) * g.nelem + le;
 #pragma unroll
           for (int q = 0; q < 9; q++) val[q] += src[(int64_t)q * g.nelem];
-        } else {
-          double ke[9];
-          ke_block(g, mat, a, bn, ke);
+        } else {  // the elastic law's one element matrix (k_elastic_ke: ke_block of every (a, bn))
+          const double* src = Ke + (a * 8 + bn) * 9;
 #pragma unroll
-          for (int q = 0; q < 9; q++) val[q] += ke[q];
+          for (int q = 0; q < 9; q++) val[q] += src[q];
         }
       }
     }
@@ -1614,8 +1629,21 @@ __global__ __launch_bounds__(TPB) void k_vi_collect(Geo g, Material mat, const d
 #pragma unroll
     for (int q = 0; q < 9; q++) {
       const unsigned long long key = (unsigned long long)__double_as_longlong(val[q]);
-      if (key == VI_EMPTY) full = true;
-      else vi_insert<LS>(s_keys[q], key, &full);
+      if (key == VI_EMPTY) {
+        full = true;
+        continue;
+      }
+      bool lfull = false;
+      vi_insert<LS>(s_keys[q], key, &lfull);
+      if (lfull) {
+        // more than LS values of one slot in this block: the slot cannot take nibble indices,
+        // but the whole matrix may still fit the byte dictionary, so the value goes straight to
+        // the global set (the per-slot sets are only kept for nibble indices)
+        bool gfull = false;
+        if (vi_insert<VI_HASH>(keys, key, &gfull) && atomicAdd(&ctl[0], 1u) >= (unsigned)VI_MAX) full = true;
+        if (gfull) full = true;
+        atomicOr(&ctl[2], 1u);
+      }
     }
   }
   if (full) s_over = 1;
@@ -1870,6 +1898,137 @@ __global__ __launch_bounds__(TPB) void k_vib_pack(Geo g, Material mat, const dou
   unsigned h = vi_hash(key) & (VI_HASH - 1);
   for (int probe = 0; probe < VI_HASH && s_bkeys[h] != key; probe++) h = (h + 1) & (VI_HASH - 1);
   I[(((int64_t)(n >> 6) * 2 + (nb >> 4)) * 64 + (n & 63)) * 16 + (nb & 15)] = s_bmap[h];
+}
+
+// ---- block-indexed storage in one pass over the blocks (round 3).  Round 2 evaluated every
+// matrix block three times (k_vi_collect, k_vib_collect, k_vib_pack) with a host round trip
+// after each of the first two.  Here every block is evaluated once:
+//   k_vib_build (thread = owned node x block position nb, 256 nodes per workgroup): the block's
+//     9 values go into per-slot LDS sets, the sets into per-slot global sets (VB_GSV entries,
+//     open addressing; an entry never moves once written, so its position is an exact 6-bit name
+//     of the value within its slot); the block's code nb << 54 | the 9 positions (6 bits each)
+//     is then exact too, and goes through an LDS set into the global block-code set, whose
+//     position (< VI_HASH) is written per (nb, node) [27][nown] (2 B);
+//   the host (one readback + sync) sorts each slot's values and the block codes into the
+//     dictionary (by block position, then the 9 values' ranks in their slots: the order round 2
+//     produced), and maps every block-set position to its dictionary index;
+//   k_vib_remap (thread = owned node) streams the 27 positions through that map into the 27
+//     index bytes ([n/64][2][n%64] x 16 B, as before).
+// ctl[0] = distinct blocks, ctl[1] = overflow (a set full, a NaN-pattern value, > VI_MAX blocks).
+
+// insert key into an open-addressing set; returns the key's position (new or found), -1 when the
+// probe budget is exhausted; *isnew when this call wrote it
+template <int SIZE>
+__device__ __forceinline__ int vi_insert_pos(unsigned long long* set, unsigned long long key, bool* isnew) {
+  unsigned h = vi_hash(key) & (SIZE - 1);
+  *isnew = false;
+  for (int probe = 0; probe < SIZE; probe++) {
+    const unsigned long long cur = __hip_atomic_load(&set[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (cur == key) return (int)h;
+    if (cur == VI_EMPTY) {
+      const unsigned long long old = atomicCAS(&set[h], VI_EMPTY, key);
+      if (old == VI_EMPTY) {
+        *isnew = true;
+        return (int)h;
+      }
+      if (old == key) return (int)h;
+    }
+    h = (h + 1) & (SIZE - 1);
+  }
+  return -1;
+}
+
+template <bool TABLE>
+__global__ __launch_bounds__(TPB) void k_vib_build(Geo g, Material mat, const double* __restrict__ Ke,
+                                                   unsigned long long* __restrict__ gsv,
+                                                   unsigned long long* __restrict__ gbk,
+                                                   unsigned short* __restrict__ bpos, unsigned* __restrict__ ctl) {
+  constexpr int LSV = 64, LSB = 64;
+  __shared__ unsigned long long s_v[9][LSV];
+  __shared__ unsigned char s_vp[9][LSV];
+  __shared__ unsigned long long s_b[LSB];
+  __shared__ unsigned short s_bp[LSB];
+  __shared__ unsigned s_over;
+  for (int t = threadIdx.x; t < 9 * LSV; t += TPB) (&s_v[0][0])[t] = VI_EMPTY;
+  for (int t = threadIdx.x; t < LSB; t += TPB) s_b[t] = VI_EMPTY;
+  if (threadIdx.x == 0) s_over = __hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_over) return;  // uniform: the build already overflowed
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  const int nb = blockIdx.y;
+  const bool own = n < g.nown;
+  bool bad = false, isnew;
+  int lp[9];
+  if (own) {
+    int i, j, k;
+    node_ijk(g, n, i, j, k);
+    double val[9];
+    matrix_block<TABLE>(g, mat, Ke, g.xs + i, g.ys + j, g.zs + k, nb % 3 - 1, (nb / 3) % 3 - 1, nb / 9 - 1, val);
+#pragma unroll
+    for (int q = 0; q < 9; q++) {
+      const unsigned long long key = (unsigned long long)__double_as_longlong(val[q]);
+      lp[q] = key == VI_EMPTY ? -1 : vi_insert_pos<LSV>(s_v[q], key, &isnew);
+      if (lp[q] < 0) bad = true;
+    }
+  }
+  if (bad) s_over = 1;
+  __syncthreads();
+  if (s_over) {
+    if (threadIdx.x == 0) atomicOr(&ctl[1], 1u);
+    return;
+  }
+  for (int t = threadIdx.x; t < 9 * LSV; t += TPB) {  // this group's values of each slot -> the slot's set
+    const int q = t / LSV;
+    const unsigned long long key = s_v[q][t % LSV];
+    if (key == VI_EMPTY) continue;
+    const int gp = vi_insert_pos<VB_GSV>(gsv + (nb * 9 + q) * VB_GSV, key, &isnew);
+    if (gp < 0) s_over = 1;
+    (&s_vp[0][0])[t] = (unsigned char)(gp < 0 ? 0 : gp);
+  }
+  __syncthreads();
+  if (s_over) {
+    if (threadIdx.x == 0) atomicOr(&ctl[1], 1u);
+    return;
+  }
+  int lb = 0;
+  if (own) {
+    unsigned long long code = (unsigned long long)nb << 54;
+#pragma unroll
+    for (int q = 0; q < 9; q++) code |= (unsigned long long)s_vp[q][lp[q]] << (6 * q);
+    lb = vi_insert_pos<LSB>(s_b, code, &isnew);
+    if (lb < 0) s_over = 1;
+  }
+  __syncthreads();
+  if (s_over) {
+    if (threadIdx.x == 0) atomicOr(&ctl[1], 1u);
+    return;
+  }
+  for (int t = threadIdx.x; t < LSB; t += TPB) {  // this group's block codes -> the block set
+    const unsigned long long key = s_b[t];
+    if (key == VI_EMPTY) continue;
+    const int gp = vi_insert_pos<VI_HASH>(gbk, key, &isnew);
+    if (gp < 0 || (isnew && atomicAdd(&ctl[0], 1u) >= (unsigned)VI_MAX)) atomicOr(&ctl[1], 1u);
+    s_bp[t] = (unsigned short)(gp < 0 ? 0 : gp);
+  }
+  __syncthreads();
+  if (own) bpos[(int64_t)nb * g.nown + n] = s_bp[lb];
+}
+
+// the 27 block-set positions of every owned node -> its 27 index bytes (+5 zero pad)
+__global__ __launch_bounds__(TPB) void k_vib_remap(Geo g, const unsigned short* __restrict__ bpos,
+                                                   const unsigned char* __restrict__ bmap, u32x4* __restrict__ I) {
+  __shared__ unsigned char s_map[VI_HASH];
+  for (int t = threadIdx.x; t < VI_HASH / 16; t += TPB)
+    reinterpret_cast<u32x4*>(s_map)[t] = reinterpret_cast<const u32x4*>(bmap)[t];
+  __syncthreads();
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  unsigned w[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+  for (int nb = 0; nb < 27; nb++) w[nb >> 2] |= (unsigned)s_map[bpos[(int64_t)nb * g.nown + n]] << (8 * (nb & 3));
+  u32x4* dst = I + (int64_t)(n >> 6) * 128 + (n & 63);
+  dst[0] = u32x4{w[0], w[1], w[2], w[3]};
+  dst[64] = u32x4{w[4], w[5], w[6], w[7]};
 }
 
 __device__ __forceinline__ double jacobi_inv(double d) {
@@ -2861,6 +3020,10 @@ void launch_residual(Ctx& c) {
 
 // every law but the isotropic elastic one hands over a per-GP tangent (ctan)
 static bool table_law(const Ctx& c) { return c.mat.law != MCX_LAW_ELASTIC; }
+// the element matrices matrix_block reads: per element (table laws) or the elastic law's one
+static const double* ke_src(const Ctx& c) { return table_law(c) ? c.Ke : c.ke_uni; }
+
+void launch_elastic_ke(Ctx& c) { hipLaunchKernelGGL(k_elastic_ke, dim3(1), dim3(64), 0, c.stream, c.g, c.mat, c.ke_uni); }
 
 // element matrices of a per-GP-tangent law (k_element_ke), read by the gathers below
 void launch_element_ke(Ctx& c) {
@@ -2871,20 +3034,20 @@ void launch_element_ke(Ctx& c) {
 
 void launch_gather_matrix(Ctx& c) {
   if (table_law(c))
-    hipLaunchKernelGGL(k_gather_matrix<true>, dim3(nblk(c.g.nown), 27), dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke,
+    hipLaunchKernelGGL(k_gather_matrix<true>, dim3(nblk(c.g.nown), 27), dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c),
                        c.V);
   else
-    hipLaunchKernelGGL(k_gather_matrix<false>, dim3(nblk(c.g.nown), 27), dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke,
+    hipLaunchKernelGGL(k_gather_matrix<false>, dim3(nblk(c.g.nown), 27), dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c),
                        c.V);
 }
 
 void launch_gather_matrix_sym(Ctx& c) {
   const int npad = c.g.PX * c.g.PY * c.g.PZ;
   if (table_law(c))
-    hipLaunchKernelGGL(k_gather_matrix_sym<true>, dim3(nblk(npad), 14), dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke,
+    hipLaunchKernelGGL(k_gather_matrix_sym<true>, dim3(nblk(npad), 14), dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c),
                        c.U, npad);
   else
-    hipLaunchKernelGGL(k_gather_matrix_sym<false>, dim3(nblk(npad), 14), dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke,
+    hipLaunchKernelGGL(k_gather_matrix_sym<false>, dim3(nblk(npad), 14), dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c),
                        c.U, npad);
 }
 
@@ -2895,9 +3058,9 @@ int build_split(Ctx& c, bool* exact) {
   MCX_HIP(hipMemsetAsync(c.d_mask, 0, 16 * sizeof(unsigned), c.stream));
   const dim3 grid(nblk(c.g.nown), 14);
   if (table_law(c))
-    hipLaunchKernelGGL(k_split_mask<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.U, c.d_mask);
+    hipLaunchKernelGGL(k_split_mask<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.U, c.d_mask);
   else
-    hipLaunchKernelGGL(k_split_mask<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.U, c.d_mask);
+    hipLaunchKernelGGL(k_split_mask<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.U, c.d_mask);
   unsigned hm[16];
   MCX_HIP(hipMemcpyAsync(hm, c.d_mask, sizeof(hm), hipMemcpyDeviceToHost, c.stream));
   MCX_HIP(hipStreamSynchronize(c.stream));
@@ -2951,9 +3114,9 @@ int build_split(Ctx& c, bool* exact) {
   if (dl.L) {
     MCX_HIP(hipMemsetAsync(c.D, 0, (size_t)c.npgroups * dl.Lq * 64 * 16, c.stream));
     if (table_law(c))
-      hipLaunchKernelGGL(k_split_pack<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.U, c.D, dl);
+      hipLaunchKernelGGL(k_split_pack<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.U, c.D, dl);
     else
-      hipLaunchKernelGGL(k_split_pack<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.U, c.D, dl);
+      hipLaunchKernelGGL(k_split_pack<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.U, c.D, dl);
   }
   return 0;
 }
@@ -2977,17 +3140,115 @@ static int ensure_vi_idx(Ctx& c, int64_t bytes_per_node) {
   return 0;
 }
 
+// single-pass block build (k_vib_build / k_vib_remap); ok = at most VI_MAX distinct blocks and no
+// set overflowed.  One host round trip: the sets come back, the dictionary and the position map
+// go up from pinned buffers that stay untouched until the next build's readback has synchronised.
+static int build_vib(Ctx& c, bool* ok) {
+  *ok = false;
+  const int64_t nsv = (int64_t)NSLOT * VB_GSV;
+  unsigned long long* gsv = c.vib_keys;
+  unsigned long long* gbk = c.vib_keys + nsv;
+  const int64_t need = (int64_t)27 * c.g.nown * sizeof(unsigned short);
+  if (need > c.vib_pos_bytes) {
+    if (c.vib_pos) {
+      MCX_HIP(hipStreamSynchronize(c.stream));
+      MCX_HIP(hipFree(c.vib_pos));
+      c.device_bytes -= c.vib_pos_bytes;
+      c.vib_pos = nullptr;
+    }
+    MCX_HIP(hipMalloc(&c.vib_pos, need));
+    c.vib_pos_bytes = need;
+    c.device_bytes += need;
+  }
+  MCX_HIP(hipMemsetAsync(c.vib_keys, 0xff, (nsv + VI_HASH) * sizeof(unsigned long long), c.stream));
+  MCX_HIP(hipMemsetAsync(c.vib_ctl, 0, 4 * sizeof(unsigned), c.stream));
+  const dim3 grid(nblk(c.g.nown), 27);
+  if (table_law(c))
+    hipLaunchKernelGGL(k_vib_build<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), gsv, gbk, c.vib_pos,
+                       c.vib_ctl);
+  else
+    hipLaunchKernelGGL(k_vib_build<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), gsv, gbk, c.vib_pos,
+                       c.vib_ctl);
+  unsigned long long* hk = c.h_vib_keys;
+  unsigned* hctl = reinterpret_cast<unsigned*>(hk + nsv + VI_HASH);
+  MCX_HIP(hipMemcpyAsync(hk, c.vib_keys, (nsv + VI_HASH) * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                         c.stream));
+  MCX_HIP(hipMemcpyAsync(hctl, c.vib_ctl, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  if (hctl[1] || hctl[0] > (unsigned)VI_MAX) return 0;
+  // each slot's values sorted by bit pattern; rank of every set position
+  std::vector<unsigned char> rank(nsv, 0);
+  std::vector<unsigned long long> all;
+  int maxper = 0;
+  for (int S = 0; S < NSLOT; S++) {
+    const unsigned long long* ks = hk + (int64_t)S * VB_GSV;
+    std::vector<unsigned long long> v;
+    for (int h = 0; h < VB_GSV; h++)
+      if (ks[h] != VI_EMPTY) v.push_back(ks[h]);
+    std::sort(v.begin(), v.end());
+    maxper = std::max(maxper, (int)v.size());
+    for (int h = 0; h < VB_GSV; h++)
+      if (ks[h] != VI_EMPTY) rank[(int64_t)S * VB_GSV + h] = (unsigned char)(std::lower_bound(v.begin(), v.end(), ks[h]) - v.begin());
+    all.insert(all.end(), v.begin(), v.end());
+  }
+  std::sort(all.begin(), all.end());
+  const int nvals = (int)(std::unique(all.begin(), all.end()) - all.begin());
+  // blocks ordered by (position nb, the 9 values' ranks from slot 8 down to slot 0): with <= 16
+  // values per slot this is round 2's key order (nb << 36 | rank nibbles)
+  std::vector<std::pair<unsigned long long, int>> blk;  // (order key, set position)
+  for (int h = 0; h < VI_HASH; h++) {
+    const unsigned long long code = hk[nsv + h];
+    if (code == VI_EMPTY) continue;
+    const int nb = (int)(code >> 54);
+    unsigned long long key = (unsigned long long)nb << 54;
+    for (int q = 0; q < 9; q++) {
+      const int gp = (int)((code >> (6 * q)) & 63);
+      key |= (unsigned long long)rank[(int64_t)(nb * 9 + q) * VB_GSV + gp] << (6 * q);
+    }
+    blk.push_back({key, h});
+  }
+  std::sort(blk.begin(), blk.end());
+  std::memset(c.h_vib_map, 0, VI_HASH);
+  std::memset(c.h_vib_dict, 0, VI_MAX * VIB_STRIDE * sizeof(double));
+  for (size_t b = 0; b < blk.size(); b++) {
+    const unsigned long long code = hk[nsv + blk[b].second];
+    const int nb = (int)(code >> 54);
+    c.h_vib_map[blk[b].second] = (unsigned char)b;
+    for (int q = 0; q < 9; q++) {
+      const unsigned long long bits = hk[(int64_t)(nb * 9 + q) * VB_GSV + ((code >> (6 * q)) & 63)];
+      std::memcpy(&c.h_vib_dict[b * VIB_STRIDE + q], &bits, sizeof(double));
+    }
+  }
+  unsigned char* bmap = c.vi_slot + NSLOT * 32;
+  MCX_HIP(hipMemcpyAsync(bmap, c.h_vib_map, VI_HASH, hipMemcpyHostToDevice, c.stream));
+  MCX_HIP(hipMemcpyAsync(c.vi_bdict, c.h_vib_dict, VI_MAX * VIB_STRIDE * sizeof(double), hipMemcpyHostToDevice,
+                         c.stream));
+  if (int rc = ensure_vi_idx(c, 32)) return rc;
+  hipLaunchKernelGGL(k_vib_remap, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.vib_pos, bmap,
+                     reinterpret_cast<u32x4*>(c.vi_idx));
+  c.vi_n = nvals;
+  c.vi_bits = maxper <= 16 ? 4 : 8;
+  c.vi_nblocks = (int)blk.size();
+  c.vi_block = true;
+  *ok = true;
+  return 0;
+}
+
 int build_vi(Ctx& c, bool* ok) {
   *ok = false;
+  if (c.vi_block_on && c.vi_bits_max == 4 && c.vib_onepass) {
+    if (int rc = build_vib(c, ok)) return rc;
+    if (*ok) return 0;
+  }
   const bool table = table_law(c);
   MCX_HIP(hipMemsetAsync(c.vi_keys, 0xff, (VI_HASH + NSLOT * 32) * sizeof(unsigned long long), c.stream));
   MCX_HIP(hipMemsetAsync(c.vi_ctl, 0, (3 + NSLOT) * sizeof(unsigned), c.stream));
   unsigned long long* skeys = c.vi_keys + VI_HASH;
   const dim3 grid(nblk(c.g.nown), 27);
   if (table)
-    hipLaunchKernelGGL(k_vi_collect<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.vi_keys, skeys, c.vi_ctl);
+    hipLaunchKernelGGL(k_vi_collect<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.vi_keys, skeys, c.vi_ctl);
   else
-    hipLaunchKernelGGL(k_vi_collect<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.vi_keys, skeys, c.vi_ctl);
+    hipLaunchKernelGGL(k_vi_collect<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.vi_keys, skeys, c.vi_ctl);
   std::vector<unsigned> ctl(3 + NSLOT);
   std::vector<unsigned long long> keys(VI_HASH + NSLOT * 32);
   MCX_HIP(hipMemcpyAsync(ctl.data(), c.vi_ctl, ctl.size() * sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
@@ -3016,17 +3277,17 @@ int build_vi(Ctx& c, bool* ok) {
   MCX_HIP(hipMemcpyAsync(c.vi_slot, slot.data(), slot.size(), hipMemcpyHostToDevice, c.stream));
   MCX_HIP(hipMemcpyAsync(c.vi_dict, dict.data(), dict.size() * sizeof(double), hipMemcpyHostToDevice, c.stream));
   c.vi_block = false;
-  if (bits == 4 && c.vi_block_on) {  // one byte per 3x3 block when the blocks are few (k_vib_collect)
+  if (bits == 4 && c.vi_block_on && !c.vib_onepass) {  // one byte per 3x3 block when the blocks are few (k_vib_collect)
     unsigned long long* bkeys = c.vi_keys + VI_HASH + NSLOT * 32;
     unsigned char* bmap = c.vi_slot + NSLOT * 32;
     unsigned* bctl = c.vi_ctl + 3 + NSLOT;
     MCX_HIP(hipMemsetAsync(bkeys, 0xff, VI_HASH * sizeof(unsigned long long), c.stream));
     MCX_HIP(hipMemsetAsync(bctl, 0, 2 * sizeof(unsigned), c.stream));
     if (table)
-      hipLaunchKernelGGL(k_vib_collect<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, skeys, c.vi_slot, bkeys,
+      hipLaunchKernelGGL(k_vib_collect<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), skeys, c.vi_slot, bkeys,
                          bctl);
     else
-      hipLaunchKernelGGL(k_vib_collect<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, skeys, c.vi_slot, bkeys,
+      hipLaunchKernelGGL(k_vib_collect<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), skeys, c.vi_slot, bkeys,
                          bctl);
     unsigned bc[2];
     std::vector<unsigned long long> bk(VI_HASH);
@@ -3050,10 +3311,10 @@ int build_vi(Ctx& c, bool* ok) {
       MCX_HIP(hipMemcpyAsync(c.vi_bdict, bd.data(), bd.size() * sizeof(double), hipMemcpyHostToDevice, c.stream));
       if (int rc = ensure_vi_idx(c, 32)) return rc;
       if (table)
-        hipLaunchKernelGGL(k_vib_pack<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, skeys, c.vi_slot, bkeys,
+        hipLaunchKernelGGL(k_vib_pack<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), skeys, c.vi_slot, bkeys,
                            bmap, c.vi_idx);
       else
-        hipLaunchKernelGGL(k_vib_pack<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, skeys, c.vi_slot, bkeys,
+        hipLaunchKernelGGL(k_vib_pack<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), skeys, c.vi_slot, bkeys,
                            bmap, c.vi_idx);
       MCX_HIP(hipStreamSynchronize(c.stream));
       c.vi_n = (int)ctl[0];
@@ -3068,13 +3329,13 @@ int build_vi(Ctx& c, bool* ok) {
   u32x4* I = reinterpret_cast<u32x4*>(c.vi_idx);
   const dim3 pg(nblk(c.g.nown));
   if (bits == 8 && table)
-    hipLaunchKernelGGL((k_vi_pack<true, 8>), pg, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.vi_keys, c.vi_slot, I);
+    hipLaunchKernelGGL((k_vi_pack<true, 8>), pg, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.vi_keys, c.vi_slot, I);
   else if (bits == 8)
-    hipLaunchKernelGGL((k_vi_pack<false, 8>), pg, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, c.vi_keys, c.vi_slot, I);
+    hipLaunchKernelGGL((k_vi_pack<false, 8>), pg, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.vi_keys, c.vi_slot, I);
   else if (table)
-    hipLaunchKernelGGL((k_vi_pack<true, 4>), pg, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, skeys, c.vi_slot, I);
+    hipLaunchKernelGGL((k_vi_pack<true, 4>), pg, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), skeys, c.vi_slot, I);
   else
-    hipLaunchKernelGGL((k_vi_pack<false, 4>), pg, dim3(TPB), 0, c.stream, c.g, c.mat, c.Ke, skeys, c.vi_slot, I);
+    hipLaunchKernelGGL((k_vi_pack<false, 4>), pg, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), skeys, c.vi_slot, I);
   // the host copies above must outlive the async uploads
   MCX_HIP(hipStreamSynchronize(c.stream));
   c.vi_n = (int)ctl[0];

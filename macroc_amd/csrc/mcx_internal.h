@@ -79,6 +79,7 @@ constexpr int VI_MAX = 256;     // dictionary entries (one index byte per value)
 constexpr int VI_HASH = 4096;   // open-addressing set of the distinct values (bit patterns)
 constexpr int VI_CHUNKS = 16;   // 16-B index chunks per node: 243 slots + 13 zero pad bytes
 constexpr int VIB_STRIDE = 10;  // doubles per dictionary block (9 values + pad: 16-B aligned)
+constexpr int VB_GSV = 64;      // single-pass block build: entries of each slot's global value set (6-bit positions)
 
 // AIJ-split correction slots, passed by value: slot = nb*9 + r*3 + c of the row node's lower
 // block nb < 13 holds A(n, nb)[r][c] - U(m, 26-nb)[c][r], m = n + off(nb); nb = 13 (the
@@ -160,6 +161,18 @@ struct Ctx {
   int vi_block_on = 1;                    // option vi_block: try the block dictionary (needs nibbles)
   int vi_nblocks = 0;                     // distinct blocks of the current matrix (block mode)
   double* vi_bdict = nullptr;             // [VI_MAX][VIB_STRIDE] dictionary blocks
+  // single-pass block build (k_vib_build + k_vib_remap): per-slot value sets [NSLOT][VB_GSV] and
+  // the block-code set [VI_HASH] (one buffer), its control words, every (block position, owned
+  // node)'s block-set position [27][nown], and the pinned host images of what crosses PCIe
+  unsigned long long* vib_keys = nullptr;
+  unsigned* vib_ctl = nullptr;
+  unsigned short* vib_pos = nullptr;
+  int64_t vib_pos_bytes = 0;
+  unsigned long long* h_vib_keys = nullptr;  // readback: sets + ctl
+  unsigned char* h_vib_map = nullptr;        // upload: block-set position -> dictionary index [VI_HASH]
+  double* h_vib_dict = nullptr;              // upload: [VI_MAX][VIB_STRIDE]
+  int vib_onepass = 1;       // option vib_onepass: the single-pass block build (0: round 2's three passes)
+  double* ke_uni = nullptr;  // elastic law: the element matrix [8 a][8 b][9], the same for every element
   int aij_vi = 1;            // aij: assemble in FMT_VI when the matrix has at most VI_MAX distinct values
   int vi_xread = 1;          // staged block-indexed SpMV: x as unpaired 8-B LDS reads (option vi_xread; 0: compiler's pairs)
   int vi_stage = -1;         // FMT_VI SpMV: 1 = x staged in LDS, z-marching tiles; 0 = x gathered; -1 = by grid (vi_staged)
@@ -256,6 +269,7 @@ void launch_strains(Ctx& c);
 void launch_homogenize(Ctx& c);
 void launch_residual(Ctx& c);          // b + partial sums of b.b
 void launch_element_ke(Ctx& c);        // Ke of a per-GP-tangent law
+void launch_elastic_ke(Ctx& c);        // the elastic law's one element matrix (ke_uni)
 void launch_gather_matrix(Ctx& c);
 void launch_gather_matrix_sym(Ctx& c);
 int build_split(Ctx& c, bool* exact);  // AIJ-split corrections from U (exact = usable)

@@ -116,6 +116,15 @@ def test_aij_vi_single_rank(name):
         assert np.array_equal(m.spmv(x), y)
         # every slot takes <= 16 values and every block position few blocks: one byte per 3x3 block
         assert info["vi_bits"] == 4 and 0 < info["vi_blocks"] <= 256
+        # the single-pass block build (default) and round 2's three-pass build: the same
+        # dictionary order, so the same index bytes, matrix and products
+        m.set_option("vib_onepass", 0)
+        m.assembly_jac()
+        i3 = m.get_info()
+        assert (i3["vi_blocks"], i3["vi_values"], i3["vi_bits"]) == (info["vi_blocks"], info["vi_values"], 4)
+        assert np.array_equal(m.dump_csr()[2], v) and np.array_equal(m.spmv(x), y)
+        m.set_option("vib_onepass", 1)
+        m.assembly_jac()
         m.set_option("vi_block", 0)  # per-slot nibble indices: the same matrix and products
         m.assembly_jac()
         assert m.get_info()["vi_blocks"] == 0 and np.array_equal(m.dump_csr()[2], v)
