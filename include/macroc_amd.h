@@ -100,6 +100,11 @@ typedef struct {
                                   value into a dictionary of its distinct values when there are at most
                                   256 (value-indexed AIJ; rows summed in the CPU AIJ order, bit-exact
                                   SpMV); otherwise -mat_aij_split decides */
+  int mat_vi_fma;              /* -mat_vi_fma 0|1 (1): the value-indexed SpMV's z-marching kernel sums
+                                  each row with fused multiply-adds (one rounding per term, what a
+                                  PETSc built with -march=native does in MatMult), rows within
+                                  1e-14 sum|a_ij x_j| of the CPU AIJ order; 0: separate multiply and
+                                  add in the CPU AIJ order (bit-exact SpMV) */
 } mcx_opts;
 
 typedef struct {

@@ -58,6 +58,7 @@ class Opts(C.Structure):
         ("device", C.c_int), ("ksp_monitor", C.c_int), ("mat_type", C.c_int), ("mat_law", C.c_int),
         ("mat_aij_split", C.c_int),
         ("mat_aij_vi", C.c_int),
+        ("mat_vi_fma", C.c_int),
     ]
 
 

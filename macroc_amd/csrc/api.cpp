@@ -121,6 +121,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   c.g.ncu = c.ncu;
   c.aij_split = o->mat_type == MCX_MAT_AIJ && o->mat_aij_split;
   c.aij_vi = o->mat_type == MCX_MAT_AIJ && o->mat_aij_vi;
+  c.vi_fma = o->mat_vi_fma != 0;
   if (o->mat_type == MCX_MAT_SBAIJ) {
     // phased z-march 256x4 / 128x4 / 64x4 (128^3: 0.436 vs 0.502 ms for symz 128x2; 64^3:
     // 0.0555 vs 0.0625 ms for symz 64x4; profiles/r02_ab_sbaij{128,64}.log)
@@ -316,6 +317,7 @@ void mcx_default_opts(mcx_opts* o) {
   o->device = -1;
   o->mat_aij_split = 1;
   o->mat_aij_vi = 1;
+  o->mat_vi_fma = 1;
 }
 
 int mcx_parse_args(mcx_opts* o, int argc, const char* const* argv) {
@@ -358,7 +360,8 @@ int mcx_parse_args(mcx_opts* o, int argc, const char* const* argv) {
         D("-ksp_rtol", &o->ksp_rtol) || D("-ksp_atol", &o->ksp_abstol) || D("-ksp_divtol", &o->ksp_dtol) ||
         I("-ksp_max_it", &o->ksp_max_it) || I("-micro_n", &o->micro_n) || I("-micro_type", &o->micro_type) ||
         A4("-micro_mat_1", o->micro_mat_1) || A4("-micro_mat_2", o->micro_mat_2) || I("-device", &o->device) ||
-        I("-mat_aij_split", &o->mat_aij_split) || I("-mat_aij_vi", &o->mat_aij_vi))
+        I("-mat_aij_split", &o->mat_aij_split) || I("-mat_aij_vi", &o->mat_aij_vi) ||
+        I("-mat_vi_fma", &o->mat_vi_fma))
       continue;
     if (!std::strcmp(k, "-dm_mat_type")) {
       if (!v || (std::strcmp(v, "aij") && std::strcmp(v, "sbaij"))) {
@@ -1388,6 +1391,18 @@ int mcx_set_option(void* ctx, const char* name, double value) {
   }
   if (!std::strcmp(name, "vib_onepass")) {  // takes effect at the next mcx_assembly_jac
     c.vib_onepass = value != 0.;
+    return 0;
+  }
+  if (!std::strcmp(name, "vi_fma")) {
+    c.vi_fma = value != 0.;
+    return 0;
+  }
+  if (!std::strcmp(name, "vi_patch")) {
+    c.vi_patch = value != 0.;
+    return 0;
+  }
+  if (!std::strcmp(name, "vi_uni")) {
+    c.vi_uni = value != 0.;
     return 0;
   }
   if (!std::strcmp(name, "vi_xread")) {

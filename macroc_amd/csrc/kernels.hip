@@ -944,6 +944,7 @@ __global__ __launch_bounds__(TPB) void k_spmv_sym(Geo g, const double* __restric
 // products were routed, so the result is independent of tiling and rank grid.
 struct ZTiling {
   int ntx, nty, nzc, kc;  // tiles in x, y; z chunks and planes per chunk
+  int dbg = 0;            // timing-only diagnostics (k_spmv_vibm: 1 = every wave takes the scalar path)
 };
 
 static ZTiling z_tiling(const Geo& g, int ztx, int zty, int want) {
@@ -2116,12 +2117,23 @@ __global__ __launch_bounds__(TPB) void k_spmv_vib(Geo g, const u32x4* __restrict
 // in LDS beside it.  The gathered kernel (k_spmv_vib) spends most of its time in the 81 8-B x
 // loads per node at a 24-B lane stride; here x comes from LDS and HBM streams 32 B of indices
 // per node.  Same slot order and products as k_spmv: bit-identical to the CPU AIJ product.
-template <bool DOT, bool GATED, int TX, int TY, bool XV = true>
+// PATCH: a wave covers a 16 x 4 node patch of the tile instead of 64 nodes of one row, and the
+// staged rows are padded to RL = 16 mod 32 doubles (the two rows a 32-lane ds_read_b64 group reads
+// then fall on disjoint banks).  A tile row's two x-edge nodes then sit in 2 of the tile's 16
+// patches instead of 2 of its 4 row quarters: with UNI, 14 of 16 waves of an interior tile plane
+// take the scalar-dictionary path instead of 8 of 16.
+template <int TX, bool PATCH>
+constexpr int vibm_rl() {
+  return PATCH ? 3 * (TX + 2) + ((16 - (3 * (TX + 2)) % 32) + 32) % 32 : 3 * (TX + 2);
+}
+
+template <bool DOT, bool GATED, int TX, int TY, bool XV = true, bool UNI = false, bool PATCH = false, bool FMA = false>
 __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __restrict__ I,
                                                        const double* __restrict__ bdict, const double* __restrict__ x,
                                                        double* __restrict__ y, double* __restrict__ part,
                                                        const CgState* __restrict__ cg, ZTiling zt) {
-  constexpr int T = TX * TY, RL = 3 * (TX + 2), PR = TY + 2, PLANE = PR * RL;  // doubles per staged plane
+  static_assert(!PATCH || (TX % 16 == 0 && TY % 4 == 0 && TX * TY == 1024), "16 x 4 patches");
+  constexpr int T = TX * TY, RL = vibm_rl<TX, PATCH>(), PR = TY + 2, PLANE = PR * RL;  // doubles per staged plane
   constexpr int NL = (PLANE + T - 1) / T;                                      // x loads per thread per plane
   __shared__ double xs[3][PLANE];
   __shared__ double2 tab[VI_MAX * VIB_STRIDE / 2];
@@ -2141,7 +2153,10 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
   const int tyi = ty0 + r8 % nty_here, zc = r8 / nty_here;
   const int i0 = txi * TX, j0 = tyi * TY;
   const int k0 = zc * zt.kc, k1 = min(g.nz, k0 + zt.kc);
-  const int me = threadIdx.x, lx = me % TX, ly = me / TX;
+  const int me = threadIdx.x;
+  const int wv = me >> 6, ln = me & 63;
+  const int lx = PATCH ? (wv % (TX / 16)) * 16 + (ln & 15) : me % TX;
+  const int ly = PATCH ? (wv / (TX / 16)) * 4 + (ln >> 4) : me / TX;
   const int i = i0 + lx, j = j0 + ly;
   const bool inxy = i < g.nx && j < g.ny;
   const int PX = g.PX, PXY = g.PX * g.PY;
@@ -2182,7 +2197,75 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       for (int m = 0; m < NL; m++) xr[m] = xload(k + 2, m);
       iload(k + 1, n0, n1);
     }
-    if (inxy) {
+    // UNI: a wave whose 64 nodes have the same 27 block indices (interior x-lines: no domain
+    // boundary, no Dirichlet neighbour) reads the block values with scalar loads (s_load from
+    // the dictionary in global memory, scalar cache) and multiplies them as SGPR operands: the
+    // dictionary's 486 LDS cycles per wave and plane leave the LDS, which then only serves the x
+    // ring.  Other waves read the dictionary from LDS.  Same values, same products, same order.
+    unsigned sw[7] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    bool uni = false;
+    if (UNI) {
+#pragma unroll
+      for (int q = 0; q < 7; q++) sw[q] = __builtin_amdgcn_readfirstlane(q < 4 ? c0[q] : c1[q - 4]);
+      unsigned diff = 0u;
+#pragma unroll
+      for (int q = 0; q < 7; q++) diff |= (q < 4 ? c0[q] : c1[q - 4]) ^ sw[q];
+      uni = __all(inxy && diff == 0u) || (zt.dbg & 1);
+    }
+    if (UNI && uni) {  // (every lane is inxy)
+      double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+      typedef const volatile __attribute__((address_space(3))) double lds_vdouble;
+      lds_vdouble* xsv = (lds_vdouble*)&xs[0][0];
+      // blocks in groups of 3 (one dy row of the stencil): the 3 blocks' scalar loads are issued
+      // together and waited for once (an SMEM result can only be waited for with lgkmcnt(0), so
+      // a load issued ahead of the block in use would be waited for with it)
+#pragma unroll
+      for (int nb0 = 0; nb0 < 27; nb0 += 3) {
+        double av[3][9], xv[3][3];
+#pragma unroll
+        for (int t = 0; t < 3; t++) {
+          const int nb = nb0 + t;
+          const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
+          const int xo = ((k + dz - k0 + 1) % 3) * PLANE + (ly + 1 + dy) * RL + 3 * (lx + 1 + dx);
+          lds_vdouble* xp = xsv + xo;
+          xv[t][0] = xp[0];
+          xv[t][1] = xp[1];
+          xv[t][2] = xp[2];
+          const unsigned id = (sw[nb >> 2] >> (8 * (nb & 3))) & 255u;  // wave-uniform
+          const double* e = bdict + id * VIB_STRIDE;                    // values 0-7: one s_load_dwordx16
+#pragma unroll
+          for (int q = 0; q < 8; q++) av[t][q] = e[q];
+          // value 8 from the LDS copy (one broadcast ds_read_b64, 2 LDS cycles): an s_load_dwordx2
+          // per block needs an SGPR pair of its own, and the compiler reused one pair for every
+          // block, so each block's loads waited for the previous block's
+          av[t][8] = reinterpret_cast<const double*>(tab + id * (VIB_STRIDE / 2))[8];
+        }
+        // the group's loads first, then its products: one lgkmcnt(0) wait per group, while the
+        // SIMD's other waves compute (the scheduler would otherwise issue the next group's loads
+        // among these products, and the wait for one value would wait for those too)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < 3; t++) {
+          if (nb0 + t == 13) {
+            xc0 = xv[t][0];
+            xc1 = xv[t][1];
+            xc2 = xv[t][2];
+          }
+#pragma unroll
+          for (int q = 0; q < 9; q++) {
+            const int r = q / 3, cc = q % 3;
+            double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
+            yr = FMA ? __builtin_fma(av[t][q], xv[t][cc], yr) : yr + av[t][q] * xv[t][cc];
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
+      __builtin_nontemporal_store(y0, &y[3 * n + 0]);
+      __builtin_nontemporal_store(y1, &y[3 * n + 1]);
+      __builtin_nontemporal_store(y2, &y[3 * n + 2]);
+      if (DOT) dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
+    } else if (inxy) {
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
       // x as separate 8-B LDS reads (ds_read_b64: 2 LDS cycles each): the compiler would pair
       // them into ds_read2_b64, 8 cycles for the same 16 B (MI355X_MICROARCH.md, LDS table);
@@ -2219,9 +2302,8 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
 #pragma unroll
         for (int q = 0; q < 9; q++) {
           const int r = q / 3, cc = q % 3;
-          if (r == 0) y0 += a[q] * xv[cc];
-          else if (r == 1) y1 += a[q] * xv[cc];
-          else y2 += a[q] * xv[cc];
+          double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
+          yr = FMA ? __builtin_fma(a[q], xv[cc], yr) : yr + a[q] * xv[cc];
         }
       }
       const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
@@ -3418,29 +3500,42 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
   if (c.fmt == FMT_VI && c.vi_block) {
     const u32x4* I = reinterpret_cast<const u32x4*>(c.vi_idx);
     if (vi_staged(c)) {  // x staged in LDS, 1024-node tiles marching z-chunks
-      const ZTiling zt = vis_tiling(c);
+      ZTiling zt = vis_tiling(c);
+      zt.dbg = c.split_dbg;
       int tx, ty;
       vis_shape(c, tx, ty);
-#define MCX_VIBM(TXV, TYV, XVV)                                                                                       \
+#define MCX_VIBM(TXV, TYV, XVV, UV, PV, ...)                                                                          \
   do {                                                                                                             \
     if (dot && gated)                                                                                              \
-      hipLaunchKernelGGL((k_spmv_vibm<true, true, TXV, TYV, XVV>), dim3(nb), dim3(1024), 0, c.stream, c.g, I, c.vi_bdict, \
-                         xpad, y, c.partials, c.cg, zt);                                                           \
+      hipLaunchKernelGGL((k_spmv_vibm<true, true, TXV, TYV, XVV, UV, PV, ##__VA_ARGS__>), dim3(nb), dim3(1024), 0,        \
+                         c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt);                             \
     else if (dot)                                                                                                  \
-      hipLaunchKernelGGL((k_spmv_vibm<true, false, TXV, TYV, XVV>), dim3(nb), dim3(1024), 0, c.stream, c.g, I,            \
-                         c.vi_bdict, xpad, y, c.partials, c.cg, zt);                                               \
+      hipLaunchKernelGGL((k_spmv_vibm<true, false, TXV, TYV, XVV, UV, PV, ##__VA_ARGS__>), dim3(nb), dim3(1024), 0,       \
+                         c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt);                             \
     else                                                                                                           \
-      hipLaunchKernelGGL((k_spmv_vibm<false, false, TXV, TYV, XVV>), dim3(nb), dim3(1024), 0, c.stream, c.g, I,           \
-                         c.vi_bdict, xpad, y, c.partials, c.cg, zt);                                               \
+      hipLaunchKernelGGL((k_spmv_vibm<false, false, TXV, TYV, XVV, UV, PV, ##__VA_ARGS__>), dim3(nb), dim3(1024), 0,      \
+                         c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt);                             \
   } while (0)
-      if (c.vi_xread) {
-        if (tx == 256) MCX_VIBM(256, 4, true);
-        else if (tx == 128) MCX_VIBM(128, 8, true);
-        else MCX_VIBM(64, 16, true);
+      if (c.vi_fma) {
+        if (tx == 256) MCX_VIBM(256, 4, true, true, true, true);
+        else if (tx == 128) MCX_VIBM(128, 8, true, true, true, true);
+        else MCX_VIBM(64, 16, true, true, true, true);
+      } else if (c.vi_uni && c.vi_patch) {
+        if (tx == 256) MCX_VIBM(256, 4, true, true, true);
+        else if (tx == 128) MCX_VIBM(128, 8, true, true, true);
+        else MCX_VIBM(64, 16, true, true, true);
+      } else if (c.vi_uni) {
+        if (tx == 256) MCX_VIBM(256, 4, true, true, false);
+        else if (tx == 128) MCX_VIBM(128, 8, true, true, false);
+        else MCX_VIBM(64, 16, true, true, false);
+      } else if (c.vi_xread) {
+        if (tx == 256) MCX_VIBM(256, 4, true, false, false);
+        else if (tx == 128) MCX_VIBM(128, 8, true, false, false);
+        else MCX_VIBM(64, 16, true, false, false);
       } else {
-        if (tx == 256) MCX_VIBM(256, 4, false);
-        else if (tx == 128) MCX_VIBM(128, 8, false);
-        else MCX_VIBM(64, 16, false);
+        if (tx == 256) MCX_VIBM(256, 4, false, false, false);
+        else if (tx == 128) MCX_VIBM(128, 8, false, false, false);
+        else MCX_VIBM(64, 16, false, false, false);
       }
 #undef MCX_VIBM
       return;

@@ -174,6 +174,10 @@ struct Ctx {
   int vib_onepass = 1;       // option vib_onepass: the single-pass block build (0: round 2's three passes)
   double* ke_uni = nullptr;  // elastic law: the element matrix [8 a][8 b][9], the same for every element
   int aij_vi = 1;            // aij: assemble in FMT_VI when the matrix has at most VI_MAX distinct values
+  int vi_fma = 1;            // staged block-indexed SpMV: fused multiply-add rows (-mat_vi_fma, option vi_fma;
+                             // rounding-level, not bit-exact); implies vi_uni + vi_patch
+  int vi_patch = 1;          // with vi_uni: 16 x 4 node patches per wave (option vi_patch)
+  int vi_uni = 1;            // staged block-indexed SpMV: wave-uniform blocks from scalar loads (option vi_uni)
   int vi_xread = 1;          // staged block-indexed SpMV: x as unpaired 8-B LDS reads (option vi_xread; 0: compiler's pairs)
   int vi_stage = -1;         // FMT_VI SpMV: 1 = x staged in LDS, z-marching tiles; 0 = x gathered; -1 = by grid (vi_staged)
   bool vi_declined = false;  // a per-GP-tangent law overflowed the dictionary: skip the attempt

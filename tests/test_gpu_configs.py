@@ -59,18 +59,27 @@ def test_config3_256_cubed():
         # the same 256^3 matrix as AIJ stencil blocks (-mat_aij_vi 0 -mat_aij_split 0: every value
         # stored, rows in the CPU AIJ order, bit-exact with the oracle at small grids): the
         # value-indexed product is bit for bit the same
+        # (-mat_vi_fma 0: the value-indexed rows in the CPU AIJ order; the default fused
+        # multiply-adds differ from them by rounding only)
+        m.set_option("vi_fma", 0)
+        Ax_exact = m.spmv(x)
+        assert np.linalg.norm(Ax - Ax_exact) <= 1e-14 * np.linalg.norm(Ax_exact)
+        assert np.max(np.abs(Ax - Ax_exact)) <= 1e-12 * np.max(np.abs(Ax_exact))
         m.set_option("aij_vi", 0)
         m.set_option("aij_split", 0)
         m.assembly_jac()
         assert m.get_info()["storage"] == 0
-        assert np.array_equal(m.spmv(x), Ax)
+        assert np.array_equal(m.spmv(x), Ax_exact)
         m.set_option("aij_split", 1)
+        m.set_option("vi_fma", 1)
         # the AIJ-split storage of the same matrix: 24 exact bf16 correction slots, same solve
         m.set_option("aij_vi", 0)
         res3, its3, reason3, du3 = step()
         info = m.get_info()
         assert (info["storage"], info["split_slots"], info["split_bits"]) == (2, 24, 16)
-        assert res3 == res and abs(its3 - its) <= 1 and reason3 == 2
+        # the value-indexed rows use fused multiply-adds (-mat_vi_fma 1): rounding-level row
+        # differences move the iteration count by a few (2,818 vs 2,814 measured)
+        assert res3 == res and abs(its3 - its) <= 0.005 * its and reason3 == 2
         assert np.linalg.norm(m.spmv(du3) - b) <= 10 * rtol * np.linalg.norm(b)
 
 

@@ -254,12 +254,14 @@ def test_rccl_transport_one_rank():
     assert abs(r0 - r1) <= 1e-15 * r0
 
 
+@pytest.mark.parametrize("fma", [0, 1])
 @pytest.mark.parametrize("grid,procs", [((516, 5, 4), (2, 1, 1)), ((260, 9, 10), (1, 1, 2))])
-def test_multirank_vi_production_tiles(grid, procs):
+def test_multirank_vi_production_tiles(grid, procs, fma):
     """The value-indexed SpMV's 256x4 tiles on decomposed subdomains (258 = 256 + 2 wide, an
     internal x face at a partial tile's last lane; or a z split with internal z faces at the
-    chunk ends): every rank's matrix rows and SpMV bit-exact with the one-rank oracle (MATAIJ
-    MatMult, src/init.c:85-93), du within the north-star bar at rtol 1e-12."""
+    chunk ends): every rank's matrix rows bit-exact with the one-rank oracle, the SpMV too under
+    -mat_vi_fma 0 (MATAIJ MatMult, src/init.c:85-93) and within 1e-14 sum|a||x| with the default
+    fused multiply-adds; du within the north-star bar at rtol 1e-12."""
     NX, NY, NZ = grid
     px, py, pz = procs
     rtol = 1e-12
@@ -271,12 +273,16 @@ def test_multirank_vi_production_tiles(grid, procs):
     rp1, ci1 = ref.csr()
     x = np.random.default_rng(23).uniform(-1, 1, ref.ndofs)
     y1 = ref.spmv(x)
-    out = run_group(argv, px * py * pz, newton_step(x, [("vi_stage", 1)]))
+    absrow = np.add.reduceat(np.abs(v1) * np.abs(x[ci1]), rp1[:-1])
+    out = run_group(argv, px * py * pz, newton_step(x, [("vi_stage", 1), ("vi_fma", fma)]))
     du = np.zeros(ref.ndofs)
     for o in out:
         info = o["info"]
         assert info["storage"] == 3 and info["vi_blocks"] > 0 and (info["spmv_tx"], info["spmv_ty"]) == (256, 4), info
-        assert np.array_equal(o["y"], y1[o["nat"]])
+        if fma:
+            assert np.all(np.abs(o["y"] - y1[o["nat"]]) <= 1e-14 * absrow[o["nat"]] + 1e-300)
+        else:
+            assert np.array_equal(o["y"], y1[o["nat"]])
         for q in range(0, len(o["nat"]), 7):  # rows bit-exact (every 7th: the dump is large)
             row = o["nat"][q]
             assert np.array_equal(np.sort(o["v"][o["rp"][q]:o["rp"][q + 1]].view(np.int64)),

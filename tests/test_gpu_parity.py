@@ -145,13 +145,25 @@ def test_aij_vi_single_rank(name):
         m.set_option("vi_block", 1)
         m.assembly_jac()
         assert m.get_info()["vi_blocks"] > 0
-        # block dictionary: gathered x, staged x, marching; x read from LDS unpaired or paired
-        for stage, zblocks, xread in ((0, 0, 1), (1, 0, 1), (1, 1, 1), (1, 0, 0), (1, 1, 0)):
-            m.set_option("vi_stage", stage)
+        # block dictionary: gathered x, staged x, marching (-mat_vi_fma 0: products in the CPU AIJ
+        # order): wave-uniform blocks from scalar loads on 16x4 patches or row quarters, or every
+        # block from LDS with x read unpaired or paired — all bit-exact
+        rp_, ci_, v_ = m.dump_csr()
+        absrow = np.add.reduceat(np.abs(v_) * np.abs(x[ci_]), rp_[:-1])
+        for stage, zblocks, uni, patch, xread in ((0, 0, 1, 1, 1), (1, 0, 1, 1, 1), (1, 1, 1, 1, 1), (1, 0, 1, 0, 1),
+                                                  (1, 0, 0, 0, 1), (1, 1, 0, 0, 1), (1, 0, 0, 0, 0), (1, 1, 0, 0, 0)):
+            for k_, v_o in (("vi_fma", 0), ("vi_stage", stage), ("spmv_zblocks", zblocks), ("vi_uni", uni),
+                            ("vi_patch", patch), ("vi_xread", xread)):
+                m.set_option(k_, v_o)
+            assert np.array_equal(m.spmv(x), y), (stage, zblocks, uni, patch, xread)
+        # the default staged kernel sums with fused multiply-adds: rows within rounding of the
+        # CPU order, deterministic
+        for k_, v_o in (("vi_fma", 1), ("vi_uni", 1), ("vi_patch", 1), ("vi_xread", 1), ("vi_stage", 1)):
+            m.set_option(k_, v_o)
+        for zblocks in (0, 1):
             m.set_option("spmv_zblocks", zblocks)
-            m.set_option("vi_xread", xread)
-            assert np.array_equal(m.spmv(x), y), (stage, zblocks, xread)
-        m.set_option("vi_xread", 1)
+            yf = m.spmv(x)
+            assert np.all(np.abs(yf - y) <= 1e-14 * absrow + 1e-300) and np.array_equal(m.spmv(x), yf)
         m.set_option("vi_stage", -1)
         m.set_option("spmv_zblocks", 0)
         its, rn, reason = m.solve_Ax()
@@ -461,9 +473,11 @@ def test_aij_split_tile_shapes(NX, NY, NZ):
 def test_aij_vi_production_tiles(NX, NY, NZ, tile):
     """The headline kernel at the tile shapes it runs at full size (k_spmv_vibm 256x4 from nx 256
     on, 128x8 from nx 128 on), with partial tiles in x (260 = 256 + 4, 130 = 128 + 2) and y
-    (6 = 4 + 2 rows, 9 = 8 + 1): matrix dump and SpMV bit-exact with the oracle's CPU AIJ
-    (MatMult_SeqAIJ order, the MATAIJ matrix of src/init.c:92 applied by KSPSolve,
-    src/assembly.c:179-192) for several z-chunkings, the solve within the north-star bar."""
+    (6 = 4 + 2 rows, 9 = 8 + 1): matrix dump bit-exact, and the SpMV bit-exact with the
+    oracle's CPU AIJ (MatMult_SeqAIJ order, the MATAIJ matrix of src/init.c:92 applied by
+    KSPSolve, src/assembly.c:179-192) under -mat_vi_fma 0 for several z-chunkings and wave
+    layouts; the default fused multiply-add rows within 1e-14 sum|a||x|; the solve within the
+    north-star bar."""
     rtol = 1e-12
     P = O.Problem(NX, NY, NZ, rtol=rtol)
     with M.Macroc(argv_for(NX, NY, NZ, rtol)) as m:
@@ -476,12 +490,24 @@ def test_aij_vi_production_tiles(NX, NY, NZ, tile):
         info = m.get_info()
         assert info["storage"] == 3 and info["vi_blocks"] > 0, info
         assert (info["spmv_tx"], info["spmv_ty"]) == tile, info
-        assert np.array_equal(m.dump_csr()[2], P.A_values())
+        rp, ci, v = m.dump_csr()
+        assert np.array_equal(v, P.A_values())
         x = np.random.default_rng(17).uniform(-1, 1, m.n)
         y_ref = P.spmv(x)
+        absrow = np.add.reduceat(np.abs(v) * np.abs(x[ci]), rp[:-1])
         for zblocks in (0, 1, 2, 3 * NZ):  # chunks of 1, NZ, NZ/2, ... planes per tile
             m.set_option("spmv_zblocks", zblocks)
-            assert np.array_equal(m.spmv(x), y_ref), zblocks
+            # -mat_vi_fma 0: the CPU AIJ order, bit-exact (scalar-dictionary 16x4 patches, row
+            # quarters, every block from LDS); the default fused multiply-adds: within rounding
+            for uni, patch in ((1, 1), (1, 0), (0, 0)):
+                m.set_option("vi_fma", 0)
+                m.set_option("vi_uni", uni)
+                m.set_option("vi_patch", patch)
+                assert np.array_equal(m.spmv(x), y_ref), (zblocks, uni, patch)
+            m.set_option("vi_fma", 1)
+            yf = m.spmv(x)
+            assert np.all(np.abs(yf - y_ref) <= 1e-14 * absrow + 1e-300), zblocks
+            assert np.array_equal(m.spmv(x), yf)
         m.set_option("spmv_zblocks", 1)  # every tile marches all planes: the prefetch ring end to end
         assert m.get_info()["spmv_kc"] == NZ
         its, rn, reason = m.solve_Ax()
