@@ -10,11 +10,13 @@ the same state, nothing is cached across steps.  Workload: 256^3 nodes per GPU
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-The headline storage is the default AIJ one: value-indexed (one index byte per matrix value into
-a dictionary of the matrix's distinct values, rebuilt by every assembly inside the step; exact,
-rows in the CPU AIJ order).  On one GPU the AIJ-split storage of the same matrix is measured
-after it (1 warmup + 1 step, `variants` in the line; `--variants aij-split,aij-blocks,sbaij`
-for more) while the `--budget` wall time lasts.  Rank 0 prints ONE JSON line (the contract in
+The headline storage is the default AIJ one: value-indexed (one index byte per 3x3 block into
+a dictionary of the matrix's distinct blocks, rebuilt by every assembly inside the step; exact
+values), its SpMV rows summed with fused multiply-adds (-mat_vi_fma 1, the default).  On one GPU
+the same storage with the bit-exact CPU-order rows (-mat_vi_fma 0) and the AIJ-split storage
+of the same matrix are measured after it (1 warmup + 1 step each, `variants` in the line;
+`--variants aij-vi-exact,aij-split,aij-blocks,sbaij` for more) while the `--budget` wall time
+lasts.  Rank 0 prints ONE JSON line (the contract in
 the task statement / DESIGN.md §6) once the headline, the variants and the CPU baseline are
 measured.
 """
@@ -43,7 +45,8 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # value-indexed (one index byte per value into the matrix's <= 256 distinct values; the default,
 # with fallback), as upper blocks + exact bf16 lower corrections (aij-split) or as plain AIJ blocks
 # summed in the CPU AIJ order; -dm_mat_type sbaij through DMSetFromOptions (src/init.c:93)
-STORAGE_ARGS = {"aij": ["-dm_mat_type", "aij"], "aij-split": ["-dm_mat_type", "aij", "-mat_aij_vi", 0],
+STORAGE_ARGS = {"aij": ["-dm_mat_type", "aij"], "aij-vi-exact": ["-dm_mat_type", "aij", "-mat_vi_fma", 0],
+                "aij-split": ["-dm_mat_type", "aij", "-mat_aij_vi", 0],
                 "aij-blocks": ["-dm_mat_type", "aij", "-mat_aij_vi", 0, "-mat_aij_split", 0],
                 "sbaij": ["-dm_mat_type", "sbaij"]}
 STORAGE_NAME = {0: "aij-blocks", 1: "sbaij", 2: "aij-split", 3: "aij-vi"}
@@ -53,12 +56,17 @@ KERNEL_NAME = {0: "k_spmv (AIJ stencil blocks, CPU AIJ row order)",
                3: "k_spmv_vi (value-indexed AIJ: index bytes + dictionary in LDS, CPU AIJ row order)",
                # value-indexed, one byte per 3x3 block (vi_blocks > 0): z-marching x ring in LDS
                # where a tile marches >= 4 planes (k_spmv_vibm), else x gathered (k_spmv_vib)
-               "3b": "k_spmv_vibm (block-indexed AIJ: one byte per 3x3 block, block dictionary + x ring in "
-                     "LDS, CPU AIJ row order)"}
+               "3b": "k_spmv_vibm (block-indexed AIJ: one byte per 3x3 block; x ring in LDS; wave-uniform blocks "
+                     "from scalar loads, others from the dictionary in LDS; 16x4-node waves; rows summed with fused "
+                     "multiply-adds)",
+               "3be": "k_spmv_vibm (block-indexed AIJ as above, -mat_vi_fma 0: multiply then add in the CPU AIJ "
+                      "row order, bit-exact)"}
 
 
 def kernel_name(r):
-    return KERNEL_NAME["3b" if r["storage_id"] == 3 and r["vi_blocks"] else r["storage_id"]]
+    if r["storage_id"] == 3 and r["vi_blocks"]:
+        return KERNEL_NAME["3be" if r.get("exact") else "3b"]
+    return KERNEL_NAME[r["storage_id"]]
 
 
 def log(*a):
@@ -84,21 +92,27 @@ def pmc_traffic(mat_type, NX, NY, NZ):
 
 
 def lds_limiter(mat_type, NX, NY, NZ):
-    """LDS-array busy fraction of the headline SpMV kernel from the committed rocprofv3 SQ counter
-    passes (profiles/pmc_vibm.json, tools/pmc_vibm.sh: SQ_LDS_IDX_ACTIVE per CU / SQ_BUSY_CYCLES per
-    shader engine), or None.  The value-indexed kernel streams only ~80 B per node from HBM; its
-    limiter is the LDS (x ring + block dictionary reads), which this reports beside the HBM roofline."""
+    """LDS-array and VALU busy fractions of the headline SpMV kernel from the committed rocprofv3
+    SQ counter passes (profiles/pmc_vibm.json, tools/pmc_vibm.sh: SQ_LDS_IDX_ACTIVE per CU and
+    SQ_ACTIVE_INST_VALU per SIMD over SQ_BUSY_CYCLES per shader engine), or None.  The
+    value-indexed kernel streams only ~80 B per node from HBM; what bounds it is reported beside
+    the HBM roofline."""
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_vibm.json")
     try:
         with open(path) as f:
             e = json.load(f).get(f"{mat_type}:{NX}x{NY}x{NZ}")
         if not e:
             return None
-        return {"resource": "LDS", "busy_frac": e["lds_busy_frac"], "kernel": e["kernel"],
-                "valu_insts_per_wave_plane": e["valu_insts_per_wave_plane"],
-                "lds_insts_per_wave_plane": e["lds_insts_per_wave_plane"],
-                "source": "profiles/pmc_vibm.json (committed SQ counter passes, not measured by this run)",
-                "measured": e.get("measured")}
+        busy = {"LDS": e["lds_busy_frac"], "VALU": e.get("valu_busy_frac")}
+        out = {"resource": "latency (no unit saturated)" if max(v or 0 for v in busy.values()) < 0.7 else
+               max(busy, key=lambda k: busy[k] or 0),
+               "lds_busy_frac": e["lds_busy_frac"], "valu_busy_frac": e.get("valu_busy_frac"),
+               "wait_any_frac": e.get("wait_any_frac"), "kernel": e["kernel"],
+               "valu_insts_per_wave_plane": e["valu_insts_per_wave_plane"],
+               "lds_insts_per_wave_plane": e["lds_insts_per_wave_plane"],
+               "source": "profiles/pmc_vibm.json (committed SQ counter passes, not measured by this run)",
+               "measured": e.get("measured")}
+        return out
     except (OSError, ValueError, KeyError):
         return None
 
@@ -265,6 +279,7 @@ def measure(argv, rank, world, comm_id, args, steps, warmup):
     # PETSc AIJ bytes of the same SpMV (int32 col, int64 rowptr, x once, y once): SURVEY §8(d)
     csr_bytes = info["nnz_local"] * 12 + (nloc + 1) * 8 + 2 * nloc * 8
     return {"its": its, "tm": tm, "info": info, "check": check, "spmv_avg_ms": spmv_avg_ms, "spmv_bytes": spmv_bytes,
+            "exact": "-mat_vi_fma" in [str(a) for a in argv],
             "csr_bytes": csr_bytes, "storage": STORAGE_NAME[storage["storage"]], "storage_id": storage["storage"],
             "split_slots": storage["split_slots"], "split_bits": storage["split_bits"],
             "vi_values": storage["vi_values"], "vi_bits": storage["vi_bits"], "vi_blocks": storage["vi_blocks"],
@@ -298,7 +313,7 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.variants is None:
-        args.variants = "aij-split" if world == 1 and args.mat_type == "aij" else ""
+        args.variants = "aij-vi-exact,aij-split" if world == 1 and args.mat_type == "aij" else ""
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -368,7 +383,9 @@ def main():
                        "dofs": ndofs, "nnz": info["nnz_global"], "parallelism": f"dmda{px}x{py}x{pz}",
                        "mat_type": "aij" if args.mat_type.startswith("aij") else "sbaij", "storage": r["storage"],
                        "split_slots": r["split_slots"], "split_bits": r["split_bits"],
-                       "vi_values": r["vi_values"], "vi_bits": r["vi_bits"], "vi_blocks": r["vi_blocks"]},
+                       "vi_values": r["vi_values"], "vi_bits": r["vi_bits"], "vi_blocks": r["vi_blocks"],
+                       "spmv_rows": "fused multiply-add (-mat_vi_fma 1)" if r["storage_id"] == 3 and not r["exact"]
+                       else "multiply, add (CPU AIJ order)"},
             "cg_its": its,
             "ms_per_cg_iter": tm["solve_ms"] / max(its, 1),
             # CG iterations grow ~linearly with the global grid edge (720 at 64^3, 2814 at 256^3),
