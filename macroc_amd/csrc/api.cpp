@@ -55,7 +55,7 @@ static int free_ctx(Ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
   void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
-                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni,
+                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf, c->halo.d_bnd};
   for (void* p : ptrs)
@@ -195,12 +195,14 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
 // ---------------------------------------------------------------- phases
 static int cg_solve(Ctx& c, int* its, double* rnorm, int* reason) {
   launch_jacobi(c);  // PCSetUp_Jacobi happens inside KSPSolve in the reference
+  c.fusep_used = false;  // set by cg_iteration when the p update runs inside the SpMV
   CgState s{};
   s.rtol = c.o.ksp_rtol;
   s.abstol = c.o.ksp_abstol;
   s.dtol = c.o.ksp_dtol;
   s.maxits = c.o.ksp_max_it;
   s.hist_on = c.o.ksp_monitor ? 1 : 0;
+  s.xp = -1;
   c.h_cg[0] = s;
   MCX_HIP(hipMemcpyAsync(c.cg, &c.h_cg[0], sizeof(CgState), hipMemcpyHostToDevice, c.stream));
   launch_cg_init(c);
@@ -1302,6 +1304,8 @@ int mcx_get_timing(void* ctx, mcx_timing* t) {
                          : c.nupper_local * 8) +
       2 * 3 * (int64_t)c.g.nown * 8;
   if (c.fmt == FMT_SPLIT) t->spmv_bytes_per_launch += (int64_t)c.g.nown * c.dsl.Lq * 16;
+  // the fused p update (cg_fusep): r and the diagonal index read, p(i) written
+  if (c.fusep_used) t->spmv_bytes_per_launch += (int64_t)c.g.nown * (24 + 1 + 24);
   return 0;
 }
 
@@ -1387,6 +1391,20 @@ int mcx_set_option(void* ctx, const char* name, double value) {
   }
   if (!std::strcmp(name, "vi_block")) {  // takes effect at the next mcx_assembly_jac
     c.vi_block_on = value != 0.;
+    return 0;
+  }
+  if (!std::strcmp(name, "vi_tx")) {
+    c.vi_tx = (int)value;
+    if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
+      set_error("vi_tx: partials buffer too small");
+      return 7;
+    }
+    return 0;
+  }
+  if (!std::strcmp(name, "cg_fusep")) {  // the second p buffer is allocated on first use
+    c.cg_fusep = value != 0.;
+    if (c.cg_fusep && !c.p_pad2 && c.nranks == 1 && !c.comm && !c.lg)
+      return dalloc(c, &c.p_pad2, (int64_t)c.g.PX * c.g.PY * c.g.PZ * 3);
     return 0;
   }
   if (!std::strcmp(name, "vib_onepass")) {  // takes effect at the next mcx_assembly_jac

@@ -2117,6 +2117,23 @@ __global__ __launch_bounds__(TPB) void k_spmv_vib(Geo g, const u32x4* __restrict
 // in LDS beside it.  The gathered kernel (k_spmv_vib) spends most of its time in the 81 8-B x
 // loads per node at a 24-B lane stride; here x comes from LDS and HBM streams 32 B of indices
 // per node.  Same slot order and products as k_spmv: bit-identical to the CPU AIJ product.
+// FP: the CG's p update (VecAYPX) fused into the SpMV's staging of p (single rank,
+// value-indexed block storage, Jacobi from the diagonal index).  The kernel of CG iteration i
+// reads p(i-1) from pb[(i-1)&1], r and the index bytes while it marches, computes
+// p(i) = z + (beta/betaold) p(i-1) with z = r D^-1 (p(0) = z) for every staged node — its own and
+// the halo rows of the neighbouring tiles alike, the operations k_cg_pupdate performs — writes
+// p(i) of its own nodes to pb[i&1] and multiplies the staged p(i).  p is double-buffered because
+// a tile reads its neighbours' p(i-1) while they write their p(i); the two buffers also let
+// VecAXPY(x) run every second iteration in the update kernel (k_cg_update_x: x + a(i-1) p(i-1)
+// + a(i) p(i), in PETSc's order).  Results are bitwise those of k_cg_pupdate + k_spmv_vibm +
+// k_cg_update; p is read once per iteration instead of twice, x half as often.
+struct FusedP {
+  const double* r = nullptr;
+  const double* jdd = nullptr;          // [VI_MAX][3] inverse diagonals of the dictionary blocks
+  const unsigned char* jix = nullptr;   // owned nodes' diagonal-block index
+  double* pb[2] = {nullptr, nullptr};   // padded p, double-buffered
+};
+
 // PATCH: a wave covers a 16 x 4 node patch of the tile instead of 64 nodes of one row, and the
 // staged rows are padded to RL = 16 mod 32 doubles (the two rows a 32-lane ds_read_b64 group reads
 // then fall on disjoint banks).  A tile row's two x-edge nodes then sit in 2 of the tile's 16
@@ -2127,17 +2144,19 @@ constexpr int vibm_rl() {
   return PATCH ? 3 * (TX + 2) + ((16 - (3 * (TX + 2)) % 32) + 32) % 32 : 3 * (TX + 2);
 }
 
-template <bool DOT, bool GATED, int TX, int TY, bool XV = true, bool UNI = false, bool PATCH = false, bool FMA = false>
+template <bool DOT, bool GATED, int TX, int TY, bool XV = true, bool UNI = false, bool PATCH = false, bool FMA = false,
+          bool FP = false>
 __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __restrict__ I,
                                                        const double* __restrict__ bdict, const double* __restrict__ x,
                                                        double* __restrict__ y, double* __restrict__ part,
-                                                       const CgState* __restrict__ cg, ZTiling zt) {
+                                                       const CgState* __restrict__ cg, ZTiling zt, FusedP fp = {}) {
   static_assert(!PATCH || (TX % 16 == 0 && TY % 4 == 0 && TX * TY == 1024), "16 x 4 patches");
   constexpr int T = TX * TY, RL = vibm_rl<TX, PATCH>(), PR = TY + 2, PLANE = PR * RL;  // doubles per staged plane
   constexpr int NL = (PLANE + T - 1) / T;                                      // x loads per thread per plane
   __shared__ double xs[3][PLANE];
   __shared__ double2 tab[VI_MAX * VIB_STRIDE / 2];
   __shared__ double sh[T / 64];
+  __shared__ double s_jdd[FP ? 3 * VI_MAX : 1];
   if (GATED && cg->reason) return;
   const int b = blockIdx.x;
   const int xcd = b & 7, t8 = b >> 3;
@@ -2154,6 +2173,11 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
   const int i0 = txi * TX, j0 = tyi * TY;
   const int k0 = zc * zt.kc, k1 = min(g.nz, k0 + zt.kc);
   const int me = threadIdx.x;
+  // FP: the CG step's scalars and the p buffers of this iteration
+  const int cgi = FP ? cg->i : 0;
+  const double cb = FP ? cg->bcoef : 0.;
+  const double* psrc = FP ? fp.pb[(cgi & 1) ^ 1] : x;
+  double* pdst = FP ? fp.pb[cgi & 1] : nullptr;
   const int wv = me >> 6, ln = me & 63;
   const int lx = PATCH ? (wv % (TX / 16)) * 16 + (ln & 15) : me % TX;
   const int ly = PATCH ? (wv / (TX / 16)) * 4 + (ln >> 4) : me / TX;
@@ -2180,21 +2204,79 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       w1 = __builtin_nontemporal_load(ip + 64);
     }
   };
+  // FP staging of element me + m T of plane p: load p(i-1), r, the index byte and (own nodes) x;
+  // then p(i) into the ring (and, own nodes, to pb[i&1] and x).  Elements outside the domain are
+  // the zero ghost layer.
+  struct Fe {
+    double po, rv;
+    unsigned jx;
+  };
+  auto fload = [&](int p, int m, Fe& f) {
+    f.po = f.rv = 0.;
+    f.jx = 0u;
+    const int e = me + m * T;
+    const int rr = e / RL, o = e - rr * RL;
+    if (e >= PLANE || o >= len || rr >= rows) return;
+    const int gi = i0 - 1 + o / 3, gj = j0 - 1 + rr;
+    if (gi < 0 || gi >= g.nx || gj < 0 || gj >= g.ny || p < 0 || p >= g.nz) return;
+    const int64_t n = gi + (int64_t)g.nx * (gj + (int64_t)g.ny * p);
+    const int d = o - 3 * (o / 3);
+    f.rv = fp.r[3 * n + d];
+    f.jx = fp.jix[n];
+    if (cgi > 0) f.po = psrc[3 * (int64_t)(i0 + (j0 + rr) * PX + (p + 1) * PXY) + o];
+  };
+  auto fstore = [&](int slot, int p, int m, const Fe& f) {
+    int e = me + m * T;
+    // recompute the element's indices here instead of keeping fload's live across the plane's
+    // products (an opaque copy stops the compiler from reusing them: 128 VGPRs and spills else)
+    asm volatile("" : "+v"(e));
+    if (e >= PLANE) return;
+    const int rr = e / RL, o = e - rr * RL;
+    const int gi = i0 - 1 + o / 3, gj = j0 - 1 + rr;
+    double pn = 0.;
+    if (o < len && rr < rows && gi >= 0 && gi < g.nx && gj >= 0 && gj < g.ny && p >= 0 && p < g.nz) {
+      const int d = o - 3 * (o / 3);
+      const double z = f.rv * s_jdd[3 * f.jx + d];  // z = D^-1 r (k_cg_pupdate's z_of<DIX>)
+      pn = cgi == 0 ? z : z + cb * f.po;
+      if (gi >= i0 && gi < i0 + TX && gj >= j0 && gj < j0 + TY && p >= k0 && p < k1)
+        pdst[3 * (int64_t)(i0 + (j0 + rr) * PX + (p + 1) * PXY) + o] = pn;
+    }
+    xs[slot][e] = pn;
+  };
   for (int t = me; t < VI_MAX * VIB_STRIDE / 2; t += T) tab[t] = reinterpret_cast<const double2*>(bdict)[t];
+  if (FP) {
+    for (int t = me; t < 3 * VI_MAX; t += T) s_jdd[t] = fp.jdd[t];
+    __syncthreads();
 #pragma unroll
-  for (int s = 0; s < 3; s++)  // prologue: planes k0-1, k0, k0+1 in ring slots 0, 1, 2
+    for (int s = 0; s < 3; s++) {  // prologue: planes k0-1, k0, k0+1 in ring slots 0, 1, 2
+      Fe fe[NL];
 #pragma unroll
-    for (int m = 0; m < NL; m++) xstore(s, m, xload(k0 - 1 + s, m));
+      for (int m = 0; m < NL; m++) fload(k0 - 1 + s, m, fe[m]);
+#pragma unroll
+      for (int m = 0; m < NL; m++) fstore(s, k0 - 1 + s, m, fe[m]);
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 3; s++)  // prologue: planes k0-1, k0, k0+1 in ring slots 0, 1, 2
+#pragma unroll
+      for (int m = 0; m < NL; m++) xstore(s, m, xload(k0 - 1 + s, m));
+  }
   u32x4 c0 = {0u, 0u, 0u, 0u}, c1 = c0, n0 = c0, n1 = c0;
   iload(k0, c0, c1);
   __syncthreads();
   double dot = 0.;
   for (int k = k0; k < k1; k++) {
     const bool more = k + 1 < k1;
-    double xr[NL];
-    if (more) {  // in flight during this plane: x of plane k+2, indices of plane k+1
+    double xr[FP ? 1 : NL];
+    Fe fe[FP ? NL : 1];
+    if (more) {  // in flight during this plane: x (p) of plane k+2, indices of plane k+1
+      if (FP) {
 #pragma unroll
-      for (int m = 0; m < NL; m++) xr[m] = xload(k + 2, m);
+        for (int m = 0; m < NL; m++) fload(k + 2, m, fe[m]);
+      } else {
+#pragma unroll
+        for (int m = 0; m < NL; m++) xr[m] = xload(k + 2, m);
+      }
       iload(k + 1, n0, n1);
     }
     // UNI: a wave whose 64 nodes have the same 27 block indices (interior x-lines: no domain
@@ -2219,11 +2301,13 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       // blocks in groups of 3 (one dy row of the stencil): the 3 blocks' scalar loads are issued
       // together and waited for once (an SMEM result can only be waited for with lgkmcnt(0), so
       // a load issued ahead of the block in use would be waited for with it)
+      // (FP: one block per group, its SGPRs being needed for the fused p update's scalars)
+      constexpr int GB = FP ? 1 : 3;
 #pragma unroll
-      for (int nb0 = 0; nb0 < 27; nb0 += 3) {
-        double av[3][9], xv[3][3];
+      for (int nb0 = 0; nb0 < 27; nb0 += GB) {
+        double av[GB][9], xv[GB][3];
 #pragma unroll
-        for (int t = 0; t < 3; t++) {
+        for (int t = 0; t < GB; t++) {
           const int nb = nb0 + t;
           const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
           const int xo = ((k + dz - k0 + 1) % 3) * PLANE + (ly + 1 + dy) * RL + 3 * (lx + 1 + dx);
@@ -2245,7 +2329,7 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
         // among these products, and the wait for one value would wait for those too)
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int t = 0; t < 3; t++) {
+        for (int t = 0; t < GB; t++) {
           if (nb0 + t == 13) {
             xc0 = xv[t][0];
             xc1 = xv[t][1];
@@ -2314,8 +2398,13 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
     }
     if (more) {  // uniform
       __syncthreads();  // plane k-1's slot is free
+      if (FP) {
 #pragma unroll
-      for (int m = 0; m < NL; m++) xstore((k + 2 - k0 + 1) % 3, m, xr[m]);
+        for (int m = 0; m < NL; m++) fstore((k + 2 - k0 + 1) % 3, k + 2, m, fe[m]);
+      } else {
+#pragma unroll
+        for (int m = 0; m < NL; m++) xstore((k + 2 - k0 + 1) % 3, m, xr[m]);
+      }
       c0 = n0;
       c1 = n1;
       __syncthreads();
@@ -2650,10 +2739,18 @@ __global__ void k_cg_pupdate_list(Geo g, const double* __restrict__ z, const dou
   pupdate_node<NT, DIX>(g, list[t], z, dinv, jix, ppad, x, cg);
 }
 
-// the last iteration's x += alpha p (when that iteration reached its update)
-__global__ void k_cg_xfinal(Geo g, const double* __restrict__ ppad, double* __restrict__ x,
-                            const CgState* __restrict__ cg) {
-  if (!cg->xpend) return;
+// the last iteration's x += alpha p (when that iteration reached its update); ppad2: the fused
+// path's second p buffer (p of iteration i in buffer i & 1)
+__global__ void k_cg_xfinal(Geo g, const double* __restrict__ ppad, const double* __restrict__ ppad2,
+                            double* __restrict__ x, const CgState* __restrict__ cg) {
+  if (ppad2) {
+    // fused path: odd iterations' updates applied x through them, so only an even last
+    // successful iteration xp (whose update ran, but applies no x) leaves a(xp) p(xp) pending;
+    // an indefinite matrix stops before the update of xp + 1, cg->alpha is still a(xp)
+    if (cg->xp < 0 || (cg->xp & 1)) return;
+  } else if (!cg->xpend) {
+    return;
+  }
   int n = blockIdx.x * TPB + threadIdx.x;
   if (n >= g.nown) return;
   int i, j, k;
@@ -2690,6 +2787,57 @@ __global__ __launch_bounds__(UTPB) void k_cg_update(Geo g, const double* __restr
       if (!DIX) st<NT>(&z[q], zv);
       zz += zv * zv;
       zr += zv * rv;
+    }
+  }
+  double s0 = block_sum<UTPB>(zz, sh);
+  double s1 = block_sum<UTPB>(zr, sh);
+  if (threadIdx.x == 0) {
+    part[blockIdx.x] = s0;
+    part[nparts + blockIdx.x] = s1;
+  }
+}
+
+// the fused p-update path's update (FusedP): r += (-a) w; z = D^-1 r; partials z.z, z.r; and on
+// odd iterations i the two VecAXPYs of x that iterations i-1 and i owe, x = (x + a(i-1) p(i-1))
+// + a(i) p(i), from the two p buffers (p(i) in pb[i&1]) — the same operations, in the same
+// order, as KSPSolve_CG's VecAXPY(x) per iteration
+template <bool NT>
+__global__ __launch_bounds__(UTPB) void k_cg_update_x(Geo g, const double* __restrict__ w,
+                                                     const double* __restrict__ jdd,
+                                                     const unsigned char* __restrict__ jix, double* __restrict__ r,
+                                                     double* __restrict__ x, const double* __restrict__ pb0,
+                                                     const double* __restrict__ pb1, double* __restrict__ part,
+                                                     int nparts, const CgState* __restrict__ cg) {
+  __shared__ double sh[UTPB / 64];
+  if (cg->reason) return;
+  const double a = cg->alpha, ma = -a;
+  const int it = cg->i;
+  int n = blockIdx.x * UTPB + threadIdx.x;
+  double zz = 0., zr = 0.;
+  if (n < g.nown) {
+    const unsigned jx = jix[n];
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      const int q = 3 * n + d;
+      const double rv = r[q] + ma * w[q];
+      st<NT>(&r[q], rv);
+      const double zv = rv * jdd[3 * jx + d];
+      zz += zv * zv;
+      zr += zv * rv;
+    }
+    if (it & 1) {  // uniform
+      int i, j, k;
+      node_ijk(g, n, i, j, k);
+      const int pc = pad_of(g, i, j, k);
+      const double ap = cg->alpha_prev;
+      const double* pp = (it & 1) ? pb0 : pb1;  // p(i-1) (i odd: buffer 0)
+      const double* pi = (it & 1) ? pb1 : pb0;  // p(i)
+#pragma unroll
+      for (int d = 0; d < 3; d++) {
+        const int q = 3 * n + d;
+        const double x1 = x[q] + ap * pp[3 * pc + d];
+        st<NT>(&x[q], x1 + a * pi[3 * pc + d]);
+      }
     }
   }
   double s0 = block_sum<UTPB>(zz, sh);
@@ -2841,8 +2989,10 @@ __device__ void cg_logic_alpha(CgState* s, double dpi) {
     s->xpend = 0;
     return;
   }
+  s->alpha_prev = s->alpha;
   s->alpha = s->beta / dpi;
   s->xpend = 1;
+  s->xp = s->i;
 }
 
 __device__ void cg_logic_beta(CgState* s, double zz, double zr, double* hist) {
@@ -3013,8 +3163,13 @@ static void split_shape(const Ctx& c, int& ztx, int& zty) {
 
 // FMT_VI with x staged in LDS (k_spmv_vim): 1024-thread tiles TX x TY marching z-chunks, one
 // resident round of blocks (one per CU: the ring and the dictionaries fill the LDS)
+// 64x16 tiles: with the scalar-dictionary 16x4 patches, 256^3 0.358 vs 0.419 ms (256x4) and
+// 128^3 0.0563 vs 0.0589 ms (128x8) per SpMV (profiles/r03_ab_tx{256b,128}.log): a third less
+// halo than 256x4 (66x18 staged nodes per 1024 instead of 258x6), and tiles away from the x
+// faces have no wave that reads the dictionary from LDS.  Option vi_tx selects 256x4 / 128x8.
 static void vis_shape(const Ctx& c, int& tx, int& ty) {
-  tx = c.g.nx >= 256 ? 256 : (c.g.nx >= 128 ? 128 : 64);
+  tx = 64;
+  if (c.vi_tx == 256 || c.vi_tx == 128 || c.vi_tx == 64) tx = c.vi_tx;
   ty = 1024 / tx;
 }
 
@@ -3494,6 +3649,40 @@ static void launch_spmv_vi(Ctx& c, const double* xpad, double* y, bool dot, bool
                        c.partials, c.cg, tl);
 }
 
+// the CG iteration's p update fused into the value-indexed SpMV (FP, see FusedP): single rank,
+// block-indexed storage with x staged, Jacobi from the diagonal index, scalar-dictionary patches
+bool fusep(const Ctx& c) {
+  return c.cg_fusep && c.p_pad2 && c.nranks == 1 && !c.comm && !c.lg && c.fmt == FMT_VI && c.vi_block &&
+         vi_staged(c) && c.cg_dix && c.vi_uni && c.vi_patch;
+}
+
+static void launch_spmv_fusep(Ctx& c, double* y) {
+  const int nb = (int)spmv_grid_blocks(c);
+  const u32x4* I = reinterpret_cast<const u32x4*>(c.vi_idx);
+  ZTiling zt = vis_tiling(c);
+  int tx, ty;
+  vis_shape(c, tx, ty);
+  FusedP fp;
+  fp.r = c.r;
+  fp.jdd = c.jdd;
+  fp.jix = c.jix;
+  fp.pb[0] = c.p_pad;
+  fp.pb[1] = c.p_pad2;
+#define MCX_VIBM_FP(TXV, TYV, FV)                                                                                   \
+  hipLaunchKernelGGL((k_spmv_vibm<true, true, TXV, TYV, true, true, true, FV, true>), dim3(nb), dim3(1024), 0,        \
+                     c.stream, c.g, I, c.vi_bdict, c.p_pad, y, c.partials, c.cg, zt, fp)
+  if (c.vi_fma) {
+    if (tx == 256) MCX_VIBM_FP(256, 4, true);
+    else if (tx == 128) MCX_VIBM_FP(128, 8, true);
+    else MCX_VIBM_FP(64, 16, true);
+  } else {
+    if (tx == 256) MCX_VIBM_FP(256, 4, false);
+    else if (tx == 128) MCX_VIBM_FP(128, 8, false);
+    else MCX_VIBM_FP(64, 16, false);
+  }
+#undef MCX_VIBM_FP
+}
+
 void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
   const int nb = (int)spmv_grid_blocks(c);
   const SpmvTiling tl = spmv_tiling(c.g, c.spmv_subl);
@@ -3705,7 +3894,8 @@ int cg_finish_init(Ctx& c) {
 }
 
 void launch_cg_xfinal(Ctx& c) {
-  hipLaunchKernelGGL(k_cg_xfinal, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.p_pad, c.du, c.cg);
+  hipLaunchKernelGGL(k_cg_xfinal, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.p_pad,
+                     c.fusep_used ? c.p_pad2 : nullptr, c.du, c.cg);
 }
 
 // CG vector kernels' Jacobi form: DIX (block-indexed value storage, option cg_dix) reads one
@@ -3771,6 +3961,21 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) 
   const bool dix = cg_dix(c);
   const double* zs = dix ? c.r : c.z;
   const double* jd = dix ? c.jdd : c.dinv;
+  if (fusep(c) && !fa) {  // p update inside the SpMV (no k_cg_pupdate, no halo: single rank)
+    c.fusep_used = true;
+    if (ev0) MCX_HIP(hipEventRecord(ev0, c.stream));
+    launch_spmv_fusep(c, c.w);
+    if (ev1) MCX_HIP(hipEventRecord(ev1, c.stream));
+    rc = reduce_and_logic(c, 1, nbs, RED_ALPHA, true, c.partials, c.cg);
+    if (rc) return rc;
+    if (c.cg_nt)
+      hipLaunchKernelGGL(k_cg_update_x<true>, dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, c.jdd, c.jix, c.r, c.du,
+                         c.p_pad, c.p_pad2, c.partials2, nbu, c.cg);
+    else
+      hipLaunchKernelGGL(k_cg_update_x<false>, dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, c.jdd, c.jix, c.r, c.du,
+                         c.p_pad, c.p_pad2, c.partials2, nbu, c.cg);
+    return reduce_and_logic(c, 2, nbu, RED_BETA, true, c.partials2, c.cg);
+  }
   if (fb && !first) {
     MCX_NT_DIX(c.cg_nt, dix,
                hipLaunchKernelGGL((k_cg_pupdate_fb<NT, DX>), dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, zs, jd,

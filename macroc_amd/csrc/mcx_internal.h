@@ -43,6 +43,8 @@ struct CgState {
   double rtol, abstol, dtol;
   int i, its, reason, maxits, hist_on;
   int xpend;  // x += alpha p of the last iteration not yet applied (k_cg_pupdate / k_cg_xfinal apply it)
+  int xp;     // the last iteration whose alpha step succeeded (-1: none); the fused path's pending x update
+  double alpha_prev;  // alpha of the iteration before (the fused path's every-second-iteration x update)
 };
 
 struct Material {
@@ -131,6 +133,9 @@ struct Ctx {
   // device arrays
   double* u_pad = nullptr;   // displacement, padded ghosted box [PX*PY*PZ][3]
   double* p_pad = nullptr;   // CG search direction, padded
+  double* p_pad2 = nullptr;  // its second buffer (single rank: the p update fused into the SpMV, cg_fusep)
+  int cg_fusep = 0;          // option cg_fusep: fuse the CG p update into the value-indexed SpMV (single rank; A/B: no gain)
+  bool fusep_used = false;   // the last solve ran the fused kernel (timing: its bytes per launch)
   double* b = nullptr;       // residual (owned, PETSc-local order)
   double* du = nullptr;      // CG solution x
   double* r = nullptr;
@@ -177,6 +182,7 @@ struct Ctx {
   int vi_fma = 1;            // staged block-indexed SpMV: fused multiply-add rows (-mat_vi_fma, option vi_fma;
                              // rounding-level, not bit-exact); implies vi_uni + vi_patch
   int vi_patch = 1;          // with vi_uni: 16 x 4 node patches per wave (option vi_patch)
+  int vi_tx = 0;             // staged block-indexed SpMV tile width 256 | 128 | 64 (0: 64; option vi_tx)
   int vi_uni = 1;            // staged block-indexed SpMV: wave-uniform blocks from scalar loads (option vi_uni)
   int vi_xread = 1;          // staged block-indexed SpMV: x as unpaired 8-B LDS reads (option vi_xread; 0: compiler's pairs)
   int vi_stage = -1;         // FMT_VI SpMV: 1 = x staged in LDS, z-marching tiles; 0 = x gathered; -1 = by grid (vi_staged)
@@ -295,6 +301,7 @@ int64_t spmv_grid_blocks(const Ctx& c);
 int64_t spmv_nparts(const Ctx& c);   // partial sums the CG's SpMV leaves (its own grid, or the dense pass's)
 int64_t node_blocks(const Ctx& c);
 bool vi_staged(const Ctx& c);
+bool fusep(const Ctx& c);  // the CG's p update runs inside the value-indexed SpMV
 // z-marching SpMV tile of the current storage (tx, ty, planes per chunk); all 0 for gathered kernels
 void spmv_tile(const Ctx& c, int* tx, int* ty, int* kc);
 int dirichlet_mask_host(const Geo& g, int gi, int gj, int gk);

@@ -55,7 +55,7 @@ def test_config3_256_cubed():
         assert np.linalg.norm(Axy - (Ax + 2.0 * Ay)) <= 1e-13 * np.linalg.norm(np.abs(Ax) + 2.0 * np.abs(Ay))
         res2, its2, reason2, du2 = step()
         assert res2 == res and its2 == its and np.array_equal(du2, du)
-        assert (m.get_info()["spmv_tx"], m.get_info()["spmv_ty"]) == (256, 4)  # the headline instantiation
+        assert (m.get_info()["spmv_tx"], m.get_info()["spmv_ty"]) == (64, 16)  # the headline instantiation
         # the same 256^3 matrix as AIJ stencil blocks (-mat_aij_vi 0 -mat_aij_split 0: every value
         # stored, rows in the CPU AIJ order, bit-exact with the oracle at small grids): the
         # value-indexed product is bit for bit the same

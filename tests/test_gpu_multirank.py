@@ -254,11 +254,11 @@ def test_rccl_transport_one_rank():
     assert abs(r0 - r1) <= 1e-15 * r0
 
 
-@pytest.mark.parametrize("fma", [0, 1])
+@pytest.mark.parametrize("fma,vi_tx,tile", [(0, 0, (64, 16)), (1, 0, (64, 16)), (1, 256, (256, 4))])
 @pytest.mark.parametrize("grid,procs", [((516, 5, 4), (2, 1, 1)), ((260, 9, 10), (1, 1, 2))])
-def test_multirank_vi_production_tiles(grid, procs, fma):
-    """The value-indexed SpMV's 256x4 tiles on decomposed subdomains (258 = 256 + 2 wide, an
-    internal x face at a partial tile's last lane; or a z split with internal z faces at the
+def test_multirank_vi_production_tiles(grid, procs, fma, vi_tx, tile):
+    """The value-indexed SpMV's 64x16 (default) and 256x4 tiles on decomposed subdomains (258
+    wide: an internal x face at a partial tile's last lane; or a z split with internal z faces at the
     chunk ends): every rank's matrix rows bit-exact with the one-rank oracle, the SpMV too under
     -mat_vi_fma 0 (MATAIJ MatMult, src/init.c:85-93) and within 1e-14 sum|a||x| with the default
     fused multiply-adds; du within the north-star bar at rtol 1e-12."""
@@ -274,11 +274,11 @@ def test_multirank_vi_production_tiles(grid, procs, fma):
     x = np.random.default_rng(23).uniform(-1, 1, ref.ndofs)
     y1 = ref.spmv(x)
     absrow = np.add.reduceat(np.abs(v1) * np.abs(x[ci1]), rp1[:-1])
-    out = run_group(argv, px * py * pz, newton_step(x, [("vi_stage", 1), ("vi_fma", fma)]))
+    out = run_group(argv, px * py * pz, newton_step(x, [("vi_stage", 1), ("vi_fma", fma), ("vi_tx", vi_tx)]))
     du = np.zeros(ref.ndofs)
     for o in out:
         info = o["info"]
-        assert info["storage"] == 3 and info["vi_blocks"] > 0 and (info["spmv_tx"], info["spmv_ty"]) == (256, 4), info
+        assert info["storage"] == 3 and info["vi_blocks"] > 0 and (info["spmv_tx"], info["spmv_ty"]) == tile, info
         if fma:
             assert np.all(np.abs(o["y"] - y1[o["nat"]]) <= 1e-14 * absrow[o["nat"]] + 1e-300)
         else:

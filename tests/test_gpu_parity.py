@@ -469,11 +469,12 @@ def test_aij_split_tile_shapes(NX, NY, NZ):
             assert np.array_equal(y, ys[0])
 
 
-@pytest.mark.parametrize("NX,NY,NZ,tile", [(260, 6, 5, (256, 4)), (130, 9, 6, (128, 8))])
-def test_aij_vi_production_tiles(NX, NY, NZ, tile):
-    """The headline kernel at the tile shapes it runs at full size (k_spmv_vibm 256x4 from nx 256
-    on, 128x8 from nx 128 on), with partial tiles in x (260 = 256 + 4, 130 = 128 + 2) and y
-    (6 = 4 + 2 rows, 9 = 8 + 1): matrix dump bit-exact, and the SpMV bit-exact with the
+@pytest.mark.parametrize("vi_tx,tile", [(0, (64, 16)), (128, (128, 8)), (256, (256, 4))])
+@pytest.mark.parametrize("NX,NY,NZ", [(260, 6, 5), (130, 9, 6), (70, 20, 7)])
+def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
+    """The headline kernel at the tile shapes it runs (k_spmv_vibm 64x16, the default, and the
+    selectable 128x8 / 256x4), with partial tiles in x (260 = 4 x 64 + 4 = 256 + 4, 130,
+    70) and y (6, 9, 20 rows against 16 / 8 / 4): matrix dump bit-exact, and the SpMV bit-exact with the
     oracle's CPU AIJ (MatMult_SeqAIJ order, the MATAIJ matrix of src/init.c:92 applied by
     KSPSolve, src/assembly.c:179-192) under -mat_vi_fma 0 for several z-chunkings and wave
     layouts; the default fused multiply-add rows within 1e-14 sum|a||x|; the solve within the
@@ -482,6 +483,7 @@ def test_aij_vi_production_tiles(NX, NY, NZ, tile):
     P = O.Problem(NX, NY, NZ, rtol=rtol)
     with M.Macroc(argv_for(NX, NY, NZ, rtol)) as m:
         m.set_option("vi_stage", 1)  # the grid is too flat for the default rule (>= 4 planes per chunk)
+        m.set_option("vi_tx", vi_tx)
         for ts in (0, 1):
             m.apply_bc_on_u(m.get_displacement(ts))
             P.apply_bc_u(P.get_displacement(ts))
@@ -514,3 +516,26 @@ def test_aij_vi_production_tiles(NX, NY, NZ, tile):
         out = P.solve()
         assert reason == out["reason"] and abs(its - out["its"]) <= 1
         assert np.linalg.norm(m.du() - P.du()) <= 1e-10 * np.linalg.norm(P.du())
+
+
+@pytest.mark.parametrize("maxits", [0, 5, 6])
+def test_cg_fused_p_update_bitwise(maxits):
+    """Option cg_fusep: the CG's p update inside the value-indexed SpMV (two p buffers) and
+    VecAXPY(x) every second iteration in the update kernel give bitwise the solve of the separate
+    kernels — converged, and stopped by maxits after an odd and an even number of iterations
+    (the pending x update of the last iteration, k_cg_xfinal)."""
+    NX, NY, NZ = 70, 20, 12
+    argv = argv_for(NX, NY, NZ, 1e-12) + (["-ksp_max_it", maxits] if maxits else [])
+    out = []
+    with M.Macroc(argv) as m:
+        m.set_option("vi_stage", 1)
+        m.apply_bc_on_u(m.get_displacement(1))
+        m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
+        for fusep in (0, 1, 0):
+            m.set_option("cg_fusep", fusep)
+            its, rn, reason = m.solve_Ax()
+            out.append((its, reason, m.du()))
+    for its, reason, du in out[1:]:
+        assert (its, reason) == out[0][:2] and np.array_equal(du, out[0][2])
+    if maxits:
+        assert out[0][:2] == (maxits, -3)
