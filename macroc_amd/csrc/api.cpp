@@ -1393,6 +1393,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.vi_block_on = value != 0.;
     return 0;
   }
+  if (!std::strcmp(name, "vi_ring3")) {
+    c.vi_ring3 = value != 0.;
+    return 0;
+  }
   if (!std::strcmp(name, "vi_tx")) {
     c.vi_tx = (int)value;
     if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {

@@ -2145,7 +2145,7 @@ constexpr int vibm_rl() {
 }
 
 template <bool DOT, bool GATED, int TX, int TY, bool XV = true, bool UNI = false, bool PATCH = false, bool FMA = false,
-          bool FP = false>
+          bool FP = false, bool RING3 = false>
 __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __restrict__ I,
                                                        const double* __restrict__ bdict, const double* __restrict__ x,
                                                        double* __restrict__ y, double* __restrict__ part,
@@ -2153,7 +2153,11 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
   static_assert(!PATCH || (TX % 16 == 0 && TY % 4 == 0 && TX * TY == 1024), "16 x 4 patches");
   constexpr int T = TX * TY, RL = vibm_rl<TX, PATCH>(), PR = TY + 2, PLANE = PR * RL;  // doubles per staged plane
   constexpr int NL = (PLANE + T - 1) / T;                                      // x loads per thread per plane
-  __shared__ double xs[3][PLANE];
+  // ring of x planes: 4 slots where they fit the LDS (TX <= 128: plane k+2 then goes to the slot
+  // of plane k-2, which plane k does not read, so one barrier per plane), else 3 (256x4 tiles:
+  // plane k+2 overwrites plane k-1's slot after a barrier, and a second barrier publishes it)
+  constexpr int R = TX <= 128 && !RING3 ? 4 : 3;  // RING3: A/B of the 3-slot ring (option vi_ring3)
+  __shared__ double xs[R][PLANE];
   __shared__ double2 tab[VI_MAX * VIB_STRIDE / 2];
   __shared__ double sh[T / 64];
   __shared__ double s_jdd[FP ? 3 * VI_MAX : 1];
@@ -2310,7 +2314,7 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
         for (int t = 0; t < GB; t++) {
           const int nb = nb0 + t;
           const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
-          const int xo = ((k + dz - k0 + 1) % 3) * PLANE + (ly + 1 + dy) * RL + 3 * (lx + 1 + dx);
+          const int xo = ((k + dz - k0 + 1) % R) * PLANE + (ly + 1 + dy) * RL + 3 * (lx + 1 + dx);
           lds_vdouble* xp = xsv + xo;
           xv[t][0] = xp[0];
           xv[t][1] = xp[1];
@@ -2359,7 +2363,7 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
 #pragma unroll
       for (int nb = 0; nb < 27; nb++) {
         const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
-        const int xo = ((k + dz - k0 + 1) % 3) * PLANE + (ly + 1 + dy) * RL + 3 * (lx + 1 + dx);
+        const int xo = ((k + dz - k0 + 1) % R) * PLANE + (ly + 1 + dy) * RL + 3 * (lx + 1 + dx);
         double xv[3];
         if (XV) {
           lds_vdouble* xp = xsv + xo;
@@ -2397,13 +2401,13 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       if (DOT) dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
     }
     if (more) {  // uniform
-      __syncthreads();  // plane k-1's slot is free
+      if (R == 3) __syncthreads();  // plane k-1's slot is free
       if (FP) {
 #pragma unroll
-        for (int m = 0; m < NL; m++) fstore((k + 2 - k0 + 1) % 3, k + 2, m, fe[m]);
+        for (int m = 0; m < NL; m++) fstore((k + 2 - k0 + 1) % R, k + 2, m, fe[m]);
       } else {
 #pragma unroll
-        for (int m = 0; m < NL; m++) xstore((k + 2 - k0 + 1) % 3, m, xr[m]);
+        for (int m = 0; m < NL; m++) xstore((k + 2 - k0 + 1) % R, m, xr[m]);
       }
       c0 = n0;
       c1 = n1;
@@ -3705,7 +3709,9 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
       hipLaunchKernelGGL((k_spmv_vibm<false, false, TXV, TYV, XVV, UV, PV, ##__VA_ARGS__>), dim3(nb), dim3(1024), 0,      \
                          c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt);                             \
   } while (0)
-      if (c.vi_fma) {
+      if (c.vi_fma && c.vi_ring3 && tx == 64) {
+        MCX_VIBM(64, 16, true, true, true, true, false, true);
+      } else if (c.vi_fma) {
         if (tx == 256) MCX_VIBM(256, 4, true, true, true, true);
         else if (tx == 128) MCX_VIBM(128, 8, true, true, true, true);
         else MCX_VIBM(64, 16, true, true, true, true);

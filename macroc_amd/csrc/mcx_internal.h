@@ -182,6 +182,7 @@ struct Ctx {
   int vi_fma = 1;            // staged block-indexed SpMV: fused multiply-add rows (-mat_vi_fma, option vi_fma;
                              // rounding-level, not bit-exact); implies vi_uni + vi_patch
   int vi_patch = 1;          // with vi_uni: 16 x 4 node patches per wave (option vi_patch)
+  int vi_ring3 = 0;          // A/B: the 3-slot x ring (two barriers per plane) for 64x16 tiles (option vi_ring3)
   int vi_tx = 0;             // staged block-indexed SpMV tile width 256 | 128 | 64 (0: 64; option vi_tx)
   int vi_uni = 1;            // staged block-indexed SpMV: wave-uniform blocks from scalar loads (option vi_uni)
   int vi_xread = 1;          // staged block-indexed SpMV: x as unpaired 8-B LDS reads (option vi_xread; 0: compiler's pairs)
