@@ -141,6 +141,9 @@ typedef struct {
   int spmv_tx, spmv_ty, spmv_kc; /* SpMV of the last assembled storage when it is a z-marching tile kernel:
                                    tile width (x nodes), height (y rows) and planes per z-chunk; 0 for the
                                    gathered (one-node-per-thread) kernels */
+  int64_t vi_exc_nodes;         /* value-indexed AIJ, block mode: owned nodes whose 27 blocks are stored as
+                                   plain values (a per-GP-tangent law: the nodes touching an element whose
+                                   tangent differs from the law's reference tangent) */
 } mcx_info;
 
 typedef struct {

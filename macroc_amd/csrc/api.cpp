@@ -55,7 +55,8 @@ static int free_ctx(Ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
   void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
-                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2,
+                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2, c->elem_plain, c->cref, c->vi_xslot,
+                  c->vi_xlist, c->vi_exc,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf, c->halo.d_bnd};
   for (void* p : ptrs)
@@ -498,6 +499,7 @@ static void fill_info(const Ctx& c, mcx_info* in) {
   in->vi_values = c.fmt == FMT_VI ? c.vi_n : 0;
   in->vi_bits = c.fmt == FMT_VI ? c.vi_bits : 0;
   in->vi_blocks = c.fmt == FMT_VI && c.vi_block ? c.vi_nblocks : 0;
+  in->vi_exc_nodes = c.fmt == FMT_VI && c.vi_block ? c.vi_nexc : 0;
   if (c.device >= 0) spmv_tile(c, &in->spmv_tx, &in->spmv_ty, &in->spmv_kc);
   in->ex0 = g.ex0;
   in->ey0 = g.ey0;
@@ -1133,6 +1135,11 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
   std::vector<uint16_t> Dh;
   std::vector<unsigned char> Ih;
   std::vector<double> dict;
+  std::vector<double> Xh;  // exception nodes' blocks
+  if (vals && c.fmt == FMT_VI && c.vi_block && c.vi_nexc) {
+    Xh.resize((size_t)c.vi_nexc * 27 * 9);
+    MCX_HIP(hipMemcpyAsync(Xh.data(), c.vi_exc, Xh.size() * sizeof(double), hipMemcpyDeviceToHost, c.stream));
+  }
   if (vals && c.fmt == FMT_VI) {
     Ih.resize((size_t)c.vi_idx_bytes);
     dict.resize(c.vi_block ? VI_MAX * VIB_STRIDE : std::max(VI_MAX, NSLOT * 16));
@@ -1197,7 +1204,10 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
           } else if (vals && c.fmt == FMT_VI) {
             const int s = nb * 9 + r * 3 + cc;
             if (c.vi_block) {  // byte nb of 2 chunks of 16 B: the block's dictionary entry
-              v = dict[Ih[(((n >> 6) * 2 + (nb >> 4)) * 64 + (n & 63)) * 16 + (nb & 15)] * VIB_STRIDE + r * 3 + cc];
+              uint32_t xs = 0;  // exception slot + 1 in bytes 28-31
+              std::memcpy(&xs, &Ih[(((n >> 6) * 2 + 1) * 64 + (n & 63)) * 16 + 12], 4);
+              if (xs && !Xh.empty()) v = Xh[((size_t)(xs - 1) * 27 + nb) * 9 + r * 3 + cc];
+              else v = dict[Ih[(((n >> 6) * 2 + (nb >> 4)) * 64 + (n & 63)) * 16 + (nb & 15)] * VIB_STRIDE + r * 3 + cc];
             } else if (c.vi_bits == 8) {
               v = dict[Ih[(((n >> 6) * VI_CHUNKS + (s >> 4)) * 64 + (n & 63)) * 16 + (s & 15)]];
             } else {  // nibble s of 8 chunks of 16 B, low nibble first
@@ -1304,6 +1314,7 @@ int mcx_get_timing(void* ctx, mcx_timing* t) {
                          : c.nupper_local * 8) +
       2 * 3 * (int64_t)c.g.nown * 8;
   if (c.fmt == FMT_SPLIT) t->spmv_bytes_per_launch += (int64_t)c.g.nown * c.dsl.Lq * 16;
+  if (c.fmt == FMT_VI && c.vi_block) t->spmv_bytes_per_launch += c.vi_nexc * 27 * 9 * 8;  // exception blocks
   // the fused p update (cg_fusep): r and the diagonal index read, p(i) written
   if (c.fusep_used) t->spmv_bytes_per_launch += (int64_t)c.g.nown * (24 + 1 + 24);
   return 0;
@@ -1409,6 +1420,11 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.cg_fusep = value != 0.;
     if (c.cg_fusep && !c.p_pad2 && c.nranks == 1 && !c.comm && !c.lg)
       return dalloc(c, &c.p_pad2, (int64_t)c.g.PX * c.g.PY * c.g.PZ * 3);
+    return 0;
+  }
+  if (!std::strcmp(name, "vi_exc_max")) {  // takes effect at the next mcx_assembly_jac
+    c.vi_exc_max = std::max(0, std::min(1000, (int)value));
+    c.vi_declined = false;
     return 0;
   }
   if (!std::strcmp(name, "vib_onepass")) {  // takes effect at the next mcx_assembly_jac

@@ -283,6 +283,24 @@ __global__ void k_homogenize_elastic(int64_t ngp, Material mat, const double* __
   }
 }
 
+__device__ __forceinline__ void j2_moduli(const Material& mat, double& G, double& K) {
+  G = mat.E / (2. * (1. + mat.nu));
+  K = mat.E / (3. * (1. - 2. * mat.nu));
+}
+
+// the J2 law's tangent on its elastic branch (f <= 0): every such Gauss point gets these bits
+__device__ __forceinline__ void j2_elastic_tangent(double G, double K, double (&C)[36]) {
+  const double lam = K - 2. * G / 3.;
+#pragma unroll
+  for (int k2 = 0; k2 < 36; k2++) C[k2] = 0.;
+#pragma unroll
+  for (int a = 0; a < 3; a++)
+#pragma unroll
+    for (int b = 0; b < 3; b++) C[a * 6 + b] = lam + (a == b ? 2. * G : 0.);
+#pragma unroll
+  for (int a = 3; a < 6; a++) C[a * 6 + a] = G;
+}
+
 // small-strain J2 plasticity with linear isotropic hardening (MicroPP material type 1: E, nu,
 // Sy, Ka), radial return + consistent tangent; same operation order as orc_j2_point (oracle).
 __global__ void k_homogenize_plastic(int64_t ngp, Material mat, const double* __restrict__ eps,
@@ -291,9 +309,9 @@ __global__ void k_homogenize_plastic(int64_t ngp, Material mat, const double* __
                                      double* __restrict__ ftrial) {
   int64_t q = (int64_t)blockIdx.x * TPB + threadIdx.x;
   if (q >= ngp) return;
-  const double E = mat.E, nu = mat.nu, Sy = mat.Sy, Ka = mat.Ka;
-  const double G = E / (2. * (1. + nu));
-  const double K = E / (3. * (1. - 2. * nu));
+  const double Sy = mat.Sy, Ka = mat.Ka;
+  double G, K;
+  j2_moduli(mat, G, K);
   double e[6], h[7];
 #pragma unroll
   for (int l = 0; l < 6; l++) e[l] = eps[l * ngp + q];
@@ -314,15 +332,7 @@ __global__ void k_homogenize_plastic(int64_t ngp, Material mat, const double* __
   const double f = snorm - sqrt(2. / 3.) * (Sy + Ka * alpha);
   ftrial[q] = f;
   double C[36], s[6];
-  const double lam = K - 2. * G / 3.;
-#pragma unroll
-  for (int k2 = 0; k2 < 36; k2++) C[k2] = 0.;
-#pragma unroll
-  for (int a = 0; a < 3; a++)
-#pragma unroll
-    for (int b = 0; b < 3; b++) C[a * 6 + b] = lam + (a == b ? 2. * G : 0.);
-#pragma unroll
-  for (int a = 3; a < 6; a++) C[a * 6 + a] = G;
+  j2_elastic_tangent(G, K, C);
   if (f <= 0.) {
 #pragma unroll
     for (int i = 0; i < 3; i++) s[i] = K * tr + st[i];
@@ -1943,7 +1953,8 @@ template <bool TABLE>
 __global__ __launch_bounds__(TPB) void k_vib_build(Geo g, Material mat, const double* __restrict__ Ke,
                                                    unsigned long long* __restrict__ gsv,
                                                    unsigned long long* __restrict__ gbk,
-                                                   unsigned short* __restrict__ bpos, unsigned* __restrict__ ctl) {
+                                                   unsigned short* __restrict__ bpos, unsigned* __restrict__ ctl,
+                                                   const unsigned* __restrict__ xslot) {
   constexpr int LSV = 64, LSB = 64;
   __shared__ unsigned long long s_v[9][LSV];
   __shared__ unsigned char s_vp[9][LSV];
@@ -1957,7 +1968,7 @@ __global__ __launch_bounds__(TPB) void k_vib_build(Geo g, Material mat, const do
   if (s_over) return;  // uniform: the build already overflowed
   const int n = blockIdx.x * TPB + threadIdx.x;
   const int nb = blockIdx.y;
-  const bool own = n < g.nown;
+  const bool own = n < g.nown && !(xslot && xslot[n]);  // exception nodes stay out of the dictionary
   bool bad = false, isnew;
   int lp[9];
   if (own) {
@@ -2015,9 +2026,11 @@ __global__ __launch_bounds__(TPB) void k_vib_build(Geo g, Material mat, const do
   if (own) bpos[(int64_t)nb * g.nown + n] = s_bp[lb];
 }
 
-// the 27 block-set positions of every owned node -> its 27 index bytes (+5 zero pad)
+// the 27 block-set positions of every owned node -> its 27 index bytes (+5 zero pad); an
+// exception node gets 27 zero bytes and its slot + 1 in bytes 28-31
 __global__ __launch_bounds__(TPB) void k_vib_remap(Geo g, const unsigned short* __restrict__ bpos,
-                                                   const unsigned char* __restrict__ bmap, u32x4* __restrict__ I) {
+                                                   const unsigned char* __restrict__ bmap, u32x4* __restrict__ I,
+                                                   const unsigned* __restrict__ xslot) {
   __shared__ unsigned char s_map[VI_HASH];
   for (int t = threadIdx.x; t < VI_HASH / 16; t += TPB)
     reinterpret_cast<u32x4*>(s_map)[t] = reinterpret_cast<const u32x4*>(bmap)[t];
@@ -2025,11 +2038,94 @@ __global__ __launch_bounds__(TPB) void k_vib_remap(Geo g, const unsigned short* 
   const int n = blockIdx.x * TPB + threadIdx.x;
   if (n >= g.nown) return;
   unsigned w[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+  const unsigned xs = xslot ? xslot[n] : 0u;
+  if (xs) w[7] = xs;
+  else {
 #pragma unroll
-  for (int nb = 0; nb < 27; nb++) w[nb >> 2] |= (unsigned)s_map[bpos[(int64_t)nb * g.nown + n]] << (8 * (nb & 3));
+    for (int nb = 0; nb < 27; nb++) w[nb >> 2] |= (unsigned)s_map[bpos[(int64_t)nb * g.nown + n]] << (8 * (nb & 3));
+  }
   u32x4* dst = I + (int64_t)(n >> 6) * 128 + (n & 63);
   dst[0] = u32x4{w[0], w[1], w[2], w[3]};
   dst[64] = u32x4{w[4], w[5], w[6], w[7]};
+}
+
+// ---- exception nodes (laws with a per-GP tangent).  A J2 law whose few plastic Gauss points sit
+// under the load (config 5: 552-2,920 of 16.8 M) leaves every other element with the elastic
+// branch's tangent, bit for bit, and so with one element matrix: the nodes whose elements are all
+// such "plain" elements assemble into the same few blocks as the elastic law's matrix.  Only the
+// nodes touching a non-plain element (the exceptions) keep their 27 blocks as plain values.
+// cref: the plastic law's elastic-branch tangent; other laws: GP 0 of the context's first element.
+__global__ void k_cref(Material mat, const double* __restrict__ ctan, int64_t ngp, double* __restrict__ cref) {
+  if (threadIdx.x) return;
+  if (mat.law == MCX_LAW_PLASTIC) {
+    double G, K, C[36];
+    j2_moduli(mat, G, K);
+    j2_elastic_tangent(G, K, C);
+#pragma unroll
+    for (int q = 0; q < 36; q++) cref[q] = C[q];
+  } else {
+    for (int q = 0; q < 36; q++) cref[q] = ctan[q * ngp];
+  }
+}
+
+// plain[le] = the 8 Gauss points' tangents (ctan [36][8][nelem]) all equal cref bit for bit
+__global__ __launch_bounds__(TPB) void k_elem_plain(Geo g, const double* __restrict__ ctan,
+                                                    const double* __restrict__ cref, unsigned char* __restrict__ plain) {
+  const int64_t le = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  const int64_t E = g.nelem, NG = 8 * E;
+  if (le >= E) return;
+  bool same = true;
+  for (int kl = 0; kl < 36; kl++) {
+    const long long r = __double_as_longlong(cref[kl]);
+#pragma unroll
+    for (int gp = 0; gp < 8; gp++) same = same && __double_as_longlong(ctan[kl * NG + gp * E + le]) == r;
+  }
+  plain[le] = same ? 1 : 0;
+}
+
+// owned node n is an exception when one of its elements is not plain: slot = ctl[2]++,
+// xslot[n] = slot + 1, xlist[slot] = n (slots in arrival order; a row's values do not depend on it)
+__global__ __launch_bounds__(TPB) void k_node_exc(Geo g, const unsigned char* __restrict__ plain,
+                                                  unsigned* __restrict__ xslot, int* __restrict__ xlist,
+                                                  unsigned* __restrict__ ctl) {
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  const int gi = g.xs + i, gj = g.ys + j, gk = g.zs + k;
+  bool exc = false;
+  for (int oz = 0; oz < 2; oz++)
+    for (int oy = 0; oy < 2; oy++)
+      for (int ox = 0; ox < 2; ox++) {
+        const int ex = gi - ox, ey = gj - oy, ez = gk - oz;
+        if (ex < 0 || ex > g.NX - 2 || ey < 0 || ey > g.NY - 2 || ez < 0 || ez > g.NZ - 2) continue;
+        const int64_t le = (ex - g.ex0) + (int64_t)(ey - g.ey0) * g.nex + (int64_t)(ez - g.ez0) * g.nex * g.ney;
+        exc = exc || !plain[le];
+      }
+  unsigned v = 0u;
+  if (exc) {
+    const unsigned slot = atomicAdd(&ctl[2], 1u);
+    xlist[slot] = n;
+    v = slot + 1u;
+  }
+  xslot[n] = v;
+}
+
+// the exception nodes' 27 blocks, [slot][nb][9]: thread = (slot, nb)
+template <bool TABLE>
+__global__ __launch_bounds__(TPB) void k_exc_fill(Geo g, Material mat, const double* __restrict__ Ke,
+                                                  const int* __restrict__ xlist, int64_t nexc,
+                                                  double* __restrict__ exc) {
+  const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  const int nb = blockIdx.y;
+  if (t >= nexc) return;
+  const int n = xlist[t];
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  double val[9];
+  matrix_block<TABLE>(g, mat, Ke, g.xs + i, g.ys + j, g.zs + k, nb % 3 - 1, (nb / 3) % 3 - 1, nb / 9 - 1, val);
+#pragma unroll
+  for (int q = 0; q < 9; q++) exc[(t * 27 + nb) * 9 + q] = val[q];
 }
 
 __device__ __forceinline__ double jacobi_inv(double d) {
@@ -2039,14 +2135,18 @@ __device__ __forceinline__ double jacobi_inv(double d) {
 }
 
 // dinv per owned DOF, and jix[n] = the node's diagonal-block index (block 13 = offset 0,0,0)
+// (exc: an exception node's diagonal block is its plain block 13)
 __global__ void k_jacobi_vib(Geo g, const unsigned char* __restrict__ I, const double* __restrict__ bdict,
-                             double* __restrict__ dinv, unsigned char* __restrict__ jix) {
+                             double* __restrict__ dinv, unsigned char* __restrict__ jix, const double* __restrict__ exc) {
   const int n = blockIdx.x * TPB + threadIdx.x;
   if (n >= g.nown) return;
   const int id = I[(((int64_t)(n >> 6) * 2 + 0) * 64 + (n & 63)) * 16 + 13];
   jix[n] = (unsigned char)id;
+  const unsigned xs =
+      exc ? *reinterpret_cast<const unsigned*>(I + (((int64_t)(n >> 6) * 2 + 1) * 64 + (n & 63)) * 16 + 12) : 0u;
+  const double* d = xs ? exc + ((int64_t)(xs - 1) * 27 + 13) * 9 : bdict + id * VIB_STRIDE;
 #pragma unroll
-  for (int r = 0; r < 3; r++) dinv[3 * n + r] = jacobi_inv(bdict[id * VIB_STRIDE + r * 4]);
+  for (int r = 0; r < 3; r++) dinv[3 * n + r] = jacobi_inv(d[r * 4]);
 }
 
 // the dictionary's inverse diagonals [VI_MAX][3] (same values as k_jacobi_vib's dinv)
@@ -2059,11 +2159,13 @@ __global__ void k_jacobi_vib_dict(const double* __restrict__ bdict, double* __re
 // y = A x on block-indexed FMT_VI: 2 16-B index chunks per node (27 block bytes), each block's
 // 9 values from the dictionary in LDS (4 x 16-B + 8-B reads), x gathered.  Same slot order and
 // products as k_spmv: bit-identical to the CPU AIJ product.
-template <bool DOT, bool GATED>
+// EXC: exception nodes (slot + 1 in bytes 28-31) read their blocks from exc [slot][27][9].
+template <bool DOT, bool GATED, bool EXC = false>
 __global__ __launch_bounds__(TPB) void k_spmv_vib(Geo g, const u32x4* __restrict__ I,
                                                   const double* __restrict__ bdict, const double* __restrict__ x,
                                                   double* __restrict__ y, double* __restrict__ part,
-                                                  const CgState* __restrict__ cg, SpmvTiling tl) {
+                                                  const CgState* __restrict__ cg, SpmvTiling tl,
+                                                  const double* __restrict__ exc = nullptr) {
   __shared__ double2 tab[VI_MAX * VIB_STRIDE / 2];
   __shared__ double sh[TPB / 64];
   if (GATED && cg->reason) return;
@@ -2090,9 +2192,17 @@ __global__ __launch_bounds__(TPB) void k_spmv_vib(Geo g, const u32x4* __restrict
       }
       const unsigned word = nb < 16 ? w0[nb >> 2] : w1[(nb - 16) >> 2];
       const unsigned id = (word >> (8 * (nb & 3))) & 255u;
-      const double2* e = tab + id * (VIB_STRIDE / 2);
-      const double2 a01 = e[0], a23 = e[1], a45 = e[2], a67 = e[3], a8 = e[4];
-      const double a[9] = {a01.x, a01.y, a23.x, a23.y, a45.x, a45.y, a67.x, a67.y, a8.x};
+      double a[9];
+      if (EXC && w1[3]) {
+        const double* e = exc + ((int64_t)(w1[3] - 1) * 27 + nb) * 9;
+#pragma unroll
+        for (int q = 0; q < 9; q++) a[q] = e[q];
+      } else {
+        const double2* e = tab + id * (VIB_STRIDE / 2);
+        const double2 a01 = e[0], a23 = e[1], a45 = e[2], a67 = e[3], a8 = e[4];
+        a[0] = a01.x, a[1] = a01.y, a[2] = a23.x, a[3] = a23.y, a[4] = a45.x, a[5] = a45.y, a[6] = a67.x;
+        a[7] = a67.y, a[8] = a8.x;
+      }
 #pragma unroll
       for (int q = 0; q < 9; q++) {
         const int r = q / 3, cc = q % 3;
@@ -2145,11 +2255,12 @@ constexpr int vibm_rl() {
 }
 
 template <bool DOT, bool GATED, int TX, int TY, bool XV = true, bool UNI = false, bool PATCH = false, bool FMA = false,
-          bool FP = false, bool RING3 = false>
+          bool FP = false, bool RING3 = false, bool EXC = false>
 __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __restrict__ I,
                                                        const double* __restrict__ bdict, const double* __restrict__ x,
                                                        double* __restrict__ y, double* __restrict__ part,
-                                                       const CgState* __restrict__ cg, ZTiling zt, FusedP fp = {}) {
+                                                       const CgState* __restrict__ cg, ZTiling zt, FusedP fp = {},
+                                                       const double* __restrict__ exc = nullptr) {
   static_assert(!PATCH || (TX % 16 == 0 && TY % 4 == 0 && TX * TY == 1024), "16 x 4 patches");
   constexpr int T = TX * TY, RL = vibm_rl<TX, PATCH>(), PR = TY + 2, PLANE = PR * RL;  // doubles per staged plane
   constexpr int NL = (PLANE + T - 1) / T;                                      // x loads per thread per plane
@@ -2296,7 +2407,7 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       unsigned diff = 0u;
 #pragma unroll
       for (int q = 0; q < 7; q++) diff |= (q < 4 ? c0[q] : c1[q - 4]) ^ sw[q];
-      uni = __all(inxy && diff == 0u) || (zt.dbg & 1);
+      uni = __all(inxy && diff == 0u && (!EXC || c1[3] == 0u)) || (zt.dbg & 1);
     }
     if (UNI && uni) {  // (every lane is inxy)
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
@@ -2347,6 +2458,34 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
           }
         }
         __builtin_amdgcn_sched_barrier(0);
+      }
+      const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
+      __builtin_nontemporal_store(y0, &y[3 * n + 0]);
+      __builtin_nontemporal_store(y1, &y[3 * n + 1]);
+      __builtin_nontemporal_store(y2, &y[3 * n + 2]);
+      if (DOT) dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
+    } else if (EXC && inxy && c1[3]) {
+      // an exception node (EXC instantiations only): its 27 plain blocks from exc [slot][27][9], a
+      // rolled loop of its own so the indexed path below keeps its registers; same order and
+      // products as the indexed rows
+      double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+      const double* eb = exc + (int64_t)(c1[3] - 1) * 243;
+#pragma unroll 1
+      for (int nb = 0; nb < 27; nb++) {
+        const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
+        const int xo = ((k + dz - k0 + 1) % R) * PLANE + (ly + 1 + dy) * RL + 3 * (lx + 1 + dx);
+        const double xv[3] = {xs[0][xo], xs[0][xo + 1], xs[0][xo + 2]};
+        if (nb == 13) {
+          xc0 = xv[0];
+          xc1 = xv[1];
+          xc2 = xv[2];
+        }
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+          const int r = q / 3, cc = q % 3;
+          double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
+          yr = FMA ? __builtin_fma(eb[nb * 9 + q], xv[cc], yr) : yr + eb[nb * 9 + q] * xv[cc];
+        }
       }
       const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
       __builtin_nontemporal_store(y0, &y[3 * n + 0]);
@@ -3199,7 +3338,7 @@ bool vi_staged(const Ctx& c) {
 }
 
 int64_t spmv_grid_blocks(const Ctx& c) {
-  if (c.fmt == FMT_VI && vi_staged(c) && c.vi_bits == 4) {
+  if (c.fmt == FMT_VI && vi_staged(c) && (c.vi_bits == 4 || c.vi_block)) {  // launch_spmv's staged kernels
     const ZTiling t = vis_tiling(c);
     return 8 * (int64_t)(((t.nty + 7) / 8) * t.ntx * t.nzc);
   }
@@ -3216,7 +3355,7 @@ int64_t spmv_grid_blocks(const Ctx& c) {
 }
 void spmv_tile(const Ctx& c, int* tx, int* ty, int* kc) {
   *tx = *ty = *kc = 0;
-  if (c.fmt == FMT_VI && vi_staged(c) && c.vi_bits == 4) {
+  if (c.fmt == FMT_VI && vi_staged(c) && (c.vi_bits == 4 || c.vi_block)) {
     vis_shape(c, *tx, *ty);
     *kc = vis_tiling(c).kc;
   } else if (c.fmt == FMT_SPLIT || (c.fmt == FMT_U && c.spmv_kernel >= 1)) {
@@ -3404,19 +3543,50 @@ static int build_vib(Ctx& c, bool* ok) {
   MCX_HIP(hipMemsetAsync(c.vib_keys, 0xff, (nsv + VI_HASH) * sizeof(unsigned long long), c.stream));
   MCX_HIP(hipMemsetAsync(c.vib_ctl, 0, 4 * sizeof(unsigned), c.stream));
   const dim3 grid(nblk(c.g.nown), 27);
+  // a per-GP-tangent law: the nodes touching a non-plain element become exceptions
+  const bool exc = table_law(c) && c.vi_exc_max > 0;
+  c.vi_nexc = 0;
+  if (exc) {
+    if (!c.elem_plain) {  // first exception build: flags, reference tangent, slots
+      MCX_HIP(hipMalloc(&c.elem_plain, c.g.nelem));
+      MCX_HIP(hipMalloc(&c.cref, 36 * sizeof(double)));
+      MCX_HIP(hipMalloc(&c.vi_xslot, c.g.nown * sizeof(unsigned)));
+      MCX_HIP(hipMalloc(&c.vi_xlist, c.g.nown * sizeof(int)));
+      c.device_bytes += c.g.nelem + 36 * 8 + c.g.nown * 8;
+    }
+    hipLaunchKernelGGL(k_cref, dim3(1), dim3(64), 0, c.stream, c.mat, c.ctan, (int64_t)8 * c.g.nelem, c.cref);
+    hipLaunchKernelGGL(k_elem_plain, dim3(nblk(c.g.nelem)), dim3(TPB), 0, c.stream, c.g, c.ctan, c.cref,
+                       c.elem_plain);
+    hipLaunchKernelGGL(k_node_exc, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.elem_plain, c.vi_xslot,
+                       c.vi_xlist, c.vib_ctl);
+  }
+  const unsigned* xslot = exc ? c.vi_xslot : nullptr;
   if (table_law(c))
     hipLaunchKernelGGL(k_vib_build<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), gsv, gbk, c.vib_pos,
-                       c.vib_ctl);
+                       c.vib_ctl, xslot);
   else
     hipLaunchKernelGGL(k_vib_build<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), gsv, gbk, c.vib_pos,
-                       c.vib_ctl);
+                       c.vib_ctl, xslot);
   unsigned long long* hk = c.h_vib_keys;
   unsigned* hctl = reinterpret_cast<unsigned*>(hk + nsv + VI_HASH);
   MCX_HIP(hipMemcpyAsync(hk, c.vib_keys, (nsv + VI_HASH) * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                          c.stream));
-  MCX_HIP(hipMemcpyAsync(hctl, c.vib_ctl, 2 * sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipMemcpyAsync(hctl, c.vib_ctl, 4 * sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
   MCX_HIP(hipStreamSynchronize(c.stream));
   if (hctl[1] || hctl[0] > (unsigned)VI_MAX) return 0;
+  const int64_t nexc = exc ? (int64_t)hctl[2] : 0;
+  if (nexc * 1000 > (int64_t)c.vi_exc_max * c.g.nown) return 0;  // too many: AIJ-split
+  if (nexc * 27 * 9 * (int64_t)sizeof(double) > c.vi_exc_bytes) {
+    if (c.vi_exc) {
+      MCX_HIP(hipFree(c.vi_exc));
+      c.device_bytes -= c.vi_exc_bytes;
+      c.vi_exc = nullptr;
+    }
+    // grown with headroom: the plastic zone spreads over the time steps
+    c.vi_exc_bytes = std::min<int64_t>(2 * nexc + 1024, c.g.nown) * 27 * 9 * (int64_t)sizeof(double);
+    MCX_HIP(hipMalloc(&c.vi_exc, c.vi_exc_bytes));
+    c.device_bytes += c.vi_exc_bytes;
+  }
   // each slot's values sorted by bit pattern; rank of every set position
   std::vector<unsigned char> rank(nsv, 0);
   std::vector<unsigned long long> all;
@@ -3466,7 +3636,13 @@ static int build_vib(Ctx& c, bool* ok) {
                          c.stream));
   if (int rc = ensure_vi_idx(c, 32)) return rc;
   hipLaunchKernelGGL(k_vib_remap, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.vib_pos, bmap,
-                     reinterpret_cast<u32x4*>(c.vi_idx));
+                     reinterpret_cast<u32x4*>(c.vi_idx), xslot);
+  if (nexc) {
+    const dim3 eg((unsigned)((nexc + TPB - 1) / TPB), 27);
+    hipLaunchKernelGGL(k_exc_fill<true>, eg, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.vi_xlist, nexc,
+                       c.vi_exc);
+  }
+  c.vi_nexc = nexc;
   c.vi_n = nvals;
   c.vi_bits = maxper <= 16 ? 4 : 8;
   c.vi_nblocks = (int)blk.size();
@@ -3589,7 +3765,7 @@ void launch_jacobi(Ctx& c) {
   if (c.fmt == FMT_VI && c.vi_block)
   {
     hipLaunchKernelGGL(k_jacobi_vib, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.vi_idx, c.vi_bdict, c.dinv,
-                       c.jix);
+                       c.jix, c.vi_nexc ? c.vi_exc : nullptr);
     hipLaunchKernelGGL(k_jacobi_vib_dict, dim3(nblk(3 * VI_MAX)), dim3(TPB), 0, c.stream, c.vi_bdict, c.jdd);
   } else if (c.fmt == FMT_VI && c.vi_bits == 4)
     hipLaunchKernelGGL(k_jacobi_vi<4>, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g,
@@ -3657,7 +3833,7 @@ static void launch_spmv_vi(Ctx& c, const double* xpad, double* y, bool dot, bool
 // block-indexed storage with x staged, Jacobi from the diagonal index, scalar-dictionary patches
 bool fusep(const Ctx& c) {
   return c.cg_fusep && c.p_pad2 && c.nranks == 1 && !c.comm && !c.lg && c.fmt == FMT_VI && c.vi_block &&
-         vi_staged(c) && c.cg_dix && c.vi_uni && c.vi_patch;
+         !c.vi_nexc && vi_staged(c) && c.cg_dix && c.vi_uni && c.vi_patch;
 }
 
 static void launch_spmv_fusep(Ctx& c, double* y) {
@@ -3709,7 +3885,33 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
       hipLaunchKernelGGL((k_spmv_vibm<false, false, TXV, TYV, XVV, UV, PV, ##__VA_ARGS__>), dim3(nb), dim3(1024), 0,      \
                          c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt);                             \
   } while (0)
-      if (c.vi_fma && c.vi_ring3 && tx == 64) {
+      if (c.vi_nexc) {  // exception nodes: the default (FMA) or exact rows, UNI + PATCH
+#define MCX_VIBM_X(TXV, TYV, FV)                                                                                    \
+  do {                                                                                                             \
+    if (dot && gated)                                                                                              \
+      hipLaunchKernelGGL((k_spmv_vibm<true, true, TXV, TYV, true, true, true, FV, false, false, true>), dim3(nb),       \
+                         dim3(1024), 0, c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt, FusedP{},      \
+                         c.vi_exc);                                                                                \
+    else if (dot)                                                                                                  \
+      hipLaunchKernelGGL((k_spmv_vibm<true, false, TXV, TYV, true, true, true, FV, false, false, true>), dim3(nb),      \
+                         dim3(1024), 0, c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt, FusedP{},      \
+                         c.vi_exc);                                                                                \
+    else                                                                                                           \
+      hipLaunchKernelGGL((k_spmv_vibm<false, false, TXV, TYV, true, true, true, FV, false, false, true>), dim3(nb),     \
+                         dim3(1024), 0, c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt, FusedP{},      \
+                         c.vi_exc);                                                                                \
+  } while (0)
+        if (c.vi_fma) {
+          if (tx == 256) MCX_VIBM_X(256, 4, true);
+          else if (tx == 128) MCX_VIBM_X(128, 8, true);
+          else MCX_VIBM_X(64, 16, true);
+        } else {
+          if (tx == 256) MCX_VIBM_X(256, 4, false);
+          else if (tx == 128) MCX_VIBM_X(128, 8, false);
+          else MCX_VIBM_X(64, 16, false);
+        }
+#undef MCX_VIBM_X
+      } else if (c.vi_fma && c.vi_ring3 && tx == 64) {
         MCX_VIBM(64, 16, true, true, true, true, false, true);
       } else if (c.vi_fma) {
         if (tx == 256) MCX_VIBM(256, 4, true, true, true, true);
@@ -3733,6 +3935,18 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
         else MCX_VIBM(64, 16, false, false, false);
       }
 #undef MCX_VIBM
+      return;
+    }
+    if (c.vi_nexc) {
+      if (dot && gated)
+        hipLaunchKernelGGL((k_spmv_vib<true, true, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_bdict, xpad,
+                           y, c.partials, c.cg, tl, c.vi_exc);
+      else if (dot)
+        hipLaunchKernelGGL((k_spmv_vib<true, false, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_bdict, xpad,
+                           y, c.partials, c.cg, tl, c.vi_exc);
+      else
+        hipLaunchKernelGGL((k_spmv_vib<false, false, true>), dim3(nb), dim3(TPB), 0, c.stream, c.g, I, c.vi_bdict,
+                           xpad, y, c.partials, c.cg, tl, c.vi_exc);
       return;
     }
     if (dot && gated)
@@ -3907,7 +4121,8 @@ void launch_cg_xfinal(Ctx& c) {
 // CG vector kernels' Jacobi form: DIX (block-indexed value storage, option cg_dix) reads one
 // diagonal-block index byte per node and recomputes z = D^-1 r from r where it is used, so the
 // update writes no z and reads no dinv vector (two fewer vectors per iteration)
-static bool cg_dix(const Ctx& c) { return c.cg_dix && c.fmt == FMT_VI && c.vi_block; }
+// (exception nodes have no dictionary diagonal: the Jacobi vector dinv then)
+static bool cg_dix(const Ctx& c) { return c.cg_dix && c.fmt == FMT_VI && c.vi_block && !c.vi_nexc; }
 
 // instantiate CALL with constexpr NT (non-temporal stores) and DX (DIX) from run-time flags
 #define MCX_NT_DIX(ntv, dixv, CALL)                      \

@@ -177,6 +177,18 @@ struct Ctx {
   unsigned char* h_vib_map = nullptr;        // upload: block-set position -> dictionary index [VI_HASH]
   double* h_vib_dict = nullptr;              // upload: [VI_MAX][VIB_STRIDE]
   int vib_onepass = 1;       // option vib_onepass: the single-pass block build (0: round 2's three passes)
+  // exception nodes (per-GP-tangent laws, one-pass block build): an owned node touching an
+  // element whose tangent differs from the law's reference tangent at some Gauss point keeps its
+  // 27 blocks as plain values, [slot][27][9]; its index chunk carries slot + 1 in bytes 28-31
+  unsigned char* elem_plain = nullptr;  // [nelem] 1 = every GP tangent equals cref bit for bit
+  double* cref = nullptr;               // [36] the reference tangent (plastic: the elastic branch's C)
+  unsigned* vi_xslot = nullptr;         // [nown] exception slot + 1, 0 = indexed node
+  int* vi_xlist = nullptr;              // [nown] exception slot -> owned node
+  double* vi_exc = nullptr;             // [exceptions][27][9] block values
+  int64_t vi_exc_bytes = 0;             // allocated bytes of vi_exc
+  int64_t vi_nexc = 0;                  // exception nodes of the current matrix
+  int vi_exc_max = 250;                 // option vi_exc_max: per-mille of owned nodes beyond which the
+                                        // assembly falls back to AIJ-split (0: no exceptions)
   double* ke_uni = nullptr;  // elastic law: the element matrix [8 a][8 b][9], the same for every element
   int aij_vi = 1;            // aij: assemble in FMT_VI when the matrix has at most VI_MAX distinct values
   int vi_fma = 1;            // staged block-indexed SpMV: fused multiply-add rows (-mat_vi_fma, option vi_fma;

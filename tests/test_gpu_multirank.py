@@ -291,6 +291,52 @@ def test_multirank_vi_production_tiles(grid, procs, fma, vi_tx, tile):
     assert np.linalg.norm(du - ref.du()) <= 1e-10 * np.linalg.norm(ref.du())
 
 
+@pytest.mark.parametrize("grid,procs,stage", [((20, 12, 10), (2, 2, 1), 0), ((130, 9, 12), (2, 1, 1), 1),
+                                              ((24, 16, 14), (2, 2, 2), 0)])
+def test_multirank_vi_exception_nodes(grid, procs, stage):
+    """J2 law with a few plastic Gauss points on decomposed subdomains: each rank's nodes that
+    touch a non-elastic element are exception nodes (their own 27 blocks), the rest index the
+    rank's dictionary.  Every rank's rows bit-exact with the one-rank oracle, the SpMV too
+    (-mat_vi_fma 0), du within the north-star bar."""
+    from test_gpu_parity import plastic_state
+
+    NX, NY, NZ = grid
+    px, py, pz = procs
+    rtol = 1e-10
+    P, u = plastic_state(NX, NY, NZ, rtol=rtol)
+    v1 = P.A_values()
+    rp1, ci1 = P.csr()
+    x = np.random.default_rng(29).uniform(-1, 1, P.ndofs)
+    y1 = P.spmv(x)
+    P.solve()
+    argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
+            "-da_processors_z", pz, "-ksp_rtol", repr(rtol), "-dt", 0.01, "-mat_law", "plastic"]
+
+    def fn(m):
+        m.set_option("vi_stage", stage)
+        m.set_option("vi_fma", 0)
+        petsc, nat = m.owned_dofs()
+        m.set_u(u[nat])
+        m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
+        rp, ci, v = m.dump_csr()
+        y = m.spmv(x[nat])
+        its, rn, reason = m.solve_Ax()
+        return dict(nat=nat, rp=rp, v=v, y=y, du=m.du(), its=its, info=m.get_info())
+
+    out = run_group(argv, px * py * pz, fn)
+    du = np.zeros(P.ndofs)
+    assert sum(o["info"]["vi_exc_nodes"] for o in out) > 0
+    for o in out:
+        assert o["info"]["storage"] == 3, o["info"]
+        assert np.array_equal(o["y"], y1[o["nat"]])
+        for q in range(len(o["nat"])):
+            row = o["nat"][q]
+            assert np.array_equal(np.sort(o["v"][o["rp"][q]:o["rp"][q + 1]].view(np.int64)),
+                                  np.sort(v1[rp1[row]:rp1[row + 1]].view(np.int64)))
+        du[o["nat"]] = o["du"]
+    assert np.linalg.norm(du - P.du()) <= 50 * rtol * np.linalg.norm(P.du())
+
+
 def test_back_to_back_halos():
     """Halo exchanges with no all-reduce between them (set_strains twice, then SpMVs back to
     back): each exchange's device copies into a rank's receive buffer are ordered after that

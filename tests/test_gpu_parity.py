@@ -207,6 +207,66 @@ def test_aij_vi_fallback_and_toggle():
             m.set_option("aij_vi", 1)
 
 
+def plastic_state(NX, NY, NZ, dt=0.01, rtol=1e-10):
+    """Oracle J2 problem after one solved Newton iteration of time step 1 (default load): the
+    Gauss points under the load are plastic, the rest on the elastic branch.  Returns the oracle
+    (assembled at that state) and its u."""
+    P = O.Problem(NX, NY, NZ, rtol=rtol, law=1, dt=dt)
+    P.apply_bc_u(P.get_displacement(1))
+    P.set_strains(); P.homogenize(); P.assembly_res(); P.assembly_jac(); P.solve(); P.update_u()
+    u = P.u()
+    P.set_strains(); P.homogenize(); P.assembly_res(); P.assembly_jac()
+    assert P.nonlinear_gps()[0] > 0
+    return P, u
+
+
+@pytest.mark.parametrize("grid,stage,vi_tx,tile", [((12, 10, 14), 0, 0, (0, 0)), ((130, 9, 12), 1, 0, (64, 16)),
+                                                   ((130, 9, 12), 1, 128, (128, 8)), ((260, 9, 10), 1, 256, (256, 4))])
+def test_aij_vi_exception_nodes(grid, stage, vi_tx, tile):
+    """A per-GP-tangent law (J2) with a few plastic Gauss points stays value-indexed: the nodes
+    touching an element with a non-elastic tangent keep their 27 blocks as plain values
+    (exception nodes), every other node indexes the elastic blocks' dictionary.  Matrix values
+    bit-exact with the oracle's AIJ; the SpMV bit-exact with the CPU AIJ product under
+    -mat_vi_fma 0 (gathered kernel, and the 64x16 / 128x8 / 256x4 staged tiles), within
+    1e-14 sum|a||x| with the fused multiply-adds; the solve within the north-star bar."""
+    NX, NY, NZ = grid
+    rtol = 1e-10
+    P, u = plastic_state(NX, NY, NZ, rtol=rtol)
+    rp1, ci1 = P.csr()
+    v1 = P.A_values()
+    x = np.random.default_rng(5).uniform(-1, 1, P.ndofs)
+    y1 = P.spmv(x)
+    absrow = np.add.reduceat(np.abs(v1) * np.abs(x[ci1]), rp1[:-1])
+    b1 = P.b()
+    ref_its = P.solve()["its"]
+    argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-dt", 0.01, "-mat_law", "plastic",
+            "-ksp_rtol", repr(rtol)]
+    with M.Macroc(argv) as m:
+        m.set_option("vi_stage", stage)
+        m.set_option("vi_tx", vi_tx)
+        m.set_u(u)
+        m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
+        info = m.get_info()
+        assert info["storage"] == 3 and info["vi_blocks"] > 0, info
+        assert 0 < info["vi_exc_nodes"] < NX * NY * NZ // 4, info
+        assert (info["spmv_tx"], info["spmv_ty"]) == tile, info
+        assert np.array_equal(m.b(), b1)
+        assert np.array_equal(m.dump_csr()[2], v1)
+        m.set_option("vi_fma", 0)
+        assert np.array_equal(m.spmv(x), y1)
+        m.set_option("vi_fma", 1)
+        y = m.spmv(x)
+        assert np.all(np.abs(y - y1) <= 1e-14 * absrow + 1e-300)
+        its, rn, reason = m.solve_Ax()
+        assert reason > 0 and abs(its - ref_its) <= 1
+        assert np.linalg.norm(m.du() - P.du()) <= 50 * rtol * np.linalg.norm(P.du())
+        # the same matrix with exceptions refused: AIJ-split, bit-exact too
+        m.set_option("vi_exc_max", 0)
+        m.assembly_jac()
+        assert m.get_info()["storage"] == 2 and m.get_info()["vi_exc_nodes"] == 0
+        assert np.array_equal(m.dump_csr()[2], v1)
+
+
 @pytest.mark.parametrize("name", SINGLE)
 def test_aij_split_single_rank(name):
     """AIJ-split storage: upper blocks + bf16 lower corrections.  Every AIJ value is

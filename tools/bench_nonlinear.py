@@ -21,6 +21,8 @@ ap.add_argument("--split", type=int, default=1, help="aij: -mat_aij_split (1: up
 ap.add_argument("--rtol", type=float, default=1e-8)
 ap.add_argument("--dt", type=float, default=0.01, help="load step (U = -ts*dt); 0.01 drives the circle plastic")
 ap.add_argument("--maxq", type=int, default=None, help="aij-split: split_maxq (correction quads per node allowed)")
+ap.add_argument("--exc-max", type=int, default=None, help="aij value-indexed: vi_exc_max (per-mille of owned nodes "
+                "allowed as exception nodes; 0: a per-GP tangent falls back to AIJ-split)")
 ap.add_argument("--micro-n", type=int, default=10, help="-micro_n (BASELINE config 5: 10; sizes MicroPP's micro-cell, "
                 "which the device law does not have: reported, no effect)")
 a = ap.parse_args()
@@ -30,6 +32,8 @@ m = M.Macroc(["-da_grid_x", N, "-da_grid_y", N, "-da_grid_z", N, "-mat_law", "pl
 m.set_timing(True)
 if a.maxq is not None:
     m.set_option("split_maxq", a.maxq)
+if a.exc_max is not None:
+    m.set_option("vi_exc_max", a.exc_max)
 steps = []
 t_all = time.perf_counter()
 for ts in range(a.ts):
@@ -39,7 +43,8 @@ for ts in range(a.ts):
     nl, fmax = m.nonlinear_stats()
     tm = m.timing()
     steps.append(dict(ts=ts, newton_its=out["newton_its"], ksp_its=out["ksp_its"], res=out["res"], seconds=dt,
-                      nonlinear_gps=nl, f_trial_max=fmax,
+                      nonlinear_gps=nl, f_trial_max=fmax, storage=m.get_info()["storage"],
+                      vi_exc_nodes=m.get_info()["vi_exc_nodes"],
                       last_phases_ms={k: tm[k] for k in ("strains_ms", "homogenize_ms", "residual_ms", "jacobian_ms",
                                                          "solve_ms")}))
     print(json.dumps(steps[-1]), file=sys.stderr, flush=True)
@@ -49,7 +54,8 @@ info = m.get_info()
 print(json.dumps({"workload": f"config 5 path: {N}^3 non-linear Newton (J2 callback), {a.ts} time steps, dt {a.dt}",
                   "micro_n": a.micro_n, "micro_n_note": "no micro-scale FE problem behind the device law (MicroPP out of scope)",
                   "device_gb": m.get_info()["device_bytes"] / 1e9,
-                  "mat_type": a.mat_type, "storage": {0: "aij-blocks", 1: "sbaij", 2: "aij-split"}[info["storage"]],
+                  "mat_type": a.mat_type, "storage": {0: "aij-blocks", 1: "sbaij", 2: "aij-split", 3: "aij-vi"}[info["storage"]],
+                  "vi_exc_nodes": info["vi_exc_nodes"], "vi_blocks": info["vi_blocks"],
                   "split_slots": info["split_slots"], "split_bits": info["split_bits"], "newton_its": nits, "cg_its": sum(sum(s["ksp_its"]) for s in steps),
                   "seconds": tot, "ms_per_newton_iter": tot / max(nits, 1) * 1e3,
                   "dof_per_s": 3 * N ** 3 * nits / tot, "steps": steps}))
