@@ -54,7 +54,7 @@ static int free_ctx(Ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
-  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->dinv, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
+  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
                   c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2, c->elem_plain, c->cref, c->vi_xslot,
                   c->vi_xlist, c->vi_exc,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
@@ -146,10 +146,12 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   // matrix storage: AIJ blocks V only for -mat_aij_split 0 (the AIJ-split path allocates it
   // lazily if a correction is not exact, mcx_assembly_jac); U for sbaij and AIJ-split; the
   // AIJ-split corrections D are sized by build_split to the active slots
+  // jdd [VI_MAX][3] and the Jacobi vector dinv behind it in one buffer: the block-indexed CG
+  // kernels read an exception node's (jix 255) inverse diagonal at jdd + 3 VI_MAX + 3n
   if ((rc = dalloc(c, &c.u_pad, npad)) || (rc = dalloc(c, &c.p_pad, npad)) || (rc = dalloc(c, &c.b, nown3)) ||
       (rc = dalloc(c, &c.du, nown3)) || (rc = dalloc(c, &c.r, nown3)) || (rc = dalloc(c, &c.z, nown3)) ||
-      (rc = dalloc(c, &c.w, nown3)) || (rc = dalloc(c, &c.dinv, nown3)) ||
-      (rc = dalloc(c, &c.jix, (int64_t)g.nown)) || (rc = dalloc(c, &c.jdd, 3 * VI_MAX)) || (rc = dalloc(c, &c.tmp, nown3)) ||
+      (rc = dalloc(c, &c.w, nown3)) || (rc = dalloc(c, &c.jdd, 3 * VI_MAX + nown3)) ||
+      (rc = dalloc(c, &c.jix, (int64_t)g.nown)) || (rc = dalloc(c, &c.tmp, nown3)) ||
       (c.o.mat_type == MCX_MAT_SBAIJ && (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))) ||
       (c.o.mat_type == MCX_MAT_AIJ && !c.aij_split && (rc = dalloc(c, &c.V, c.ngroups * NPAIR * 128))) ||
       (rc = dalloc(c, &c.eps, 6 * 8 * E)) || (rc = dalloc(c, &c.sig, 6 * 8 * E)) ||
@@ -157,6 +159,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
       (rc = dalloc(c, &c.red, 16)) || (rc = dalloc(c, &c.red_loc, 16)) || (rc = dalloc(c, &c.cg, 2)) ||
       (rc = dalloc(c, &c.hist, (int64_t)o->ksp_max_it + 2)) || (rc = dalloc(c, &c.ke_uni, 576)))
     return rc;
+  c.dinv = c.jdd + 3 * VI_MAX;
   // per-GP tangent: only laws that hand one over (the isotropic elastic C is a kernel argument)
   c.partials2 = c.partials + c.partials_cap / 2;
   if (o->mat_law != MCX_LAW_ELASTIC &&

@@ -2141,9 +2141,9 @@ __global__ void k_jacobi_vib(Geo g, const unsigned char* __restrict__ I, const d
   const int n = blockIdx.x * TPB + threadIdx.x;
   if (n >= g.nown) return;
   const int id = I[(((int64_t)(n >> 6) * 2 + 0) * 64 + (n & 63)) * 16 + 13];
-  jix[n] = (unsigned char)id;
   const unsigned xs =
       exc ? *reinterpret_cast<const unsigned*>(I + (((int64_t)(n >> 6) * 2 + 1) * 64 + (n & 63)) * 16 + 12) : 0u;
+  jix[n] = xs ? 255 : (unsigned char)id;  // 255: the CG kernels read dinv (jac_inv)
   const double* d = xs ? exc + ((int64_t)(xs - 1) * 27 + 13) * 9 : bdict + id * VIB_STRIDE;
 #pragma unroll
   for (int r = 0; r < 3; r++) dinv[3 * n + r] = jacobi_inv(d[r * 4]);
@@ -2468,23 +2468,31 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       // an exception node (EXC instantiations only): its 27 plain blocks from exc [slot][27][9], a
       // rolled loop of its own so the indexed path below keeps its registers; same order and
       // products as the indexed rows
+      // Blocks in groups of 3 (one dy row): the group's 27 values are loaded together, one
+      // round trip per group instead of per block.
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
       const double* eb = exc + (int64_t)(c1[3] - 1) * 243;
 #pragma unroll 1
-      for (int nb = 0; nb < 27; nb++) {
-        const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
-        const int xo = ((k + dz - k0 + 1) % R) * PLANE + (ly + 1 + dy) * RL + 3 * (lx + 1 + dx);
-        const double xv[3] = {xs[0][xo], xs[0][xo + 1], xs[0][xo + 2]};
-        if (nb == 13) {
-          xc0 = xv[0];
-          xc1 = xv[1];
-          xc2 = xv[2];
-        }
+      for (int nb0 = 0; nb0 < 27; nb0 += 3) {
+        double av[27];
 #pragma unroll
-        for (int q = 0; q < 9; q++) {
-          const int r = q / 3, cc = q % 3;
-          double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
-          yr = FMA ? __builtin_fma(eb[nb * 9 + q], xv[cc], yr) : yr + eb[nb * 9 + q] * xv[cc];
+        for (int q = 0; q < 27; q++) av[q] = eb[nb0 * 9 + q];
+        const int dy = (nb0 / 3) % 3 - 1, dz = nb0 / 9 - 1;
+        const int xo = ((k + dz - k0 + 1) % R) * PLANE + (ly + 1 + dy) * RL + 3 * lx;
+#pragma unroll
+        for (int t = 0; t < 3; t++) {
+          const double xv[3] = {xs[0][xo + 3 * t], xs[0][xo + 3 * t + 1], xs[0][xo + 3 * t + 2]};
+          if (nb0 + t == 13) {
+            xc0 = xv[0];
+            xc1 = xv[1];
+            xc2 = xv[2];
+          }
+#pragma unroll
+          for (int q = 0; q < 9; q++) {
+            const int r = q / 3, cc = q % 3;
+            double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
+            yr = FMA ? __builtin_fma(av[t * 9 + q], xv[cc], yr) : yr + av[t * 9 + q] * xv[cc];
+          }
         }
       }
       const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
@@ -2810,12 +2818,20 @@ __device__ __forceinline__ void st(double* p, double v) {
 // Jacobi inverse diagonal of DOF 3n+d.  DIX (block-indexed value storage): dinv is the
 // dictionary's inverse diagonals [VI_MAX][3] and jix the owned nodes' diagonal-block index (one
 // byte per node instead of 24 B of dinv); the values are k_jacobi_vib's, so z = r * dinv is
-// bit-identical either way.
+// bit-identical either way.  jix 255 (an exception node, or dictionary block 255): the node's
+// own entry of the Jacobi vector, which the context keeps right behind the dictionary's
+// (c.dinv = c.jdd + 3 VI_MAX) — the same value for a dictionary block, the only one for an
+// exception node; a branch no lane of an exception-free wave takes.
 template <bool DIX>
 __device__ __forceinline__ double jac_inv(const double* __restrict__ dinv, const unsigned char* __restrict__ jix,
                                           int n, int d) {
-  if constexpr (DIX) return dinv[3 * jix[n] + d];
-  else return dinv[3 * n + d];
+  if constexpr (DIX) {
+    const unsigned jx = jix[n];
+    if (jx == 255u) return dinv[3 * VI_MAX + 3 * n + d];
+    return dinv[3 * jx + d];
+  } else {
+    return dinv[3 * n + d];
+  }
 }
 
 // z of DOF q = 3n+d: stored z, or (DIX) recomputed from r (the update kernel then writes no z)
@@ -4121,8 +4137,7 @@ void launch_cg_xfinal(Ctx& c) {
 // CG vector kernels' Jacobi form: DIX (block-indexed value storage, option cg_dix) reads one
 // diagonal-block index byte per node and recomputes z = D^-1 r from r where it is used, so the
 // update writes no z and reads no dinv vector (two fewer vectors per iteration)
-// (exception nodes have no dictionary diagonal: the Jacobi vector dinv then)
-static bool cg_dix(const Ctx& c) { return c.cg_dix && c.fmt == FMT_VI && c.vi_block && !c.vi_nexc; }
+static bool cg_dix(const Ctx& c) { return c.cg_dix && c.fmt == FMT_VI && c.vi_block; }
 
 // instantiate CALL with constexpr NT (non-temporal stores) and DX (DIX) from run-time flags
 #define MCX_NT_DIX(ntv, dixv, CALL)                      \

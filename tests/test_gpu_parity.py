@@ -260,6 +260,13 @@ def test_aij_vi_exception_nodes(grid, stage, vi_tx, tile):
         its, rn, reason = m.solve_Ax()
         assert reason > 0 and abs(its - ref_its) <= 1
         assert np.linalg.norm(m.du() - P.du()) <= 50 * rtol * np.linalg.norm(P.du())
+        # the CG's Jacobi from the diagonal index (exception nodes: jix 255 -> the Jacobi vector)
+        # is bitwise the Jacobi vector's
+        du = m.du()
+        m.set_option("cg_dix", 0)
+        its0, _, _ = m.solve_Ax()
+        assert its0 == its and np.array_equal(m.du(), du)
+        m.set_option("cg_dix", 1)
         # the same matrix with exceptions refused: AIJ-split, bit-exact too
         m.set_option("vi_exc_max", 0)
         m.assembly_jac()
