@@ -1407,6 +1407,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.vi_block_on = value != 0.;
     return 0;
   }
+  if (!std::strcmp(name, "vi_wmap")) {
+    c.vi_wmap = value != 0.;
+    return 0;
+  }
   if (!std::strcmp(name, "vi_ring3")) {
     c.vi_ring3 = value != 0.;
     return 0;

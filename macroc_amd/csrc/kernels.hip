@@ -955,6 +955,7 @@ __global__ __launch_bounds__(TPB) void k_spmv_sym(Geo g, const double* __restric
 struct ZTiling {
   int ntx, nty, nzc, kc;  // tiles in x, y; z chunks and planes per chunk
   int dbg = 0;            // timing-only diagnostics (k_spmv_vibm: 1 = every wave takes the scalar path)
+  int wmap = 1;           // k_spmv_vibm PATCH: 1 = patches on SIMDs as a Latin square, 0 = row-major (A/B)
 };
 
 static ZTiling z_tiling(const Geo& g, int ztx, int zty, int want) {
@@ -2294,8 +2295,21 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
   const double* psrc = FP ? fp.pb[(cgi & 1) ^ 1] : x;
   double* pdst = FP ? fp.pb[cgi & 1] : nullptr;
   const int wv = me >> 6, ln = me & 63;
-  const int lx = PATCH ? (wv % (TX / 16)) * 16 + (ln & 15) : me % TX;
-  const int ly = PATCH ? (wv / (TX / 16)) * 4 + (ln >> 4) : me / TX;
+  // PATCH: wave wv -> 16 x 4 patch (px, py).  The waves of a workgroup go to the CU's 4 SIMDs
+  // round robin (SIMD wv % 4), and the patches holding a tile's x-edge column (px = 0 or the
+  // last) or y-edge row (py = 0 or the last) are the ones whose nodes differ in their block
+  // indices (domain boundary, Dirichlet neighbours): they take the slower LDS-dictionary path.
+  // Row-major numbering put a tile's 4 x-edge patches on one SIMD, whose waves then finished
+  // the plane last; the Latin square (SIMD = (px + py) mod 4 within each group of 4 columns)
+  // puts any column's and any row's patches on different SIMDs.
+  constexpr int TYP = TY / 4;
+  int px = wv % (TX / 16), py = wv / (TX / 16);
+  if (PATCH && zt.wmap) {
+    py = (wv >> 2) % TYP;
+    px = (wv / (4 * TYP)) * 4 + (((wv & 3) - py) & 3);
+  }
+  const int lx = PATCH ? px * 16 + (ln & 15) : me % TX;
+  const int ly = PATCH ? py * 4 + (ln >> 4) : me / TX;
   const int i = i0 + lx, j = j0 + ly;
   const bool inxy = i < g.nx && j < g.ny;
   const int PX = g.PX, PXY = g.PX * g.PY;
@@ -3887,6 +3901,7 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
     if (vi_staged(c)) {  // x staged in LDS, 1024-node tiles marching z-chunks
       ZTiling zt = vis_tiling(c);
       zt.dbg = c.split_dbg;
+      zt.wmap = c.vi_wmap;
       int tx, ty;
       vis_shape(c, tx, ty);
 #define MCX_VIBM(TXV, TYV, XVV, UV, PV, ...)                                                                          \

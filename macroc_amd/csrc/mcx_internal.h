@@ -141,7 +141,7 @@ struct Ctx {
   double* r = nullptr;
   double* z = nullptr;
   double* w = nullptr;
-  double* dinv = nullptr;    // Jacobi inverse diagonal
+  double* dinv = nullptr;    // Jacobi inverse diagonal (inside the jdd buffer: jdd + 3 VI_MAX)
   unsigned char* jix = nullptr;  // block-indexed storage: each owned node's diagonal-block index
   double* jdd = nullptr;         // block-indexed storage: the dictionary's inverse diagonals [VI_MAX][3]
   int cg_dix = 1;                // CG kernels: Jacobi from jix/jdd, z recomputed from r (option cg_dix)
@@ -195,6 +195,7 @@ struct Ctx {
                              // rounding-level, not bit-exact); implies vi_uni + vi_patch
   int vi_patch = 1;          // with vi_uni: 16 x 4 node patches per wave (option vi_patch)
   int vi_ring3 = 0;          // A/B: the 3-slot x ring (two barriers per plane) for 64x16 tiles (option vi_ring3)
+  int vi_wmap = 1;           // staged block-indexed SpMV: 16x4 patches on SIMDs as a Latin square (option vi_wmap; 0: row-major)
   int vi_tx = 0;             // staged block-indexed SpMV tile width 256 | 128 | 64 (0: 64; option vi_tx)
   int vi_uni = 1;            // staged block-indexed SpMV: wave-uniform blocks from scalar loads (option vi_uni)
   int vi_xread = 1;          // staged block-indexed SpMV: x as unpaired 8-B LDS reads (option vi_xread; 0: compiler's pairs)
