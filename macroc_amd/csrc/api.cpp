@@ -55,7 +55,7 @@ static int free_ctx(Ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
   void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
-                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2, c->elem_plain, c->cref, c->vi_xslot,
+                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2, c->xdone, c->elem_plain, c->cref, c->vi_xslot,
                   c->vi_xlist, c->vi_exc,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf, c->halo.d_bnd};
@@ -157,7 +157,8 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
       (rc = dalloc(c, &c.eps, 6 * 8 * E)) || (rc = dalloc(c, &c.sig, 6 * 8 * E)) ||
       (rc = dalloc(c, &c.partials, c.partials_cap = 4 * std::max(max_spmv_blocks(c), node_blocks(c)) + 64)) ||
       (rc = dalloc(c, &c.red, 16)) || (rc = dalloc(c, &c.red_loc, 16)) || (rc = dalloc(c, &c.cg, 2)) ||
-      (rc = dalloc(c, &c.hist, (int64_t)o->ksp_max_it + 2)) || (rc = dalloc(c, &c.ke_uni, 576)))
+      (rc = dalloc(c, &c.hist, (int64_t)o->ksp_max_it + 2)) || (rc = dalloc(c, &c.ke_uni, 576)) ||
+      (rc = dalloc(c, &c.p_pad2, npad)) || (rc = dalloc(c, &c.xdone, 1)))  // p's second buffer (cg_pdb, cg_fusep)
     return rc;
   c.dinv = c.jdd + 3 * VI_MAX;
   // per-GP tangent: only laws that hand one over (the isotropic elastic C is a kernel argument)
@@ -200,6 +201,8 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
 static int cg_solve(Ctx& c, int* its, double* rnorm, int* reason) {
   launch_jacobi(c);  // PCSetUp_Jacobi happens inside KSPSolve in the reference
   c.fusep_used = false;  // set by cg_iteration when the p update runs inside the SpMV
+  c.pdb_used = cg_pdb(c);
+  if (c.pdb_used) MCX_HIP(hipMemsetAsync(c.xdone, 0, sizeof(int), c.stream));
   CgState s{};
   s.rtol = c.o.ksp_rtol;
   s.abstol = c.o.ksp_abstol;
@@ -233,6 +236,7 @@ static int cg_solve(Ctx& c, int* its, double* rnorm, int* reason) {
         pair_it.push_back(issued);
         npairs++;
       }
+      c.cg_it = issued;
       if ((rc = cg_iteration(c, e0, e1, q == 0, q == CH - 1))) return rc;
     }
     MCX_HIP(hipMemcpyAsync(&c.h_cg[slot], c.cg, sizeof(CgState), hipMemcpyDeviceToHost, c.stream));
@@ -1407,6 +1411,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.vi_block_on = value != 0.;
     return 0;
   }
+  if (!std::strcmp(name, "cg_pdb")) {
+    c.cg_pdb = value != 0.;
+    return 0;
+  }
   if (!std::strcmp(name, "vi_wmap")) {
     c.vi_wmap = value != 0.;
     return 0;
@@ -1423,10 +1431,8 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     }
     return 0;
   }
-  if (!std::strcmp(name, "cg_fusep")) {  // the second p buffer is allocated on first use
+  if (!std::strcmp(name, "cg_fusep")) {
     c.cg_fusep = value != 0.;
-    if (c.cg_fusep && !c.p_pad2 && c.nranks == 1 && !c.comm && !c.lg)
-      return dalloc(c, &c.p_pad2, (int64_t)c.g.PX * c.g.PY * c.g.PZ * 3);
     return 0;
   }
   if (!std::strcmp(name, "vi_exc_max")) {  // takes effect at the next mcx_assembly_jac

@@ -2885,6 +2885,72 @@ __device__ __forceinline__ bool sent_node(const Geo& g, int i, int j, int k) {
          (j == g.ny - 1 && g.ys + g.ny < g.NY) || (k == 0 && g.zs > 0) || (k == g.nz - 1 && g.zs + g.nz < g.NZ);
 }
 
+// PDB (option cg_pdb): p double-buffered, p(i) in pb[i & 1].  Iteration i reads p(i-1) from the
+// other buffer and writes p(i) = z + (beta/betaold) p(i-1); VecAXPY(x) runs on odd iterations
+// only, both owed terms in PETSc's order: x = (x + a(i-2) p(i-2)) + a(i-1) p(i-1), p(i-2) being
+// read from p(i)'s buffer before it is overwritten (i = 1: the one term a(0) p(0)).  Even
+// iterations move 73 B per node instead of 121, odd ones 145.  xdone = the last odd iteration
+// (every term j < xdone applied); k_cg_xfinal applies the rest.
+template <bool NT, bool DIX>
+__device__ __forceinline__ void pupdate_node_db(const Geo& g, int n, const double* __restrict__ z,
+                                                const double* __restrict__ dinv, const unsigned char* __restrict__ jix,
+                                                double* __restrict__ pb0, double* __restrict__ pb1,
+                                                double* __restrict__ x, const CgState* __restrict__ cg) {
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  const int pc = pad_of(g, i, j, k);
+  const int it = cg->i;
+  double* pn = (it & 1) ? pb1 : pb0;
+  const double* po = (it & 1) ? pb0 : pb1;
+  if (it == 0) {
+#pragma unroll
+    for (int d = 0; d < 3; d++) st<NT>(&pn[3 * pc + d], z_of<DIX>(z, dinv, jix, n, d));
+    return;
+  }
+  // every load before any store (pn / po are selected at run time: the compiler cannot tell
+  // them apart, and would otherwise order each load after the previous component's stores)
+  const double bc = cg->bcoef, a = cg->alpha;
+  double pv[3], zv[3], xv[3], pp[3];
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    pv[d] = po[3 * pc + d];
+    zv[d] = z_of<DIX>(z, dinv, jix, n, d);
+  }
+  if (it & 1) {
+    const double ap = cg->alpha_prev;
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      xv[d] = x[3 * n + d];
+      pp[d] = it >= 3 ? pn[3 * pc + d] : 0.;
+    }
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      if (it >= 3) xv[d] = xv[d] + ap * pp[d];
+      st<NT>(&x[3 * n + d], xv[d] + a * pv[d]);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 3; d++) st<NT>(&pn[3 * pc + d], zv[d] + bc * pv[d]);
+}
+
+template <bool NT, bool DIX, bool SKIP_SENT = false>
+__global__ void k_cg_pupdate_db(Geo g, const double* __restrict__ z, const double* __restrict__ dinv,
+                                const unsigned char* __restrict__ jix, double* __restrict__ pb0,
+                                double* __restrict__ pb1, double* __restrict__ x, const CgState* __restrict__ cg,
+                                int* __restrict__ xdone, const int* __restrict__ list, int64_t cnt) {
+  if (cg->reason) return;
+  const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  if (t == 0 && (cg->i & 1)) *xdone = cg->i;
+  if (t >= cnt) return;
+  const int n = list ? list[t] : (int)t;
+  if (SKIP_SENT) {
+    int i, j, k;
+    node_ijk(g, n, i, j, k);
+    if (sent_node(g, i, j, k)) return;
+  }
+  pupdate_node_db<NT, DIX>(g, n, z, dinv, jix, pb0, pb1, x, cg);
+}
+
 // SKIP_SENT: the sent nodes were updated before the halo exchange (k_cg_pupdate_list)
 template <bool NT, bool DIX, bool SKIP_SENT = false>
 __global__ void k_cg_pupdate(Geo g, const double* __restrict__ z, const double* __restrict__ dinv,
@@ -2915,7 +2981,25 @@ __global__ void k_cg_pupdate_list(Geo g, const double* __restrict__ z, const dou
 // the last iteration's x += alpha p (when that iteration reached its update); ppad2: the fused
 // path's second p buffer (p of iteration i in buffer i & 1)
 __global__ void k_cg_xfinal(Geo g, const double* __restrict__ ppad, const double* __restrict__ ppad2,
-                            double* __restrict__ x, const CgState* __restrict__ cg) {
+                            double* __restrict__ x, const CgState* __restrict__ cg, const int* __restrict__ xdone) {
+  if (xdone) {  // PDB: the terms j = xdone .. xp still owed (at most two), in order
+    const int xd = *xdone, xp = cg->xp;
+    if (xp < xd) return;
+    int n = blockIdx.x * TPB + threadIdx.x;
+    if (n >= g.nown) return;
+    int i, j, k;
+    node_ijk(g, n, i, j, k);
+    const int pc = pad_of(g, i, j, k);
+    const double* pl = (xp & 1) ? ppad2 : ppad;
+    const double* pp = (xp & 1) ? ppad : ppad2;
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      double xv = x[3 * n + d];
+      if (xp - 1 >= xd) xv = xv + cg->alpha_prev * pp[3 * pc + d];
+      x[3 * n + d] = xv + cg->alpha * pl[3 * pc + d];
+    }
+    return;
+  }
   if (ppad2) {
     // fused path: odd iterations' updates applied x through them, so only an even last
     // successful iteration xp (whose update ran, but applies no x) leaves a(xp) p(xp) pending;
@@ -4146,7 +4230,7 @@ int cg_finish_init(Ctx& c) {
 
 void launch_cg_xfinal(Ctx& c) {
   hipLaunchKernelGGL(k_cg_xfinal, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.p_pad,
-                     c.fusep_used ? c.p_pad2 : nullptr, c.du, c.cg);
+                     c.fusep_used || c.pdb_used ? c.p_pad2 : nullptr, c.du, c.cg, c.pdb_used ? c.xdone : nullptr);
 }
 
 // CG vector kernels' Jacobi form: DIX (block-indexed value storage, option cg_dix) reads one
@@ -4177,6 +4261,24 @@ void launch_cg_pupdate(Ctx& c, int part) {
   const bool dix = cg_dix(c);
   const double* zs = dix ? c.r : c.z;
   const double* jd = dix ? c.jdd : c.dinv;
+  if (c.pdb_used) {  // p double-buffered, x every second iteration
+    if (part == 1) {
+      if (!c.halo.nbnd) return;
+      MCX_NT_DIX(c.cg_nt, dix,
+                 hipLaunchKernelGGL((k_cg_pupdate_db<NT, DX>), dim3(nblk(c.halo.nbnd)), dim3(TPB), 0, c.stream, c.g,
+                                    zs, jd, c.jix, c.p_pad, c.p_pad2, c.du, c.cg, c.xdone, c.halo.d_bnd,
+                                    c.halo.nbnd));
+    } else if (part == 2) {
+      MCX_NT_DIX(c.cg_nt, dix,
+                 hipLaunchKernelGGL((k_cg_pupdate_db<NT, DX, true>), dim3(nbn), dim3(TPB), 0, c.stream, c.g, zs, jd,
+                                    c.jix, c.p_pad, c.p_pad2, c.du, c.cg, c.xdone, nullptr, (int64_t)c.g.nown));
+    } else {
+      MCX_NT_DIX(c.cg_nt, dix,
+                 hipLaunchKernelGGL((k_cg_pupdate_db<NT, DX>), dim3(nbn), dim3(TPB), 0, c.stream, c.g, zs, jd,
+                                    c.jix, c.p_pad, c.p_pad2, c.du, c.cg, c.xdone, nullptr, (int64_t)c.g.nown));
+    }
+    return;
+  }
   if (part == 1) {
     if (!c.halo.nbnd) return;
     const unsigned nb = nblk(c.halo.nbnd);
@@ -4199,6 +4301,13 @@ void launch_cg_pupdate(Ctx& c, int part) {
 // beta step in k_reduce so the host poll and the next chunk read c.cg.  first: the chunk's first
 // iteration (its p update starts from c.cg).
 static bool fused(const Ctx& c) { return c.fuse && c.nranks == 1 && !c.comm; }
+
+// the solve's p update: double-buffered (PDB) unless the p update is fused into the SpMV
+// (fusep) or into the scalar steps (single rank, <= 1,024 update blocks: k_cg_pupdate_fb)
+bool cg_pdb(const Ctx& c) {
+  const int nbu = (int)((c.g.nown + UTPB - 1) / UTPB);
+  return c.cg_pdb && c.p_pad2 && c.xdone && !fusep(c) && !(fused(c) && nbu <= 1024);
+}
 
 int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) {
   const int nbs = (int)spmv_nparts(c);
@@ -4227,6 +4336,9 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) 
                          c.p_pad, c.p_pad2, c.partials2, nbu, c.cg);
     return reduce_and_logic(c, 2, nbu, RED_BETA, true, c.partials2, c.cg);
   }
+  // p of this iteration (PDB: buffer it & 1, `it` = the host's count of launched iterations, which
+  // is the device's cg->i for every iteration that runs; the fused small-grid path fb has one buffer)
+  double* pcur = c.pdb_used && (c.cg_it & 1) ? c.p_pad2 : c.p_pad;
   if (fb && !first) {
     MCX_NT_DIX(c.cg_nt, dix,
                hipLaunchKernelGGL((k_cg_pupdate_fb<NT, DX>), dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, zs, jd,
@@ -4234,15 +4346,15 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) 
   } else if (c.nranks > 1 && c.overlap && c.halo.nbnd) {
     // the sent nodes' p first, then their exchange overlaps the interior p update
     launch_cg_pupdate(c, 1);
-    if ((rc = halo_start(c, c.p_pad))) return rc;
+    if ((rc = halo_start(c, pcur))) return rc;
     launch_cg_pupdate(c, 2);
-    if ((rc = halo_finish(c, c.p_pad))) return rc;
+    if ((rc = halo_finish(c, pcur))) return rc;
   } else {
     launch_cg_pupdate(c, 0);
   }
-  if (!(c.nranks > 1 && c.overlap && c.halo.nbnd) && (rc = halo_exchange(c, c.p_pad))) return rc;
+  if (!(c.nranks > 1 && c.overlap && c.halo.nbnd) && (rc = halo_exchange(c, pcur))) return rc;
   if (ev0) MCX_HIP(hipEventRecord(ev0, c.stream));
-  launch_spmv(c, c.p_pad, c.w, true, true);
+  launch_spmv(c, pcur, c.w, true, true);
   if (ev1) MCX_HIP(hipEventRecord(ev1, c.stream));
   if (fa) {
     MCX_NT_DIX(c.cg_nt, dix,

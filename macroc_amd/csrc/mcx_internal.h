@@ -136,6 +136,10 @@ struct Ctx {
   double* p_pad2 = nullptr;  // its second buffer (single rank: the p update fused into the SpMV, cg_fusep)
   int cg_fusep = 0;          // option cg_fusep: fuse the CG p update into the value-indexed SpMV (single rank; A/B: no gain)
   bool fusep_used = false;   // the last solve ran the fused kernel (timing: its bytes per launch)
+  int cg_pdb = 1;            // option cg_pdb: p double-buffered (p_pad / p_pad2), VecAXPY(x) every second iteration
+  bool pdb_used = false;     // the current solve runs the double-buffered p update
+  int* xdone = nullptr;      // PDB: the last odd iteration whose p update applied the x terms owed
+  int cg_it = 0;             // iteration index of the cg_iteration being launched
   double* b = nullptr;       // residual (owned, PETSc-local order)
   double* du = nullptr;      // CG solution x
   double* r = nullptr;
@@ -316,6 +320,7 @@ int64_t spmv_nparts(const Ctx& c);   // partial sums the CG's SpMV leaves (its o
 int64_t node_blocks(const Ctx& c);
 bool vi_staged(const Ctx& c);
 bool fusep(const Ctx& c);  // the CG's p update runs inside the value-indexed SpMV
+bool cg_pdb(const Ctx& c);  // the CG's p update double-buffered (x every second iteration)
 // z-marching SpMV tile of the current storage (tx, ty, planes per chunk); all 0 for gathered kernels
 void spmv_tile(const Ctx& c, int* tx, int* ty, int* kc);
 int dirichlet_mask_host(const Geo& g, int gi, int gj, int gk);

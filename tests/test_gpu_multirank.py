@@ -232,6 +232,22 @@ def test_cg_dix_bitwise(grid, procs):
         assert a["its"] == b["its"] and a["reason"] == b["reason"] and np.array_equal(a["du"], b["du"])
 
 
+@pytest.mark.parametrize("grid,procs", [((20, 12, 10), (2, 2, 1)), ((12, 10, 14), (2, 2, 2))])
+def test_cg_pdb_multirank_bitwise(grid, procs):
+    """The double-buffered p update (cg_pdb) on decomposed subdomains: sent nodes first, halo of
+    the iteration's p buffer overlapping the interior update; du bitwise the single-buffer
+    solve's, same iteration count."""
+    NX, NY, NZ = grid
+    px, py, pz = procs
+    argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
+            "-da_processors_z", pz, "-ksp_rtol", "1e-10"]
+    x = np.zeros(3 * NX * NY * NZ)
+    on = run_group(argv, px * py * pz, newton_step(x, [("cg_pdb", 1)]))
+    off = run_group(argv, px * py * pz, newton_step(x, [("cg_pdb", 0)]))
+    for a, b in zip(on, off):
+        assert a["its"] == b["its"] and a["reason"] == b["reason"] and np.array_equal(a["du"], b["du"])
+
+
 def test_rccl_transport_one_rank():
     """The RCCL transport on one GPU: a one-rank communicator routes every reduction through
     the multi-rank path (k_reduce partial sums, ncclAllReduce on the compute stream,

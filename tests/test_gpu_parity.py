@@ -585,6 +585,31 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
         assert np.linalg.norm(m.du() - P.du()) <= 1e-10 * np.linalg.norm(P.du())
 
 
+
+@pytest.mark.parametrize("maxits", [None, 37, 38, 1, 2])
+@pytest.mark.parametrize("storage", ["vi", "split"])
+def test_cg_pdb_bitwise(maxits, storage):
+    """Option cg_pdb (default): p double-buffered and VecAXPY(x) applied on odd iterations only,
+    both owed terms in PETSc's order, the rest by k_cg_xfinal — bitwise the solve of the
+    single-buffer p update: converged, and stopped by maxits after odd and even iteration
+    counts (1 and 2 included)."""
+    NX, NY, NZ = 70, 20, 12
+    extra = [] if storage == "vi" else ["-mat_aij_vi", 0]
+    argv = argv_for(NX, NY, NZ, 1e-12, extra) + (["-ksp_max_it", maxits] if maxits else [])
+    out = []
+    with M.Macroc(argv) as m:
+        m.set_option("cg_fuse", 0)  # the unfused scalar steps (grids > 1,024 update blocks)
+        m.apply_bc_on_u(m.get_displacement(1))
+        m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
+        for pdb in (0, 1, 0, 1):
+            m.set_option("cg_pdb", pdb)
+            its, rn, reason = m.solve_Ax()
+            out.append((its, reason, m.du()))
+    for its, reason, du in out[1:]:
+        assert (its, reason) == out[0][:2] and np.array_equal(du, out[0][2])
+    if maxits:
+        assert out[0][:2] == (maxits, -3)
+
 @pytest.mark.parametrize("maxits", [0, 5, 6])
 def test_cg_fused_p_update_bitwise(maxits):
     """Option cg_fusep: the CG's p update inside the value-indexed SpMV (two p buffers) and
