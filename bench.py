@@ -16,9 +16,10 @@ values), its SpMV rows summed with fused multiply-adds (-mat_vi_fma 1, the defau
 the same storage with the bit-exact CPU-order rows (-mat_vi_fma 0) and the AIJ-split storage
 of the same matrix are measured after it (1 warmup + 1 step each, `variants` in the line;
 `--variants aij-vi-exact,aij-split,aij-blocks,sbaij` for more) while the `--budget` wall time
-lasts.  Rank 0 prints ONE JSON line (the contract in
-the task statement / DESIGN.md §6) once the headline, the variants and the CPU baseline are
-measured.
+lasts.  Also on one GPU, BASELINE config 5's path (128^3, the J2 Gauss-point law, three time
+steps of non-linear Newton, default AIJ storage with exception nodes) is run and reported as
+`config5` (`--config5 0` skips it).  Rank 0 prints ONE JSON line (the contract in the task
+statement / DESIGN.md §6) once the headline, the variants and the CPU baseline are measured.
 """
 import argparse
 import json
@@ -287,6 +288,33 @@ def measure(argv, rank, world, comm_id, args, steps, warmup):
             "warmup_s": t_warm}
 
 
+def nonlinear_leg(G, ts, dt, rtol, device):
+    """BASELINE config 5's path (G^3, the J2 Gauss-point law, non-linear Newton; tools/bench_nonlinear.py):
+    time steps 0 .. ts-1 of src/main.c:49-109 in this process, default AIJ storage.  Reported beside
+    the headline (config5 in the line), never the headline: per-GP tangents keep the plastic zone's
+    nodes as exception nodes."""
+    m = M.Macroc(["-da_grid_x", G, "-da_grid_y", G, "-da_grid_z", G, "-mat_law", "plastic", "-ksp_rtol", repr(rtol),
+                  "-ts", ts, "-dt", dt, "-micro_n", 10, "-device", device])
+    try:
+        m.set_timing(True)
+        steps, t0 = [], time.perf_counter()
+        for t in range(ts):
+            out = m.time_step(t)
+            info = m.get_info()
+            steps.append({"ts": t, "newton_its": out["newton_its"], "ksp_its": out["ksp_its"],
+                          "nonlinear_gps": m.nonlinear_stats()[0], "storage": info["storage"],
+                          "vi_exc_nodes": info["vi_exc_nodes"]})
+        m.synchronize()
+        sec = time.perf_counter() - t0
+    finally:
+        m.finish()
+    nits = sum(s["newton_its"] for s in steps)
+    return {"workload": f"config 5 path: {G}^3 J2 law, {ts} time steps (step 0: zero load), dt {dt}, rtol {rtol:g}",
+            "mat_type": "aij", "storage": {0: "aij-blocks", 1: "sbaij", 2: "aij-split", 3: "aij-vi"}[steps[-1]["storage"]],
+            "newton_its": nits, "cg_its": sum(sum(s["ksp_its"]) for s in steps), "seconds": sec,
+            "ms_per_newton_iter": sec / max(nits, 1) * 1e3, "dof_per_s": 3 * G ** 3 * nits / sec, "steps": steps}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -304,6 +332,9 @@ def main():
                          "'variants' (comma list; default aij-split on one GPU, none on several; skipped once "
                          "--budget would be exceeded)")
     ap.add_argument("--budget", type=float, default=480.0, help="wall seconds the optional variants may use up to")
+    ap.add_argument("--config5", type=int, default=None,
+                    help="grid of the config-5 leg (J2 law, non-linear Newton, 3 time steps) reported as 'config5' "
+                         "(default 128 on one GPU, 0 = skip; within --budget)")
     ap.add_argument("--wall", type=float, default=570.0,
                     help="wall seconds the invocation must fit: warmup steps after the first are skipped when the "
                          "timed steps would not fit (reported as warmup_run); the timed steps are never cut")
@@ -354,6 +385,14 @@ def main():
             "spmv_frac": vr["achieved"] / PEAK_HBM_GBS, "spmv_traffic": pmc_traffic(vr["storage"], NX, NY, NZ),
             "phases_ms": {k: vr["tm"][k] for k in ("jacobian_ms", "solve_ms")}, "check": vr["check"]})
         log("variant " + json.dumps(variants[-1]))
+    config5 = None
+    c5 = args.config5 if args.config5 is not None else (128 if world == 1 else 0)
+    if c5 > 0 and rank == 0:
+        if time.perf_counter() - T_START + 60 > args.budget:
+            log(f"config5 leg: skipped (budget {args.budget:.0f}s)")
+        else:
+            config5 = nonlinear_leg(c5, 3, 0.01, args.rtol, local)
+            log("config5 " + json.dumps(config5))
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_sample > 0:
@@ -407,6 +446,7 @@ def main():
             "cpu_baseline": cpu,
             "check": check,
             "variants": variants,
+            "config5": config5,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
