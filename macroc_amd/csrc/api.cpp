@@ -801,11 +801,21 @@ int mcx_assembly_jac(void* ctx) {
   CTX(ctx);
   PhaseTimer t(c, PH_JAC);
   int rc;
-  if (c.mat.law != MCX_LAW_ELASTIC) launch_element_ke(c);  // per-GP tangent: element matrices first
-  else launch_elastic_ke(c);  // one material, one element shape: one element matrix
-  if (c.o.mat_type == MCX_MAT_AIJ && c.aij_vi && !c.vi_declined) {
+  const bool table = c.mat.law != MCX_LAW_ELASTIC;
+  const bool try_vi = c.o.mat_type == MCX_MAT_AIJ && c.aij_vi && !c.vi_declined;
+  // a per-GP-tangent law headed for the value-indexed storage with exception nodes: kref and the
+  // non-plain elements' matrices only (the value-indexed build needs no other element matrix)
+  c.plain_ke = false;
+  if (table && try_vi && c.vi_exc_max > 0 && c.vi_block_on && c.vi_bits_max == 4 && c.vib_onepass) {
+    if ((rc = launch_plain_ke(c))) return rc;
+  } else if (table) {
+    launch_element_ke(c);  // per-GP tangent: element matrices first
+  } else {
+    launch_elastic_ke(c);  // one material, one element shape: one element matrix
+  }
+  if (try_vi) {
     // value-indexed AIJ when the matrix has at most VI_MAX distinct values (the elastic law's
-    // matrices); otherwise the next storage below
+    // matrices; per-GP-tangent laws with few exception nodes); otherwise the next storage below
     bool ok = false;
     if ((rc = ensure_VI(c)) || (rc = build_vi(c, &ok))) return rc;
     if (ok) {
@@ -814,7 +824,11 @@ int mcx_assembly_jac(void* ctx) {
       MCX_HIP(hipGetLastError());
       return 0;
     }
-    c.vi_declined = c.mat.law != MCX_LAW_ELASTIC;  // a per-GP tangent stays varied: skip the attempt
+    c.vi_declined = table;  // a per-GP tangent stays varied: skip the attempt
+    if (c.plain_ke) {       // the storages below sum every element's matrix
+      launch_element_ke(c);
+      c.plain_ke = false;
+    }
   }
   if (c.o.mat_type == MCX_MAT_SBAIJ) {
     launch_gather_matrix_sym(c);

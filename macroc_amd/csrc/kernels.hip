@@ -525,8 +525,10 @@ __device__ __forceinline__ void ke_body(const Geo& g, int64_t le, int a, const d
     for (int q = 0; q < 9; q++) Ke[((int64_t)(a * 8 + BH * 4 + bb) * 9 + q) * E + le] = acc[bb][q];
 }
 
+// plain (optional): skip the elements whose tangent is the reference tangent (their matrix is
+// kref, formed once by k_ref_ke)
 __global__ __launch_bounds__(TPB) void k_element_ke(Geo g, const double* __restrict__ ctan, double* __restrict__ Ke,
-                                                    int64_t ngroups) {
+                                                    int64_t ngroups, const unsigned char* __restrict__ plain) {
   // block -> (xcd, a, half, element group): blocks sharing an element group are 8 apart
   const int64_t b = blockIdx.x;
   const int x = (int)(b & 7);
@@ -535,7 +537,7 @@ __global__ __launch_bounds__(TPB) void k_element_ke(Geo g, const double* __restr
   const int64_t grp = (t >> 4) * 8 + x;
   if (grp >= ngroups) return;
   const int64_t le = grp * TPB + threadIdx.x;
-  if (le >= g.nelem) return;
+  if (le >= g.nelem || (plain && plain[le])) return;
   const int a = ah >> 1;
   if (ah & 1) ke_body<1>(g, le, a, ctan, Ke);
   else ke_body<0>(g, le, a, ctan, Ke);
@@ -564,7 +566,9 @@ __global__ void k_elastic_ke(Geo g, Material mat, double* __restrict__ keu) {
 // [576][nelem]), then the Dirichlet rows / columns.
 template <bool TABLE>
 __device__ __forceinline__ void matrix_block(const Geo& g, const Material& mat, const double* __restrict__ Ke,
-                                             int gi, int gj, int gk, int dx, int dy, int dz, double (&val)[9]) {
+                                             int gi, int gj, int gk, int dx, int dy, int dz, double (&val)[9],
+                                             const double* __restrict__ kref = nullptr,
+                                             const unsigned char* __restrict__ plain = nullptr) {
   const int hi = gi + dx, hj = gj + dy, hk = gk + dz;
 #pragma unroll
   for (int q = 0; q < 9; q++) val[q] = 0.;
@@ -581,10 +585,12 @@ __device__ __forceinline__ void matrix_block(const Geo& g, const Material& mat, 
         if (px < 0 || px > 1 || ex < 0 || ex > g.NX - 2) continue;
         const int64_t le = (ex - g.ex0) + (int64_t)(ey - g.ey0) * g.nex + (int64_t)(ez - g.ez0) * g.nex * g.ney;
         const int a = q1_local(ox, oy, oz), bn = q1_local(px, py, pz);
-        if constexpr (TABLE) {  // element matrices formed by k_element_ke
-          const double* src = Ke + (int64_t)((a * 8 + bn) * 9) * g.nelem + le;
+        if constexpr (TABLE) {  // element matrices formed by k_element_ke (plain ones: kref)
+          const bool ref = plain && plain[le];
+          const double* src = ref ? kref + (a * 8 + bn) * 9 : Ke + (int64_t)((a * 8 + bn) * 9) * g.nelem + le;
+          const int64_t st = ref ? 1 : g.nelem;
 #pragma unroll
-          for (int q = 0; q < 9; q++) val[q] += src[(int64_t)q * g.nelem];
+          for (int q = 0; q < 9; q++) val[q] += src[q * st];
         } else {  // the elastic law's one element matrix (k_elastic_ke: ke_block of every (a, bn))
           const double* src = Ke + (a * 8 + bn) * 9;
 #pragma unroll
@@ -2056,6 +2062,8 @@ __global__ __launch_bounds__(TPB) void k_vib_remap(Geo g, const unsigned short* 
 // such "plain" elements assemble into the same few blocks as the elastic law's matrix.  Only the
 // nodes touching a non-plain element (the exceptions) keep their 27 blocks as plain values.
 // cref: the plastic law's elastic-branch tangent; other laws: GP 0 of the context's first element.
+// cref[36], then cref8[36][8] = the same tangent at the 8 Gauss points of a one-element box (the
+// ctan layout k_ref_ke reads)
 __global__ void k_cref(Material mat, const double* __restrict__ ctan, int64_t ngp, double* __restrict__ cref) {
   if (threadIdx.x) return;
   if (mat.law == MCX_LAW_PLASTIC) {
@@ -2067,6 +2075,19 @@ __global__ void k_cref(Material mat, const double* __restrict__ ctan, int64_t ng
   } else {
     for (int q = 0; q < 36; q++) cref[q] = ctan[q * ngp];
   }
+  for (int q = 0; q < 36 * 8; q++) cref[36 + q] = cref[q / 8];
+}
+
+// kref [8 a][8 b][9]: the element matrix of an element whose 8 tangents are cref — ke_body on a
+// one-element box (E = 1: ctan index (kl, gp), Ke index (a*8 + b)*9 + q), the arithmetic
+// k_element_ke performs for every such element, so kref equals their matrices bit for bit
+__global__ void k_ref_ke(Geo g, const double* __restrict__ cref8, double* __restrict__ kref) {
+  const int t = threadIdx.x;
+  if (t >= 16) return;
+  Geo g1 = g;
+  g1.nelem = 1;
+  if (t & 1) ke_body<1>(g1, 0, t >> 1, cref8, kref);
+  else ke_body<0>(g1, 0, t >> 1, cref8, kref);
 }
 
 // plain[le] = the 8 Gauss points' tangents (ctan [36][8][nelem]) all equal cref bit for bit
@@ -2112,9 +2133,11 @@ __global__ __launch_bounds__(TPB) void k_node_exc(Geo g, const unsigned char* __
   xslot[n] = v;
 }
 
-// the exception nodes' 27 blocks, [slot][nb][9]: thread = (slot, nb)
-template <bool TABLE>
+// the exception nodes' 27 blocks, [slot][nb][9]: thread = (slot, nb); each element block from
+// kref (plain elements) or from Ke (the others: k_element_ke forms only those)
 __global__ __launch_bounds__(TPB) void k_exc_fill(Geo g, Material mat, const double* __restrict__ Ke,
+                                                  const double* __restrict__ kref,
+                                                  const unsigned char* __restrict__ plain,
                                                   const int* __restrict__ xlist, int64_t nexc,
                                                   double* __restrict__ exc) {
   const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
@@ -2124,7 +2147,8 @@ __global__ __launch_bounds__(TPB) void k_exc_fill(Geo g, Material mat, const dou
   int i, j, k;
   node_ijk(g, n, i, j, k);
   double val[9];
-  matrix_block<TABLE>(g, mat, Ke, g.xs + i, g.ys + j, g.zs + k, nb % 3 - 1, (nb / 3) % 3 - 1, nb / 9 - 1, val);
+  matrix_block<true>(g, mat, Ke, g.xs + i, g.ys + j, g.zs + k, nb % 3 - 1, (nb / 3) % 3 - 1, nb / 9 - 1, val,
+                     kref, plain);
 #pragma unroll
   for (int q = 0; q < 9; q++) exc[(t * 27 + nb) * 9 + q] = val[q];
 }
@@ -3523,7 +3547,31 @@ void launch_elastic_ke(Ctx& c) { hipLaunchKernelGGL(k_elastic_ke, dim3(1), dim3(
 void launch_element_ke(Ctx& c) {
   const int64_t ngroups = nblk(c.g.nelem);
   const int64_t blocks = pad8(ngroups) * 16;
-  hipLaunchKernelGGL(k_element_ke, dim3((unsigned)blocks), dim3(TPB), 0, c.stream, c.g, c.ctan, c.Ke, ngroups);
+  hipLaunchKernelGGL(k_element_ke, dim3((unsigned)blocks), dim3(TPB), 0, c.stream, c.g, c.ctan, c.Ke, ngroups,
+                     (const unsigned char*)nullptr);
+}
+
+// a per-GP-tangent law headed for the value-indexed storage with exception nodes: the plain
+// elements (every tangent = the reference tangent), the reference element matrix kref, and the
+// element matrices of the other elements only
+int launch_plain_ke(Ctx& c) {
+  if (!c.elem_plain) {
+    MCX_HIP(hipMalloc(&c.elem_plain, c.g.nelem));
+    MCX_HIP(hipMalloc(&c.cref, (36 + 36 * 8 + 576) * sizeof(double)));  // cref, cref8, kref
+    MCX_HIP(hipMalloc(&c.vi_xslot, c.g.nown * sizeof(unsigned)));
+    MCX_HIP(hipMalloc(&c.vi_xlist, c.g.nown * sizeof(int)));
+    c.device_bytes += c.g.nelem + (36 + 288 + 576) * 8 + c.g.nown * 8;
+  }
+  double* kref = c.cref + 36 + 288;
+  hipLaunchKernelGGL(k_cref, dim3(1), dim3(64), 0, c.stream, c.mat, c.ctan, (int64_t)8 * c.g.nelem, c.cref);
+  hipLaunchKernelGGL(k_ref_ke, dim3(1), dim3(64), 0, c.stream, c.g, c.cref + 36, kref);
+  hipLaunchKernelGGL(k_elem_plain, dim3(nblk(c.g.nelem)), dim3(TPB), 0, c.stream, c.g, c.ctan, c.cref, c.elem_plain);
+  const int64_t ngroups = nblk(c.g.nelem);
+  const int64_t blocks = pad8(ngroups) * 16;
+  hipLaunchKernelGGL(k_element_ke, dim3((unsigned)blocks), dim3(TPB), 0, c.stream, c.g, c.ctan, c.Ke, ngroups,
+                     (const unsigned char*)c.elem_plain);
+  c.plain_ke = true;
+  return 0;
 }
 
 void launch_gather_matrix(Ctx& c) {
@@ -3658,24 +3706,20 @@ static int build_vib(Ctx& c, bool* ok) {
   MCX_HIP(hipMemsetAsync(c.vib_ctl, 0, 4 * sizeof(unsigned), c.stream));
   const dim3 grid(nblk(c.g.nown), 27);
   // a per-GP-tangent law: the nodes touching a non-plain element become exceptions
-  const bool exc = table_law(c) && c.vi_exc_max > 0;
+  // a per-GP-tangent law (launch_plain_ke ran): the nodes touching a non-plain element become
+  // exceptions; every other node's blocks are sums of kref blocks
+  const bool exc = table_law(c) && c.plain_ke;
   c.vi_nexc = 0;
   if (exc) {
-    if (!c.elem_plain) {  // first exception build: flags, reference tangent, slots
-      MCX_HIP(hipMalloc(&c.elem_plain, c.g.nelem));
-      MCX_HIP(hipMalloc(&c.cref, 36 * sizeof(double)));
-      MCX_HIP(hipMalloc(&c.vi_xslot, c.g.nown * sizeof(unsigned)));
-      MCX_HIP(hipMalloc(&c.vi_xlist, c.g.nown * sizeof(int)));
-      c.device_bytes += c.g.nelem + 36 * 8 + c.g.nown * 8;
-    }
-    hipLaunchKernelGGL(k_cref, dim3(1), dim3(64), 0, c.stream, c.mat, c.ctan, (int64_t)8 * c.g.nelem, c.cref);
-    hipLaunchKernelGGL(k_elem_plain, dim3(nblk(c.g.nelem)), dim3(TPB), 0, c.stream, c.g, c.ctan, c.cref,
-                       c.elem_plain);
     hipLaunchKernelGGL(k_node_exc, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.elem_plain, c.vi_xslot,
                        c.vi_xlist, c.vib_ctl);
   }
   const unsigned* xslot = exc ? c.vi_xslot : nullptr;
-  if (table_law(c))
+  const double* kref = exc ? c.cref + 36 + 288 : nullptr;
+  if (exc)
+    hipLaunchKernelGGL(k_vib_build<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, kref, gsv, gbk, c.vib_pos,
+                       c.vib_ctl, xslot);
+  else if (table_law(c))
     hipLaunchKernelGGL(k_vib_build<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), gsv, gbk, c.vib_pos,
                        c.vib_ctl, xslot);
   else
@@ -3753,8 +3797,8 @@ static int build_vib(Ctx& c, bool* ok) {
                      reinterpret_cast<u32x4*>(c.vi_idx), xslot);
   if (nexc) {
     const dim3 eg((unsigned)((nexc + TPB - 1) / TPB), 27);
-    hipLaunchKernelGGL(k_exc_fill<true>, eg, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.vi_xlist, nexc,
-                       c.vi_exc);
+    hipLaunchKernelGGL(k_exc_fill, eg, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), kref, c.elem_plain,
+                       c.vi_xlist, nexc, c.vi_exc);
   }
   c.vi_nexc = nexc;
   c.vi_n = nvals;
@@ -3769,7 +3813,7 @@ int build_vi(Ctx& c, bool* ok) {
   *ok = false;
   if (c.vi_block_on && c.vi_bits_max == 4 && c.vib_onepass) {
     if (int rc = build_vib(c, ok)) return rc;
-    if (*ok) return 0;
+    if (*ok || c.plain_ke) return 0;  // (plain_ke: Ke holds the non-plain elements only)
   }
   const bool table = table_law(c);
   MCX_HIP(hipMemsetAsync(c.vi_keys, 0xff, (VI_HASH + NSLOT * 32) * sizeof(unsigned long long), c.stream));

@@ -191,6 +191,7 @@ struct Ctx {
   double* vi_exc = nullptr;             // [exceptions][27][9] block values
   int64_t vi_exc_bytes = 0;             // allocated bytes of vi_exc
   int64_t vi_nexc = 0;                  // exception nodes of the current matrix
+  bool plain_ke = false;                // this assembly formed kref + the non-plain elements' Ke only
   int vi_exc_max = 250;                 // option vi_exc_max: per-mille of owned nodes beyond which the
                                         // assembly falls back to AIJ-split (0: no exceptions)
   double* ke_uni = nullptr;  // elastic law: the element matrix [8 a][8 b][9], the same for every element
@@ -297,6 +298,7 @@ void launch_strains(Ctx& c);
 void launch_homogenize(Ctx& c);
 void launch_residual(Ctx& c);          // b + partial sums of b.b
 void launch_element_ke(Ctx& c);        // Ke of a per-GP-tangent law
+int launch_plain_ke(Ctx& c);           // plain elements, kref, the other elements' Ke (exception-node build)
 void launch_elastic_ke(Ctx& c);        // the elastic law's one element matrix (ke_uni)
 void launch_gather_matrix(Ctx& c);
 void launch_gather_matrix_sym(Ctx& c);
