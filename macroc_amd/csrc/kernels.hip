@@ -2247,6 +2247,36 @@ __global__ __launch_bounds__(TPB) void k_spmv_vib(Geo g, const u32x4* __restrict
   }
 }
 
+__device__ void cg_logic_alpha(CgState* s, double dpi);
+__device__ void cg_logic_beta(CgState* s, double zz, double zr, double* hist);
+__device__ __forceinline__ void reduce_parts(const double* part, int nparts, int nvals, double* sh, double res[2]);
+
+// FOLD (option cg_fold, one rank): the CG's scalar steps folded into the kernels whose partials
+// they sum: alpha into the value-indexed SpMV, beta into the update kernel.  Every block
+// publishes its partials and counts itself done; the last block to finish sums them with
+// k_reduce's tree and runs the step's logic, so the launch of k_reduce (and its gap) goes away
+// and the scalars are bitwise k_reduce's.
+struct CgFold {
+  unsigned* cnt = nullptr;  // blocks done (zero between launches: the last block resets it)
+  double* red = nullptr;    // the sums (k_reduce's out)
+  double* hist = nullptr;
+  CgState* cg = nullptr;
+};
+
+// the last block of the grid (all 1024 threads return the same answer): after every block's
+// partials are visible to it
+__device__ __forceinline__ bool fold_last(unsigned* cnt) {
+  __shared__ int s_last;
+  if (threadIdx.x == 0) {
+    __threadfence();  // this block's partials before its count
+    s_last = atomicAdd(cnt, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!s_last) return false;
+  __threadfence();  // the other blocks' partials after their counts
+  return true;
+}
+
 // y = A x on block-indexed FMT_VI with x staged in LDS, z-marching: k_spmv_vim's ring of three x
 // planes (rows j0-1 .. j0+TY, prefetched in registers one plane ahead) with the block dictionary
 // in LDS beside it.  The gathered kernel (k_spmv_vib) spends most of its time in the 81 8-B x
@@ -2284,8 +2314,8 @@ template <bool DOT, bool GATED, int TX, int TY, bool XV = true, bool UNI = false
 __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __restrict__ I,
                                                        const double* __restrict__ bdict, const double* __restrict__ x,
                                                        double* __restrict__ y, double* __restrict__ part,
-                                                       const CgState* __restrict__ cg, ZTiling zt, FusedP fp = {},
-                                                       const double* __restrict__ exc = nullptr) {
+                                                       const CgState* cg, ZTiling zt, FusedP fp = {},
+                                                       const double* __restrict__ exc = nullptr, CgFold fo = {}) {
   static_assert(!PATCH || (TX % 16 == 0 && TY % 4 == 0 && TX * TY == 1024), "16 x 4 patches");
   constexpr int T = TX * TY, RL = vibm_rl<TX, PATCH>(), PR = TY + 2, PLANE = PR * RL;  // doubles per staged plane
   constexpr int NL = (PLANE + T - 1) / T;                                      // x loads per thread per plane
@@ -2304,8 +2334,22 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
   const int ty0 = xcd * slab;
   const int nty_here = min(slab, zt.nty - ty0);
   const int per = max(nty_here, 0) * zt.ntx * zt.nzc;
+  // alpha step folded in (cg_fold): the last block to finish sums the partials (k_reduce's tree)
+  auto alpha_fold = [&]() {
+    if constexpr (DOT && GATED && T == 1024) {
+      if (!fo.cnt || !fold_last(fo.cnt)) return;
+      double res[2] = {0., 0.};
+      reduce_parts(part, gridDim.x, 1, sh, res);
+      if (threadIdx.x == 0) {
+        *fo.cnt = 0u;
+        fo.red[0] = res[0];
+        cg_logic_alpha(fo.cg, res[0]);
+      }
+    }
+  };
   if (t8 >= per) {  // whole block idle (uniform): still write the partial
     if (DOT && threadIdx.x == 0) part[blockIdx.x] = 0.;
+    alpha_fold();
     return;
   }
   const int txi = t8 % zt.ntx, r8 = t8 / zt.ntx;  // x tiles fastest, then the slab's tile rows, then z-chunks
@@ -2603,6 +2647,7 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
     double s = block_sum<T>(dot, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = s;
   }
+  alpha_fold();
 }
 
 // y = A x on FMT_VI with x staged in LDS, z-marching.  k_spmv_vi's 81 x gathers per node (8 B
@@ -2957,20 +3002,62 @@ __device__ __forceinline__ void pupdate_node_db(const Geo& g, int n, const doubl
   for (int d = 0; d < 3; d++) st<NT>(&pn[3 * pc + d], zv[d] + bc * pv[d]);
 }
 
-template <bool NT, bool DIX, bool SKIP_SENT = false>
+// PAR (option cg_par): the iteration's parity as the host counts it, so one kernel holds one
+// straight path with every load issued before the first use: 1 = an even iteration >= 2 (73 B
+// per node), 2 = an odd one >= 3 (145 B); 0 = the parity read from cg->i (also the fallback
+// should the device's count ever differ from the host's)
+template <bool NT, bool DIX, int PAR>
+__device__ __forceinline__ void pupdate_node_par(const Geo& g, int n, const double* __restrict__ z,
+                                                 const double* __restrict__ dinv,
+                                                 const unsigned char* __restrict__ jix, double* __restrict__ pb0,
+                                                 double* __restrict__ pb1, double* __restrict__ x,
+                                                 const CgState* __restrict__ cg) {
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  const int pc = pad_of(g, i, j, k);
+  double* pn = PAR == 2 ? pb1 : pb0;
+  const double* po = PAR == 2 ? pb0 : pb1;
+  const double bc = cg->bcoef, a = cg->alpha;
+  double pv[3], zv[3], xv[3], pp[3];
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    pv[d] = po[3 * pc + d];
+    if (PAR == 2) {
+      xv[d] = x[3 * n + d];
+      pp[d] = pn[3 * pc + d];
+    }
+    zv[d] = z_of<DIX>(z, dinv, jix, n, d);
+  }
+  if (PAR == 2) {
+    const double ap = cg->alpha_prev;
+#pragma unroll
+    for (int d = 0; d < 3; d++) st<NT>(&x[3 * n + d], (xv[d] + ap * pp[d]) + a * pv[d]);
+  }
+#pragma unroll
+  for (int d = 0; d < 3; d++) st<NT>(&pn[3 * pc + d], zv[d] + bc * pv[d]);
+}
+
+template <bool NT, bool DIX, bool SKIP_SENT = false, int PAR = 0>
 __global__ void k_cg_pupdate_db(Geo g, const double* __restrict__ z, const double* __restrict__ dinv,
                                 const unsigned char* __restrict__ jix, double* __restrict__ pb0,
                                 double* __restrict__ pb1, double* __restrict__ x, const CgState* __restrict__ cg,
                                 int* __restrict__ xdone, const int* __restrict__ list, int64_t cnt) {
   if (cg->reason) return;
   const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
-  if (t == 0 && (cg->i & 1)) *xdone = cg->i;
+  const int it = cg->i;
+  if (t == 0 && (it & 1)) *xdone = it;
   if (t >= cnt) return;
   const int n = list ? list[t] : (int)t;
   if (SKIP_SENT) {
     int i, j, k;
     node_ijk(g, n, i, j, k);
     if (sent_node(g, i, j, k)) return;
+  }
+  if constexpr (PAR != 0) {
+    if (it >= 2 && (it & 1) == (PAR == 2 ? 1 : 0)) {
+      pupdate_node_par<NT, DIX, PAR>(g, n, z, dinv, jix, pb0, pb1, x, cg);
+      return;
+    }
   }
   pupdate_node_db<NT, DIX>(g, n, z, dinv, jix, pb0, pb1, x, cg);
 }
@@ -3046,13 +3133,13 @@ __global__ void k_cg_xfinal(Geo g, const double* __restrict__ ppad, const double
 // 1024-thread blocks: a quarter of the partials for k_reduce (one block reads them all)
 static constexpr int UTPB = 1024;
 
-template <bool NT, bool DIX>
+template <bool NT, bool DIX, bool FOLD = false>
 __global__ __launch_bounds__(UTPB) void k_cg_update(Geo g, const double* __restrict__ w,
                                                    const double* __restrict__ dinv,
                                                    const unsigned char* __restrict__ jix,
                                                    double* __restrict__ r, double* __restrict__ z,
-                                                   double* __restrict__ part, int nparts,
-                                                   const CgState* __restrict__ cg) {
+                                                   double* part, int nparts,
+                                                   const CgState* cg, CgFold fo = {}) {
   __shared__ double sh[UTPB / 64];
   if (cg->reason) return;
   const double ma = -cg->alpha;
@@ -3075,6 +3162,18 @@ __global__ __launch_bounds__(UTPB) void k_cg_update(Geo g, const double* __restr
   if (threadIdx.x == 0) {
     part[blockIdx.x] = s0;
     part[nparts + blockIdx.x] = s1;
+  }
+  if constexpr (FOLD) {
+    static_assert(UTPB == 1024, "k_reduce's tree: 1024 threads");
+    if (!fold_last(fo.cnt)) return;
+    double res[2] = {0., 0.};
+    reduce_parts(part, nparts, 2, sh, res);
+    if (threadIdx.x == 0) {
+      *fo.cnt = 0u;
+      fo.red[0] = res[0];
+      fo.red[1] = res[1];
+      cg_logic_beta(fo.cg, res[0], res[1], fo.hist);
+    }
   }
 }
 
@@ -3306,16 +3405,9 @@ __device__ void cg_logic_beta(CgState* s, double zz, double zr, double* hist) {
 
 enum { RED_STORE = 0, RED_INIT = 1, RED_ALPHA = 2, RED_BETA = 3, RED_NORM = 4 };
 
-// one block: out[v] = sum_i part[v*nparts + i] (fixed order); then optional CG logic.
-// mode RED_STORE writes the local sums only (an all-reduce + k_cg_logic follows).
-// cg_src: the state the step starts from (copied to cg first when it is the other buffer)
-__global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ part, int nparts, int nvals,
-                                                 double* __restrict__ out, int mode, CgState* cg,
-                                                 double* __restrict__ hist, int gated, const CgState* cg_src) {
-  __shared__ double sh[16];
-  if (cg_src != cg && threadIdx.x == 0) *cg = *cg_src;  // read by thread 0 only below
-  if (gated && cg_src->reason) return;
-  double res[2] = {0., 0.};
+// res[v] = sum_i part[v*nparts + i], v < nvals <= 2, by one 1024-thread block (thread 0's
+// result): the fixed summation tree of k_reduce and of the update kernel's fold (cg_fold)
+__device__ __forceinline__ void reduce_parts(const double* part, int nparts, int nvals, double* sh, double res[2]) {
   for (int v = 0; v < nvals; v++) {
     // 8 independent accumulators per thread keep 8 loads in flight; fixed combination order
     const double* pv = part + (int64_t)v * nparts;
@@ -3329,6 +3421,19 @@ __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ part
     const double acc = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
     res[v] = block_sum<1024>(acc, sh);
   }
+}
+
+// one block: out[v] = sum_i part[v*nparts + i] (fixed order); then optional CG logic.
+// mode RED_STORE writes the local sums only (an all-reduce + k_cg_logic follows).
+// cg_src: the state the step starts from (copied to cg first when it is the other buffer)
+__global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ part, int nparts, int nvals,
+                                                 double* __restrict__ out, int mode, CgState* cg,
+                                                 double* __restrict__ hist, int gated, const CgState* cg_src) {
+  __shared__ double sh[16];
+  if (cg_src != cg && threadIdx.x == 0) *cg = *cg_src;  // read by thread 0 only below
+  if (gated && cg_src->reason) return;
+  double res[2] = {0., 0.};
+  reduce_parts(part, nparts, nvals, sh, res);
   if (threadIdx.x) return;
   for (int v = 0; v < nvals; v++) out[v] = res[v];
   if (mode == RED_INIT) cg_logic_init(cg, res[0], res[1], hist);
@@ -4032,11 +4137,21 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
       zt.wmap = c.vi_wmap;
       int tx, ty;
       vis_shape(c, tx, ty);
+      // the CG's alpha step folded into this launch (cg_iteration asks with c.fold_alpha; the
+      // partials are the grid's blocks, as k_reduce would read them)
+      CgFold fo;
+      if (c.fold_alpha && dot && gated && c.fold_cnt && nb == (int)spmv_nparts(c)) {
+        fo.cnt = c.fold_cnt;
+        fo.red = c.red;
+        fo.hist = c.hist;
+        fo.cg = c.cg;
+        c.fold_done = true;
+      }
 #define MCX_VIBM(TXV, TYV, XVV, UV, PV, ...)                                                                          \
   do {                                                                                                             \
     if (dot && gated)                                                                                              \
       hipLaunchKernelGGL((k_spmv_vibm<true, true, TXV, TYV, XVV, UV, PV, ##__VA_ARGS__>), dim3(nb), dim3(1024), 0,        \
-                         c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt);                             \
+                         c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt, FusedP{}, nullptr, fo);      \
     else if (dot)                                                                                                  \
       hipLaunchKernelGGL((k_spmv_vibm<true, false, TXV, TYV, XVV, UV, PV, ##__VA_ARGS__>), dim3(nb), dim3(1024), 0,       \
                          c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt);                             \
@@ -4050,7 +4165,7 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
     if (dot && gated)                                                                                              \
       hipLaunchKernelGGL((k_spmv_vibm<true, true, TXV, TYV, true, true, true, FV, false, false, true>), dim3(nb),       \
                          dim3(1024), 0, c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt, FusedP{},      \
-                         c.vi_exc);                                                                                \
+                         c.vi_exc, fo);                                                                            \
     else if (dot)                                                                                                  \
       hipLaunchKernelGGL((k_spmv_vibm<true, false, TXV, TYV, true, true, true, FV, false, false, true>), dim3(nb),      \
                          dim3(1024), 0, c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt, FusedP{},      \
@@ -4306,21 +4421,29 @@ void launch_cg_pupdate(Ctx& c, int part) {
   const double* zs = dix ? c.r : c.z;
   const double* jd = dix ? c.jdd : c.dinv;
   if (c.pdb_used) {  // p double-buffered, x every second iteration
+    // cg_par: the kernel of the iteration's parity (the host's count; the kernel checks it)
+    const int par = c.cg_par && c.cg_it >= 2 ? 1 + (c.cg_it & 1) : 0;
+#define MCX_PDB_PAR(SKIPV, GRID, LIST, CNT)                                                                          \
+  MCX_NT_DIX(c.cg_nt, dix, {                                                                                         \
+    if (par == 1)                                                                                                    \
+      hipLaunchKernelGGL((k_cg_pupdate_db<NT, DX, SKIPV, 1>), dim3(GRID), dim3(TPB), 0, c.stream, c.g, zs, jd, c.jix, \
+                         c.p_pad, c.p_pad2, c.du, c.cg, c.xdone, LIST, CNT);                                         \
+    else if (par == 2)                                                                                               \
+      hipLaunchKernelGGL((k_cg_pupdate_db<NT, DX, SKIPV, 2>), dim3(GRID), dim3(TPB), 0, c.stream, c.g, zs, jd, c.jix, \
+                         c.p_pad, c.p_pad2, c.du, c.cg, c.xdone, LIST, CNT);                                         \
+    else                                                                                                             \
+      hipLaunchKernelGGL((k_cg_pupdate_db<NT, DX, SKIPV, 0>), dim3(GRID), dim3(TPB), 0, c.stream, c.g, zs, jd, c.jix, \
+                         c.p_pad, c.p_pad2, c.du, c.cg, c.xdone, LIST, CNT);                                         \
+  })
     if (part == 1) {
       if (!c.halo.nbnd) return;
-      MCX_NT_DIX(c.cg_nt, dix,
-                 hipLaunchKernelGGL((k_cg_pupdate_db<NT, DX>), dim3(nblk(c.halo.nbnd)), dim3(TPB), 0, c.stream, c.g,
-                                    zs, jd, c.jix, c.p_pad, c.p_pad2, c.du, c.cg, c.xdone, c.halo.d_bnd,
-                                    c.halo.nbnd));
+      MCX_PDB_PAR(false, nblk(c.halo.nbnd), c.halo.d_bnd, c.halo.nbnd);
     } else if (part == 2) {
-      MCX_NT_DIX(c.cg_nt, dix,
-                 hipLaunchKernelGGL((k_cg_pupdate_db<NT, DX, true>), dim3(nbn), dim3(TPB), 0, c.stream, c.g, zs, jd,
-                                    c.jix, c.p_pad, c.p_pad2, c.du, c.cg, c.xdone, nullptr, (int64_t)c.g.nown));
+      MCX_PDB_PAR(true, nbn, nullptr, (int64_t)c.g.nown);
     } else {
-      MCX_NT_DIX(c.cg_nt, dix,
-                 hipLaunchKernelGGL((k_cg_pupdate_db<NT, DX>), dim3(nbn), dim3(TPB), 0, c.stream, c.g, zs, jd,
-                                    c.jix, c.p_pad, c.p_pad2, c.du, c.cg, c.xdone, nullptr, (int64_t)c.g.nown));
+      MCX_PDB_PAR(false, nbn, nullptr, (int64_t)c.g.nown);
     }
+#undef MCX_PDB_PAR
     return;
   }
   if (part == 1) {
@@ -4398,7 +4521,11 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) 
   }
   if (!(c.nranks > 1 && c.overlap && c.halo.nbnd) && (rc = halo_exchange(c, pcur))) return rc;
   if (ev0) MCX_HIP(hipEventRecord(ev0, c.stream));
+  const bool fold = c.cg_fold && c.fold_cnt && c.nranks == 1 && !c.comm;
+  c.fold_alpha = fold && !fa;
+  c.fold_done = false;
   launch_spmv(c, pcur, c.w, true, true);
+  c.fold_alpha = false;
   if (ev1) MCX_HIP(hipEventRecord(ev1, c.stream));
   if (fa) {
     MCX_NT_DIX(c.cg_nt, dix,
@@ -4407,8 +4534,18 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) 
     if (!fb || last) return reduce_and_logic(c, 2, nbu, RED_BETA, true, c.partials2, A);
     return 0;
   }
-  rc = reduce_and_logic(c, 1, nbs, RED_ALPHA, true, c.partials, c.cg);
-  if (rc) return rc;
+  if (!c.fold_done && (rc = reduce_and_logic(c, 1, nbs, RED_ALPHA, true, c.partials, c.cg))) return rc;
+  if (fold) {  // the beta step in the update's last block
+    CgFold fo;
+    fo.cnt = c.fold_cnt;
+    fo.red = c.red;
+    fo.hist = c.hist;
+    fo.cg = c.cg;
+    MCX_NT_DIX(c.cg_nt, dix,
+               hipLaunchKernelGGL((k_cg_update<NT, DX, true>), dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, jd,
+                                  c.jix, c.r, c.z, c.partials2, nbu, c.cg, fo));
+    return 0;
+  }
   MCX_NT_DIX(c.cg_nt, dix,
              hipLaunchKernelGGL((k_cg_update<NT, DX>), dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, jd, c.jix, c.r,
                                 c.z, c.partials2, nbu, c.cg));

@@ -138,6 +138,11 @@ struct Ctx {
   bool fusep_used = false;   // the last solve ran the fused kernel (timing: its bytes per launch)
   int cg_pdb = 1;            // option cg_pdb: p double-buffered (p_pad / p_pad2), VecAXPY(x) every second iteration
   bool pdb_used = false;     // the current solve runs the double-buffered p update
+  int cg_par = 0;            // option cg_par: PDB p update specialised per iteration parity (host count cg_it)
+  int cg_fold = 0;           // option cg_fold: alpha / beta steps in the SpMV / update kernel's last block (one rank)
+  unsigned* fold_cnt = nullptr;  // its count of finished blocks
+  bool fold_alpha = false;   // cg_iteration -> launch_spmv: fold the alpha step into the SpMV if it can
+  bool fold_done = false;    // launch_spmv -> cg_iteration: it did
   int* xdone = nullptr;      // PDB: the last odd iteration whose p update applied the x terms owed
   int cg_it = 0;             // iteration index of the cg_iteration being launched
   double* b = nullptr;       // residual (owned, PETSc-local order)

@@ -242,10 +242,12 @@ def test_cg_pdb_multirank_bitwise(grid, procs):
     argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
             "-da_processors_z", pz, "-ksp_rtol", "1e-10"]
     x = np.zeros(3 * NX * NY * NZ)
-    on = run_group(argv, px * py * pz, newton_step(x, [("cg_pdb", 1)]))
+    on = run_group(argv, px * py * pz, newton_step(x, [("cg_pdb", 1), ("cg_par", 0)]))
+    par = run_group(argv, px * py * pz, newton_step(x, [("cg_pdb", 1), ("cg_par", 1), ("cg_fold", 1)]))
     off = run_group(argv, px * py * pz, newton_step(x, [("cg_pdb", 0)]))
-    for a, b in zip(on, off):
+    for a, b, c in zip(on, off, par):
         assert a["its"] == b["its"] and a["reason"] == b["reason"] and np.array_equal(a["du"], b["du"])
+        assert c["its"] == b["its"] and c["reason"] == b["reason"] and np.array_equal(c["du"], b["du"])
 
 
 def test_rccl_transport_one_rank():
