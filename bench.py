@@ -324,7 +324,7 @@ def main():
     ap.add_argument("--rtol", type=float, default=1e-8)
     ap.add_argument("--cpu-sample", type=int, default=128, help="oracle sample grid (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0 = every usable host core)")
-    ap.add_argument("--cpu-cg-its", type=int, default=60, help="CG iterations of the oracle sample")
+    ap.add_argument("--cpu-cg-its", type=int, default=240, help="CG iterations of the oracle sample")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--mat-type", default="aij", choices=list(STORAGE_ARGS), help="matrix storage of the headline")
     ap.add_argument("--variants", default=None,

@@ -55,7 +55,7 @@ static int free_ctx(Ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
   void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
-                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2, c->xdone, c->fold_cnt, c->elem_plain, c->cref, c->vi_xslot,
+                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2, c->xdone, c->elem_plain, c->cref, c->vi_xslot,
                   c->vi_xlist, c->vi_exc,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf, c->halo.d_bnd};
@@ -158,8 +158,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
       (rc = dalloc(c, &c.partials, c.partials_cap = 4 * std::max(max_spmv_blocks(c), node_blocks(c)) + 64)) ||
       (rc = dalloc(c, &c.red, 16)) || (rc = dalloc(c, &c.red_loc, 16)) || (rc = dalloc(c, &c.cg, 2)) ||
       (rc = dalloc(c, &c.hist, (int64_t)o->ksp_max_it + 2)) || (rc = dalloc(c, &c.ke_uni, 576)) ||
-      (rc = dalloc(c, &c.p_pad2, npad)) || (rc = dalloc(c, &c.xdone, 1)) ||  // p's second buffer (cg_pdb, cg_fusep)
-      (rc = dalloc(c, &c.fold_cnt, 1)))
+      (rc = dalloc(c, &c.p_pad2, npad)) || (rc = dalloc(c, &c.xdone, 1)))  // p's second buffer (cg_pdb, cg_fusep)
     return rc;
   c.dinv = c.jdd + 3 * VI_MAX;
   // per-GP tangent: only laws that hand one over (the isotropic elastic C is a kernel argument)
@@ -1434,8 +1433,12 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.cg_par = (int)value;
     return 0;
   }
-  if (!std::strcmp(name, "cg_fold")) {
-    c.cg_fold = (int)value;
+  if (!std::strcmp(name, "vi_exc_list")) {
+    if (value < 0. || value > VI_EXC_LIST) {
+      set_error("vi_exc_list: 0 .. 2048");
+      return 1;
+    }
+    c.vi_exc_list = (int)value;
     return 0;
   }
   if (!std::strcmp(name, "vi_wmap")) {

@@ -962,6 +962,7 @@ struct ZTiling {
   int ntx, nty, nzc, kc;  // tiles in x, y; z chunks and planes per chunk
   int dbg = 0;            // timing-only diagnostics (k_spmv_vibm: 1 = every wave takes the scalar path)
   int wmap = 1;           // k_spmv_vibm PATCH: 1 = patches on SIMDs as a Latin square, 0 = row-major (A/B)
+  int xlist = VI_EXC_LIST;  // k_spmv_vibm EXC: exception nodes a tile defers (option vi_exc_list; the rest in their plane)
 };
 
 static ZTiling z_tiling(const Geo& g, int ztx, int zty, int want) {
@@ -2247,36 +2248,6 @@ __global__ __launch_bounds__(TPB) void k_spmv_vib(Geo g, const u32x4* __restrict
   }
 }
 
-__device__ void cg_logic_alpha(CgState* s, double dpi);
-__device__ void cg_logic_beta(CgState* s, double zz, double zr, double* hist);
-__device__ __forceinline__ void reduce_parts(const double* part, int nparts, int nvals, double* sh, double res[2]);
-
-// FOLD (option cg_fold, one rank): the CG's scalar steps folded into the kernels whose partials
-// they sum: alpha into the value-indexed SpMV, beta into the update kernel.  Every block
-// publishes its partials and counts itself done; the last block to finish sums them with
-// k_reduce's tree and runs the step's logic, so the launch of k_reduce (and its gap) goes away
-// and the scalars are bitwise k_reduce's.
-struct CgFold {
-  unsigned* cnt = nullptr;  // blocks done (zero between launches: the last block resets it)
-  double* red = nullptr;    // the sums (k_reduce's out)
-  double* hist = nullptr;
-  CgState* cg = nullptr;
-};
-
-// the last block of the grid (all 1024 threads return the same answer): after every block's
-// partials are visible to it
-__device__ __forceinline__ bool fold_last(unsigned* cnt) {
-  __shared__ int s_last;
-  if (threadIdx.x == 0) {
-    __threadfence();  // this block's partials before its count
-    s_last = atomicAdd(cnt, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!s_last) return false;
-  __threadfence();  // the other blocks' partials after their counts
-  return true;
-}
-
 // y = A x on block-indexed FMT_VI with x staged in LDS, z-marching: k_spmv_vim's ring of three x
 // planes (rows j0-1 .. j0+TY, prefetched in registers one plane ahead) with the block dictionary
 // in LDS beside it.  The gathered kernel (k_spmv_vib) spends most of its time in the 81 8-B x
@@ -2314,8 +2285,8 @@ template <bool DOT, bool GATED, int TX, int TY, bool XV = true, bool UNI = false
 __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __restrict__ I,
                                                        const double* __restrict__ bdict, const double* __restrict__ x,
                                                        double* __restrict__ y, double* __restrict__ part,
-                                                       const CgState* cg, ZTiling zt, FusedP fp = {},
-                                                       const double* __restrict__ exc = nullptr, CgFold fo = {}) {
+                                                       const CgState* __restrict__ cg, ZTiling zt, FusedP fp = {},
+                                                       const double* __restrict__ exc = nullptr) {
   static_assert(!PATCH || (TX % 16 == 0 && TY % 4 == 0 && TX * TY == 1024), "16 x 4 patches");
   constexpr int T = TX * TY, RL = vibm_rl<TX, PATCH>(), PR = TY + 2, PLANE = PR * RL;  // doubles per staged plane
   constexpr int NL = (PLANE + T - 1) / T;                                      // x loads per thread per plane
@@ -2327,6 +2298,12 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
   __shared__ double2 tab[VI_MAX * VIB_STRIDE / 2];
   __shared__ double sh[T / 64];
   __shared__ double s_jdd[FP ? 3 * VI_MAX : 1];
+  // EXC: the tile's exception nodes, computed after the march by the whole block (one node per
+  // thread) instead of inside their plane, where each one's nine dependent rounds of global
+  // loads held the plane's barrier for every wave of the block
+  constexpr int XL = EXC ? VI_EXC_LIST : 1;
+  __shared__ int s_xl[XL];
+  __shared__ int s_nx;
   if (GATED && cg->reason) return;
   const int b = blockIdx.x;
   const int xcd = b & 7, t8 = b >> 3;
@@ -2334,22 +2311,8 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
   const int ty0 = xcd * slab;
   const int nty_here = min(slab, zt.nty - ty0);
   const int per = max(nty_here, 0) * zt.ntx * zt.nzc;
-  // alpha step folded in (cg_fold): the last block to finish sums the partials (k_reduce's tree)
-  auto alpha_fold = [&]() {
-    if constexpr (DOT && GATED && T == 1024) {
-      if (!fo.cnt || !fold_last(fo.cnt)) return;
-      double res[2] = {0., 0.};
-      reduce_parts(part, gridDim.x, 1, sh, res);
-      if (threadIdx.x == 0) {
-        *fo.cnt = 0u;
-        fo.red[0] = res[0];
-        cg_logic_alpha(fo.cg, res[0]);
-      }
-    }
-  };
   if (t8 >= per) {  // whole block idle (uniform): still write the partial
     if (DOT && threadIdx.x == 0) part[blockIdx.x] = 0.;
-    alpha_fold();
     return;
   }
   const int txi = t8 % zt.ntx, r8 = t8 / zt.ntx;  // x tiles fastest, then the slab's tile rows, then z-chunks
@@ -2371,13 +2334,18 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
   // the plane last; the Latin square (SIMD = (px + py) mod 4 within each group of 4 columns)
   // puts any column's and any row's patches on different SIMDs.
   constexpr int TYP = TY / 4;
-  int px = wv % (TX / 16), py = wv / (TX / 16);
-  if (PATCH && zt.wmap) {
-    py = (wv >> 2) % TYP;
-    px = (wv / (4 * TYP)) * 4 + (((wv & 3) - py) & 3);
-  }
-  const int lx = PATCH ? px * 16 + (ln & 15) : me % TX;
-  const int ly = PATCH ? py * 4 + (ln >> 4) : me / TX;
+  auto lane_xy = [&](int tid, int& lxo, int& lyo) {  // thread -> node of the tile
+    const int wq = tid >> 6, lq = tid & 63;
+    int px = wq % (TX / 16), py = wq / (TX / 16);
+    if (PATCH && zt.wmap) {
+      py = (wq >> 2) % TYP;
+      px = (wq / (4 * TYP)) * 4 + (((wq & 3) - py) & 3);
+    }
+    lxo = PATCH ? px * 16 + (lq & 15) : tid % TX;
+    lyo = PATCH ? py * 4 + (lq >> 4) : tid / TX;
+  };
+  int lx, ly;
+  lane_xy(me, lx, ly);
   const int i = i0 + lx, j = j0 + ly;
   const bool inxy = i < g.nx && j < g.ny;
   const int PX = g.PX, PXY = g.PX * g.PY;
@@ -2440,6 +2408,7 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
     }
     xs[slot][e] = pn;
   };
+  if (EXC && me == 0) s_nx = 0;  // published by the prologue's barrier
   for (int t = me; t < VI_MAX * VIB_STRIDE / 2; t += T) tab[t] = reinterpret_cast<const double2*>(bdict)[t];
   if (FP) {
     for (int t = me; t < 3 * VI_MAX; t += T) s_jdd[t] = fp.jdd[t];
@@ -2458,6 +2427,12 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
 #pragma unroll
       for (int m = 0; m < NL; m++) xstore(s, m, xload(k0 - 1 + s, m));
   }
+  auto exc_defer = [&](int k) -> bool {  // this thread's node of plane k onto the tile's list
+    const int q = atomicAdd(&s_nx, 1);
+    if (q >= min(XL, zt.xlist)) return false;
+    s_xl[q] = (k - k0) * T + me;
+    return true;
+  };
   u32x4 c0 = {0u, 0u, 0u, 0u}, c1 = c0, n0 = c0, n1 = c0;
   iload(k0, c0, c1);
   __syncthreads();
@@ -2546,10 +2521,12 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       __builtin_nontemporal_store(y1, &y[3 * n + 1]);
       __builtin_nontemporal_store(y2, &y[3 * n + 2]);
       if (DOT) dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
+    } else if (EXC && inxy && c1[3] && exc_defer(k)) {
+      // deferred to the block's exception pass below
     } else if (EXC && inxy && c1[3]) {
-      // an exception node (EXC instantiations only): its 27 plain blocks from exc [slot][27][9], a
-      // rolled loop of its own so the indexed path below keeps its registers; same order and
-      // products as the indexed rows
+      // an exception node (EXC instantiations only) that found the tile's list full: its 27
+      // plain blocks from exc [slot][27][9], a rolled loop of its own so the indexed path below
+      // keeps its registers; same order and products as the indexed rows
       // Blocks in groups of 3 (one dy row): the group's 27 values are loaded together, one
       // round trip per group instead of per block.
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
@@ -2643,11 +2620,58 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       __syncthreads();
     }
   }
+  if constexpr (EXC) {
+    // the exception pass: one listed node per thread, x gathered from the padded vector (the
+    // values the ring held), rows in the indexed path's order and products: y bit-identical.
+    // Only the block's dot partial adds these nodes' terms in another order.
+    __syncthreads();
+    const int ne = min(s_nx, min(XL, zt.xlist));
+    for (int t = me; t < ne; t += T) {
+      const int code = s_xl[t];
+      const int kk = k0 + code / T;
+      int ex, ey;
+      lane_xy(code % T, ex, ey);
+      const int ei = i0 + ex, ej = j0 + ey;
+      const int64_t n = ei + g.nx * (ej + (int64_t)g.ny * kk);
+      const unsigned slot = I[(int64_t)(n >> 6) * (2 * 64) + (n & 63) + 64][3];
+      const double* eb = exc + (int64_t)(slot - 1) * 243;
+      double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+#pragma unroll 1
+      for (int nb0 = 0; nb0 < 27; nb0 += 3) {
+        double av[27];
+#pragma unroll
+        for (int q = 0; q < 27; q++) av[q] = eb[nb0 * 9 + q];
+        const int dy = (nb0 / 3) % 3 - 1, dz = nb0 / 9 - 1;
+        const double* xr = x + 3 * ((int64_t)ei + (ej + 1 + dy) * (int64_t)PX + (kk + 1 + dz) * (int64_t)PXY);
+        double xw[9];
+#pragma unroll
+        for (int q = 0; q < 9; q++) xw[q] = xr[q];  // nodes i-1, i, i+1 of the row (padded i = node i + 1)
+#pragma unroll
+        for (int t3 = 0; t3 < 3; t3++) {
+          const double xv[3] = {xw[3 * t3], xw[3 * t3 + 1], xw[3 * t3 + 2]};
+          if (nb0 + t3 == 13) {
+            xc0 = xv[0];
+            xc1 = xv[1];
+            xc2 = xv[2];
+          }
+#pragma unroll
+          for (int q = 0; q < 9; q++) {
+            const int r = q / 3, cc = q % 3;
+            double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
+            yr = FMA ? __builtin_fma(av[t3 * 9 + q], xv[cc], yr) : yr + av[t3 * 9 + q] * xv[cc];
+          }
+        }
+      }
+      __builtin_nontemporal_store(y0, &y[3 * n + 0]);
+      __builtin_nontemporal_store(y1, &y[3 * n + 1]);
+      __builtin_nontemporal_store(y2, &y[3 * n + 2]);
+      if (DOT) dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
+    }
+  }
   if (DOT) {
     double s = block_sum<T>(dot, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = s;
   }
-  alpha_fold();
 }
 
 // y = A x on FMT_VI with x staged in LDS, z-marching.  k_spmv_vi's 81 x gathers per node (8 B
@@ -3133,13 +3157,13 @@ __global__ void k_cg_xfinal(Geo g, const double* __restrict__ ppad, const double
 // 1024-thread blocks: a quarter of the partials for k_reduce (one block reads them all)
 static constexpr int UTPB = 1024;
 
-template <bool NT, bool DIX, bool FOLD = false>
+template <bool NT, bool DIX>
 __global__ __launch_bounds__(UTPB) void k_cg_update(Geo g, const double* __restrict__ w,
                                                    const double* __restrict__ dinv,
                                                    const unsigned char* __restrict__ jix,
                                                    double* __restrict__ r, double* __restrict__ z,
-                                                   double* part, int nparts,
-                                                   const CgState* cg, CgFold fo = {}) {
+                                                   double* __restrict__ part, int nparts,
+                                                   const CgState* __restrict__ cg) {
   __shared__ double sh[UTPB / 64];
   if (cg->reason) return;
   const double ma = -cg->alpha;
@@ -3162,18 +3186,6 @@ __global__ __launch_bounds__(UTPB) void k_cg_update(Geo g, const double* __restr
   if (threadIdx.x == 0) {
     part[blockIdx.x] = s0;
     part[nparts + blockIdx.x] = s1;
-  }
-  if constexpr (FOLD) {
-    static_assert(UTPB == 1024, "k_reduce's tree: 1024 threads");
-    if (!fold_last(fo.cnt)) return;
-    double res[2] = {0., 0.};
-    reduce_parts(part, nparts, 2, sh, res);
-    if (threadIdx.x == 0) {
-      *fo.cnt = 0u;
-      fo.red[0] = res[0];
-      fo.red[1] = res[1];
-      cg_logic_beta(fo.cg, res[0], res[1], fo.hist);
-    }
   }
 }
 
@@ -3406,7 +3418,7 @@ __device__ void cg_logic_beta(CgState* s, double zz, double zr, double* hist) {
 enum { RED_STORE = 0, RED_INIT = 1, RED_ALPHA = 2, RED_BETA = 3, RED_NORM = 4 };
 
 // res[v] = sum_i part[v*nparts + i], v < nvals <= 2, by one 1024-thread block (thread 0's
-// result): the fixed summation tree of k_reduce and of the update kernel's fold (cg_fold)
+// result): k_reduce's fixed summation tree
 __device__ __forceinline__ void reduce_parts(const double* part, int nparts, int nvals, double* sh, double res[2]) {
   for (int v = 0; v < nvals; v++) {
     // 8 independent accumulators per thread keep 8 loads in flight; fixed combination order
@@ -4135,23 +4147,14 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
       ZTiling zt = vis_tiling(c);
       zt.dbg = c.split_dbg;
       zt.wmap = c.vi_wmap;
+      zt.xlist = c.vi_exc_list;
       int tx, ty;
       vis_shape(c, tx, ty);
-      // the CG's alpha step folded into this launch (cg_iteration asks with c.fold_alpha; the
-      // partials are the grid's blocks, as k_reduce would read them)
-      CgFold fo;
-      if (c.fold_alpha && dot && gated && c.fold_cnt && nb == (int)spmv_nparts(c)) {
-        fo.cnt = c.fold_cnt;
-        fo.red = c.red;
-        fo.hist = c.hist;
-        fo.cg = c.cg;
-        c.fold_done = true;
-      }
 #define MCX_VIBM(TXV, TYV, XVV, UV, PV, ...)                                                                          \
   do {                                                                                                             \
     if (dot && gated)                                                                                              \
       hipLaunchKernelGGL((k_spmv_vibm<true, true, TXV, TYV, XVV, UV, PV, ##__VA_ARGS__>), dim3(nb), dim3(1024), 0,        \
-                         c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt, FusedP{}, nullptr, fo);      \
+                         c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt);                             \
     else if (dot)                                                                                                  \
       hipLaunchKernelGGL((k_spmv_vibm<true, false, TXV, TYV, XVV, UV, PV, ##__VA_ARGS__>), dim3(nb), dim3(1024), 0,       \
                          c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt);                             \
@@ -4165,7 +4168,7 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
     if (dot && gated)                                                                                              \
       hipLaunchKernelGGL((k_spmv_vibm<true, true, TXV, TYV, true, true, true, FV, false, false, true>), dim3(nb),       \
                          dim3(1024), 0, c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt, FusedP{},      \
-                         c.vi_exc, fo);                                                                            \
+                         c.vi_exc);                                                                                \
     else if (dot)                                                                                                  \
       hipLaunchKernelGGL((k_spmv_vibm<true, false, TXV, TYV, true, true, true, FV, false, false, true>), dim3(nb),      \
                          dim3(1024), 0, c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt, FusedP{},      \
@@ -4521,11 +4524,7 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) 
   }
   if (!(c.nranks > 1 && c.overlap && c.halo.nbnd) && (rc = halo_exchange(c, pcur))) return rc;
   if (ev0) MCX_HIP(hipEventRecord(ev0, c.stream));
-  const bool fold = c.cg_fold && c.fold_cnt && c.nranks == 1 && !c.comm;
-  c.fold_alpha = fold && !fa;
-  c.fold_done = false;
   launch_spmv(c, pcur, c.w, true, true);
-  c.fold_alpha = false;
   if (ev1) MCX_HIP(hipEventRecord(ev1, c.stream));
   if (fa) {
     MCX_NT_DIX(c.cg_nt, dix,
@@ -4534,18 +4533,8 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) 
     if (!fb || last) return reduce_and_logic(c, 2, nbu, RED_BETA, true, c.partials2, A);
     return 0;
   }
-  if (!c.fold_done && (rc = reduce_and_logic(c, 1, nbs, RED_ALPHA, true, c.partials, c.cg))) return rc;
-  if (fold) {  // the beta step in the update's last block
-    CgFold fo;
-    fo.cnt = c.fold_cnt;
-    fo.red = c.red;
-    fo.hist = c.hist;
-    fo.cg = c.cg;
-    MCX_NT_DIX(c.cg_nt, dix,
-               hipLaunchKernelGGL((k_cg_update<NT, DX, true>), dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, jd,
-                                  c.jix, c.r, c.z, c.partials2, nbu, c.cg, fo));
-    return 0;
-  }
+  rc = reduce_and_logic(c, 1, nbs, RED_ALPHA, true, c.partials, c.cg);
+  if (rc) return rc;
   MCX_NT_DIX(c.cg_nt, dix,
              hipLaunchKernelGGL((k_cg_update<NT, DX>), dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, jd, c.jix, c.r,
                                 c.z, c.partials2, nbu, c.cg));

@@ -78,6 +78,7 @@ struct Ctx;
 // all 27 blocks per node in FMT_V's slot order — every row summed in the CPU AIJ order.
 enum Fmt { FMT_V = 0, FMT_U = 1, FMT_SPLIT = 2, FMT_VI = 3 };
 constexpr int VI_MAX = 256;     // dictionary entries (one index byte per value)
+constexpr int VI_EXC_LIST = 2048;  // staged value-indexed SpMV: exception nodes a tile defers to its block-wide pass
 constexpr int VI_HASH = 4096;   // open-addressing set of the distinct values (bit patterns)
 constexpr int VI_CHUNKS = 16;   // 16-B index chunks per node: 243 slots + 13 zero pad bytes
 constexpr int VIB_STRIDE = 10;  // doubles per dictionary block (9 values + pad: 16-B aligned)
@@ -138,11 +139,7 @@ struct Ctx {
   bool fusep_used = false;   // the last solve ran the fused kernel (timing: its bytes per launch)
   int cg_pdb = 1;            // option cg_pdb: p double-buffered (p_pad / p_pad2), VecAXPY(x) every second iteration
   bool pdb_used = false;     // the current solve runs the double-buffered p update
-  int cg_par = 0;            // option cg_par: PDB p update specialised per iteration parity (host count cg_it)
-  int cg_fold = 0;           // option cg_fold: alpha / beta steps in the SpMV / update kernel's last block (one rank)
-  unsigned* fold_cnt = nullptr;  // its count of finished blocks
-  bool fold_alpha = false;   // cg_iteration -> launch_spmv: fold the alpha step into the SpMV if it can
-  bool fold_done = false;    // launch_spmv -> cg_iteration: it did
+  int cg_par = 1;            // option cg_par: PDB p update specialised per iteration parity (host count cg_it)
   int* xdone = nullptr;      // PDB: the last odd iteration whose p update applied the x terms owed
   int cg_it = 0;             // iteration index of the cg_iteration being launched
   double* b = nullptr;       // residual (owned, PETSc-local order)
@@ -205,6 +202,7 @@ struct Ctx {
                              // rounding-level, not bit-exact); implies vi_uni + vi_patch
   int vi_patch = 1;          // with vi_uni: 16 x 4 node patches per wave (option vi_patch)
   int vi_ring3 = 0;          // A/B: the 3-slot x ring (two barriers per plane) for 64x16 tiles (option vi_ring3)
+  int vi_exc_list = VI_EXC_LIST;  // staged block-indexed SpMV: exception nodes per tile deferred to its block pass (option vi_exc_list)
   int vi_wmap = 1;           // staged block-indexed SpMV: 16x4 patches on SIMDs as a Latin square (option vi_wmap; 0: row-major)
   int vi_tx = 0;             // staged block-indexed SpMV tile width 256 | 128 | 64 (0: 64; option vi_tx)
   int vi_uni = 1;            // staged block-indexed SpMV: wave-uniform blocks from scalar loads (option vi_uni)

@@ -243,7 +243,7 @@ def test_cg_pdb_multirank_bitwise(grid, procs):
             "-da_processors_z", pz, "-ksp_rtol", "1e-10"]
     x = np.zeros(3 * NX * NY * NZ)
     on = run_group(argv, px * py * pz, newton_step(x, [("cg_pdb", 1), ("cg_par", 0)]))
-    par = run_group(argv, px * py * pz, newton_step(x, [("cg_pdb", 1), ("cg_par", 1), ("cg_fold", 1)]))
+    par = run_group(argv, px * py * pz, newton_step(x, [("cg_pdb", 1), ("cg_par", 1)]))
     off = run_group(argv, px * py * pz, newton_step(x, [("cg_pdb", 0)]))
     for a, b, c in zip(on, off, par):
         assert a["its"] == b["its"] and a["reason"] == b["reason"] and np.array_equal(a["du"], b["du"])

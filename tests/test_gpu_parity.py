@@ -254,6 +254,11 @@ def test_aij_vi_exception_nodes(grid, stage, vi_tx, tile):
         assert np.array_equal(m.dump_csr()[2], v1)
         m.set_option("vi_fma", 0)
         assert np.array_equal(m.spmv(x), y1)
+        # staged tiles: exception nodes computed after the march by the whole block (default), in
+        # their plane (list size 0), or both (a list of 3 that overflows): the same rows
+        for xl in (0, 3, 2048):
+            m.set_option("vi_exc_list", xl)
+            assert np.array_equal(m.spmv(x), y1), xl
         m.set_option("vi_fma", 1)
         y = m.spmv(x)
         assert np.all(np.abs(y - y1) <= 1e-14 * absrow + 1e-300)
@@ -592,22 +597,20 @@ def test_cg_pdb_bitwise(maxits, storage):
     """Option cg_pdb (default): p double-buffered and VecAXPY(x) applied on odd iterations only,
     both owed terms in PETSc's order, the rest by k_cg_xfinal — bitwise the solve of the
     single-buffer p update: converged, and stopped by maxits after odd and even iteration
-    counts (1 and 2 included); with and without the parity-specialised kernels (cg_par) and the
-    beta step folded into the update kernel's last block (cg_fold)."""
+    counts (1 and 2 included); with and without the parity-specialised kernels (cg_par)."""
     NX, NY, NZ = 70, 20, 12
     extra = ["-mat_aij_vi", 0] if storage == "split" else []
     argv = argv_for(NX, NY, NZ, 1e-12, extra) + (["-ksp_max_it", maxits] if maxits else [])
     out = []
     with M.Macroc(argv) as m:
         m.set_option("cg_fuse", 0)  # the unfused scalar steps (grids > 1,024 update blocks)
-        if storage == "vi_staged":  # the z-marching SpMV (idle blocks included), which takes cg_fold's alpha step
+        if storage == "vi_staged":  # the z-marching SpMV (idle blocks included)
             m.set_option("vi_stage", 1)
         m.apply_bc_on_u(m.get_displacement(1))
         m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
-        for pdb, par, fold in ((0, 0, 0), (1, 0, 0), (0, 1, 1), (1, 1, 1), (1, 0, 1)):
+        for pdb, par in ((0, 0), (1, 0), (0, 1), (1, 1)):
             m.set_option("cg_pdb", pdb)
             m.set_option("cg_par", par)
-            m.set_option("cg_fold", fold)
             its, rn, reason = m.solve_Ax()
             out.append((its, reason, m.du()))
     for its, reason, du in out[1:]:

@@ -25,6 +25,10 @@ ap.add_argument("--exc-max", type=int, default=None, help="aij value-indexed: vi
                 "allowed as exception nodes; 0: a per-GP tangent falls back to AIJ-split)")
 ap.add_argument("--micro-n", type=int, default=10, help="-micro_n (BASELINE config 5: 10; sizes MicroPP's micro-cell, "
                 "which the device law does not have: reported, no effect)")
+ap.add_argument("--set", default="", help="options before the run, 'name=value,...'")
+ap.add_argument("--ab", default="", help="after the run: re-solve the last Newton system alternating an option's "
+                "values, 'name=v1,v2' (same process; per-CG-iteration and SpMV times to stderr)")
+ap.add_argument("--ab-rounds", type=int, default=3)
 a = ap.parse_args()
 N = a.grid
 m = M.Macroc(["-da_grid_x", N, "-da_grid_y", N, "-da_grid_z", N, "-mat_law", "plastic", "-ksp_rtol", repr(a.rtol),
@@ -34,6 +38,8 @@ if a.maxq is not None:
     m.set_option("split_maxq", a.maxq)
 if a.exc_max is not None:
     m.set_option("vi_exc_max", a.exc_max)
+for kv in [kv for kv in a.set.split(",") if kv]:
+    m.set_option(kv.split("=")[0], float(kv.split("=")[1]))
 steps = []
 t_all = time.perf_counter()
 for ts in range(a.ts):
@@ -59,4 +65,25 @@ print(json.dumps({"workload": f"config 5 path: {N}^3 non-linear Newton (J2 callb
                   "split_slots": info["split_slots"], "split_bits": info["split_bits"], "newton_its": nits, "cg_its": sum(sum(s["ksp_its"]) for s in steps),
                   "seconds": tot, "ms_per_newton_iter": tot / max(nits, 1) * 1e3,
                   "dof_per_s": 3 * N ** 3 * nits / tot, "steps": steps}))
+if a.ab:
+    import numpy as np
+    import statistics
+    name, vals = a.ab.split("=")
+    vals = [float(v) for v in vals.split(",")]
+    res = {v: [] for v in vals}
+    spmv = {v: [] for v in vals}
+    dus = {}
+    for r in range(a.ab_rounds):
+        for v in vals:
+            m.set_option(name, v)
+            its, rn, reason = m.solve_Ax()
+            t = m.timing()
+            res[v].append(t["solve_ms"] / its)
+            spmv[v].append(t["spmv_ms_total"] / max(t["spmv_launches"], 1))
+            dus.setdefault(v, (its, m.du()))
+    for v in vals:
+        d = np.linalg.norm(dus[v][1] - dus[vals[0]][1]) / np.linalg.norm(dus[vals[0]][1])
+        print(f"A/B {N}^3 {name}={v:g}: median ms/CG iter {statistics.median(res[v]):.4f}  spmv kernel "
+              f"{statistics.median(spmv[v]):.4f} ms  its {dus[v][0]}  |du-du0|/|du0| {d:.2e}", file=sys.stderr,
+              flush=True)
 m.finish()
