@@ -1429,6 +1429,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.cg_pdb = value != 0.;
     return 0;
   }
+  if (!std::strcmp(name, "cg_rev")) {
+    c.cg_rev = value != 0.;
+    return 0;
+  }
   if (!std::strcmp(name, "cg_par")) {
     c.cg_par = (int)value;
     return 0;

@@ -3065,13 +3065,15 @@ template <bool NT, bool DIX, bool SKIP_SENT = false, int PAR = 0>
 __global__ void k_cg_pupdate_db(Geo g, const double* __restrict__ z, const double* __restrict__ dinv,
                                 const unsigned char* __restrict__ jix, double* __restrict__ pb0,
                                 double* __restrict__ pb1, double* __restrict__ x, const CgState* __restrict__ cg,
-                                int* __restrict__ xdone, const int* __restrict__ list, int64_t cnt) {
+                                int* __restrict__ xdone, const int* __restrict__ list, int64_t cnt,
+                                int rev = 0) {
   if (cg->reason) return;
   const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
   const int it = cg->i;
   if (t == 0 && (it & 1)) *xdone = it;
   if (t >= cnt) return;
-  const int n = list ? list[t] : (int)t;
+  // rev (option cg_rev): nodes from the last one down (no reduction here: same results)
+  const int n = list ? list[t] : (int)(rev ? cnt - 1 - t : t);
   if (SKIP_SENT) {
     int i, j, k;
     node_ijk(g, n, i, j, k);
@@ -4430,13 +4432,13 @@ void launch_cg_pupdate(Ctx& c, int part) {
   MCX_NT_DIX(c.cg_nt, dix, {                                                                                         \
     if (par == 1)                                                                                                    \
       hipLaunchKernelGGL((k_cg_pupdate_db<NT, DX, SKIPV, 1>), dim3(GRID), dim3(TPB), 0, c.stream, c.g, zs, jd, c.jix, \
-                         c.p_pad, c.p_pad2, c.du, c.cg, c.xdone, LIST, CNT);                                         \
+                         c.p_pad, c.p_pad2, c.du, c.cg, c.xdone, LIST, CNT, c.cg_rev);                               \
     else if (par == 2)                                                                                               \
       hipLaunchKernelGGL((k_cg_pupdate_db<NT, DX, SKIPV, 2>), dim3(GRID), dim3(TPB), 0, c.stream, c.g, zs, jd, c.jix, \
-                         c.p_pad, c.p_pad2, c.du, c.cg, c.xdone, LIST, CNT);                                         \
+                         c.p_pad, c.p_pad2, c.du, c.cg, c.xdone, LIST, CNT, c.cg_rev);                               \
     else                                                                                                             \
       hipLaunchKernelGGL((k_cg_pupdate_db<NT, DX, SKIPV, 0>), dim3(GRID), dim3(TPB), 0, c.stream, c.g, zs, jd, c.jix, \
-                         c.p_pad, c.p_pad2, c.du, c.cg, c.xdone, LIST, CNT);                                         \
+                         c.p_pad, c.p_pad2, c.du, c.cg, c.xdone, LIST, CNT, c.cg_rev);                               \
   })
     if (part == 1) {
       if (!c.halo.nbnd) return;
