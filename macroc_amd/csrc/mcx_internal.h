@@ -139,7 +139,7 @@ struct Ctx {
   bool fusep_used = false;   // the last solve ran the fused kernel (timing: its bytes per launch)
   int cg_pdb = 1;            // option cg_pdb: p double-buffered (p_pad / p_pad2), VecAXPY(x) every second iteration
   bool pdb_used = false;     // the current solve runs the double-buffered p update
-  int cg_rev = 0;            // option cg_rev: PDB p update from the last node down (the update kernel's last r writes hit the Infinity Cache)
+  int cg_rev = 1;            // option cg_rev: PDB p update from the last node down (the update kernel's last r writes hit the Infinity Cache)
   int cg_par = 1;            // option cg_par: PDB p update specialised per iteration parity (host count cg_it)
   int* xdone = nullptr;      // PDB: the last odd iteration whose p update applied the x terms owed
   int cg_it = 0;             // iteration index of the cg_iteration being launched
