@@ -1453,9 +1453,16 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.vi_ring3 = value != 0.;
     return 0;
   }
-  if (!std::strcmp(name, "vi_tx")) {
-    c.vi_tx = (int)value;
+  if (!std::strcmp(name, "vi_tx")) {  // validated before it is stored: a refused width leaves the tiling as it was
+    const int v = (int)value;
+    if (!(v == 0 || v == 64 || v == 128 || v == 256) || (double)v != value) {
+      set_error("vi_tx: 0 (default), 64, 128 or 256");
+      return 1;
+    }
+    const int old = c.vi_tx;
+    c.vi_tx = v;
     if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
+      c.vi_tx = old;
       set_error("vi_tx: partials buffer too small");
       return 7;
     }

@@ -799,16 +799,59 @@ __global__ void k_jacobi_sym(Geo g, const double* __restrict__ U, double* __rest
 }
 
 // ---------------------------------------------------------------------------- SpMV
+// The exact SpMV kernels sum every row in the order of the kernel the reference's MatMult runs:
+// PETSc's MatMult_SeqAIJ_Inode [ext] (src/mat/impls/aij/seq/inode.c; MatSeqAIJCheckInode makes
+// the 3 rows of a DMDA node, dof 3, one inode of the reference's MATAIJ, src/init.c:85-95), whose
+// unrolled loop adds a row's terms t = a x in column pairs, y = 0 + (t0 + t1) + (t2 + t3) + ...
+// [+ t_last], over the row's stored columns in ascending order (oracle/oracle.c row_part).  A
+// row's columns are its node's neighbours inside the global domain (the DMDA stencil is clipped
+// there; MatZeroRowsColumns' zeros stay in the pattern), three per neighbour block, ascending
+// (nb, c) = ascending global column on one rank.  So column c of block nb sits at position
+// 3 q + c, q = the present blocks before nb, and its term either opens a pair (even position:
+// held in e) or closes one (odd: s + (e + t)).  Blocks outside the domain (zero values, zero
+// ghost x) are skipped: an added +0 would shift the pairing of every column after it.
+// present_mask: bit nb set when neighbour nb = (dz+1)*9 + (dy+1)*3 + (dx+1) of owned node
+// (i, j, k) lies inside the global domain (any rank grid: internal faces' ghosts are present).
+constexpr unsigned PRES_ALL = (1u << 27) - 1u;
+__device__ __forceinline__ unsigned present_mask(const Geo& g, int i, int j, int k) {
+  const int gi = g.xs + i, gj = g.ys + j, gk = g.zs + k;
+  const unsigned mx = 2u | (gi > 0 ? 1u : 0u) | (gi < g.NX - 1 ? 4u : 0u);
+  const unsigned my = 2u | (gj > 0 ? 1u : 0u) | (gj < g.NY - 1 ? 4u : 0u);
+  const unsigned mz = 2u | (gk > 0 ? 1u : 0u) | (gk < g.NZ - 1 ? 4u : 0u);
+  const unsigned xb = mx * 0x1249249u;  // bit nb: dx = nb % 3 present (mx replicated every 3 bits)
+  const unsigned y9 = ((my & 1u) ? 7u : 0u) | ((my & 4u) ? 0x1c0u : 0u) | 0x38u;
+  const unsigned yb = y9 * 0x40201u;     // bit nb: dy = (nb / 3) % 3 present
+  const unsigned zb = ((mz & 1u) ? 0x1ffu : 0u) | (0x1ffu << 9) | ((mz & 4u) ? (0x1ffu << 18) : 0u);
+  return xb & yb & zb;
+}
+
+// one node's three rows in the inode order; FULL: every neighbour present (pairing fixed at
+// compile time: block nb opens with an even position when nb is even)
+template <bool FULL>
+struct InodeRows {
+  double s[3] = {0., 0., 0.}, e[3] = {0., 0., 0.};
+  unsigned pres = PRES_ALL;
+  // term t = a x of row r, column c of block nb (nb, r, c compile-time constants once unrolled)
+  __device__ __forceinline__ void term(int nb, int r, int c, double t) {
+    if (!FULL && !((pres >> nb) & 1u)) return;
+    const bool odd = FULL ? ((nb + c) & 1) : ((__builtin_popcount(pres & ((1u << nb) - 1u)) + c) & 1);
+    if (odd) s[r] = s[r] + (e[r] + t);
+    else e[r] = t;
+  }
+  __device__ __forceinline__ double row(int r) const {
+    const bool odd = FULL ? true : (__builtin_popcount(pres) & 1);  // 81 terms when every block is present
+    return odd ? s[r] + e[r] : s[r];
+  }
+};
+
 // y = A x for the owned rows.  One thread = one node = 3 rows; 122 x 16-B coalesced loads of
 // the stencil blocks, x gathered from the padded box (L1/L2 resident neighbours).  Each row
-// sums its slots in ascending (nb, c) = ascending global column on one rank, the order of
-// MatMult_SeqAIJ, so y is bit-identical to the CPU AIJ product.  DOT: per-block p.w.
+// adds its slots in ascending (nb, c) = ascending global column on one rank, in the inode
+// kernel's pairs (above), so y is bit-identical to the CPU AIJ product.  DOT: per-block p.w.
 template <int S>
-__device__ __forceinline__ void slot_acc(double v, const double (&xv)[27][3], double& y0, double& y1, double& y2) {
+__device__ __forceinline__ void slot_acc(double v, const double (&xv)[27][3], InodeRows<false>& acc) {
   constexpr int nb = S / 9, r = (S % 9) / 3, c = S % 3;
-  if (r == 0) y0 += v * xv[nb][c];
-  else if (r == 1) y1 += v * xv[nb][c];
-  else y2 += v * xv[nb][c];
+  acc.term(nb, r, c, v * xv[nb][c]);
 }
 
 template <bool NT>
@@ -825,18 +868,18 @@ __device__ __forceinline__ double2 ldv(const double2* p) {
 
 template <int Q, bool NT = false>
 struct PairLoop {
-  static __device__ __forceinline__ void run(const double2* __restrict__ v, const double (&xv)[27][3], double& y0,
-                                             double& y1, double& y2) {
-    PairLoop<Q - 1, NT>::run(v, xv, y0, y1, y2);
+  static __device__ __forceinline__ void run(const double2* __restrict__ v, const double (&xv)[27][3],
+                                             InodeRows<false>& acc) {
+    PairLoop<Q - 1, NT>::run(v, xv, acc);
     const double2 a = ldv<NT>(v + (Q - 1) * 64);
-    slot_acc<2 * (Q - 1)>(a.x, xv, y0, y1, y2);
-    if constexpr (2 * (Q - 1) + 1 < NSLOT) slot_acc<2 * (Q - 1) + 1>(a.y, xv, y0, y1, y2);
+    slot_acc<2 * (Q - 1)>(a.x, xv, acc);
+    if constexpr (2 * (Q - 1) + 1 < NSLOT) slot_acc<2 * (Q - 1) + 1>(a.y, xv, acc);
   }
 };
 template <bool NT>
 struct PairLoop<0, NT> {
-  static __device__ __forceinline__ void run(const double2* __restrict__, const double (&)[27][3], double&, double&,
-                                             double&) {}
+  static __device__ __forceinline__ void run(const double2* __restrict__, const double (&)[27][3],
+                                             InodeRows<false>&) {}
 };
 
 template <bool DOT, bool GATED, int NT = 0>
@@ -861,8 +904,10 @@ __global__ __launch_bounds__(TPB) void k_spmv(Geo g, const double2* __restrict__
       xv[nb][2] = xp[2];
     }
     const double2* v = V + (int64_t)(n >> 6) * (NPAIR * 64) + (n & 63);
-    double y0 = 0., y1 = 0., y2 = 0.;
-    PairLoop<NPAIR, (NT > 0)>::run(v, xv, y0, y1, y2);
+    InodeRows<false> acc;
+    acc.pres = present_mask(g, i, j, k);
+    PairLoop<NPAIR, (NT > 0)>::run(v, xv, acc);
+    const double y0 = acc.row(0), y1 = acc.row(1), y2 = acc.row(2);
     if constexpr (NT == 2) {
       __builtin_nontemporal_store(y0, &y[3 * n + 0]);
       __builtin_nontemporal_store(y1, &y[3 * n + 1]);
@@ -1779,7 +1824,9 @@ __global__ __launch_bounds__(TPB) void k_spmv_vi(Geo g, const u32x4* __restrict_
     u32x4 w[CH];
 #pragma unroll
     for (int q = 0; q < CH; q++) w[q] = __builtin_nontemporal_load(ip + q * 64);
-    double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+    double xc0 = 0., xc1 = 0., xc2 = 0.;
+    InodeRows<false> acc;
+    acc.pres = present_mask(g, i, j, k);
 #pragma unroll
     for (int nb = 0; nb < 27; nb++) {
       const int off = (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
@@ -1804,11 +1851,10 @@ __global__ __launch_bounds__(TPB) void k_spmv_vi(Geo g, const u32x4* __restrict_
         const int S = nb * 9 + q, r = q / 3, cc = q % 3;
         const unsigned id = vi_index<NIB>(w, S);
         const double v = (DBG & 1) ? (double)id : tab[vi_entry<NIB>(S, id)];
-        if (r == 0) y0 += v * xv[cc];
-        else if (r == 1) y1 += v * xv[cc];
-        else y2 += v * xv[cc];
+        acc.term(nb, r, cc, v * xv[cc]);
       }
     }
+    const double y0 = acc.row(0), y1 = acc.row(1), y2 = acc.row(2);
     __builtin_nontemporal_store(y0, &y[3 * n + 0]);
     __builtin_nontemporal_store(y1, &y[3 * n + 1]);
     __builtin_nontemporal_store(y2, &y[3 * n + 2]);
@@ -2205,7 +2251,9 @@ __global__ __launch_bounds__(TPB) void k_spmv_vib(Geo g, const u32x4* __restrict
     const int pc = (i + 1) + (j + 1) * PX + (k + 1) * PXY;
     const u32x4* ip = I + (int64_t)(n >> 6) * (2 * 64) + (n & 63);
     const u32x4 w0 = __builtin_nontemporal_load(ip), w1 = __builtin_nontemporal_load(ip + 64);
-    double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+    double xc0 = 0., xc1 = 0., xc2 = 0.;
+    InodeRows<false> acc;
+    acc.pres = present_mask(g, i, j, k);
 #pragma unroll
     for (int nb = 0; nb < 27; nb++) {
       const int off = (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
@@ -2230,13 +2278,9 @@ __global__ __launch_bounds__(TPB) void k_spmv_vib(Geo g, const u32x4* __restrict
         a[7] = a67.y, a[8] = a8.x;
       }
 #pragma unroll
-      for (int q = 0; q < 9; q++) {
-        const int r = q / 3, cc = q % 3;
-        if (r == 0) y0 += a[q] * xv[cc];
-        else if (r == 1) y1 += a[q] * xv[cc];
-        else y2 += a[q] * xv[cc];
-      }
+      for (int q = 0; q < 9; q++) acc.term(nb, q / 3, q % 3, a[q] * xv[q % 3]);
     }
+    const double y0 = acc.row(0), y1 = acc.row(1), y2 = acc.row(2);
     __builtin_nontemporal_store(y0, &y[3 * n + 0]);
     __builtin_nontemporal_store(y1, &y[3 * n + 1]);
     __builtin_nontemporal_store(y2, &y[3 * n + 2]);
@@ -2301,9 +2345,14 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
   // EXC: the tile's exception nodes, computed after the march by the whole block (one node per
   // thread) instead of inside their plane, where each one's nine dependent rounds of global
   // loads held the plane's barrier for every wave of the block
+  // The list is split into one segment per wave, filled in (plane, lane) order from a ballot, so
+  // every node's list position, hence the pass's thread -> node map and the block's p.w partial,
+  // is a function of the tile alone: run-to-run deterministic (an LDS atomic counter handed out
+  // positions in wave arrival order).
   constexpr int XL = EXC ? VI_EXC_LIST : 1;
+  constexpr int NW = T / 64, SEG = XL / NW > 0 ? XL / NW : 1;
   __shared__ int s_xl[XL];
-  __shared__ int s_nx;
+  __shared__ int s_wn[EXC ? NW : 1];
   if (GATED && cg->reason) return;
   const int b = blockIdx.x;
   const int xcd = b & 7, t8 = b >> 3;
@@ -2401,14 +2450,15 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
     double pn = 0.;
     if (o < len && rr < rows && gi >= 0 && gi < g.nx && gj >= 0 && gj < g.ny && p >= 0 && p < g.nz) {
       const int d = o - 3 * (o / 3);
-      const double z = f.rv * s_jdd[3 * f.jx + d];  // z = D^-1 r (k_cg_pupdate's z_of<DIX>)
+      // z = D^-1 r (k_cg_pupdate's z_of<DIX>); s_jdd holds the dictionary's entries only, so FP
+      // requires a matrix without exception nodes (jix 255 would redirect): fusep() checks vi_nexc
+      const double z = f.rv * s_jdd[3 * f.jx + d];
       pn = cgi == 0 ? z : z + cb * f.po;
       if (gi >= i0 && gi < i0 + TX && gj >= j0 && gj < j0 + TY && p >= k0 && p < k1)
         pdst[3 * (int64_t)(i0 + (j0 + rr) * PX + (p + 1) * PXY) + o] = pn;
     }
     xs[slot][e] = pn;
   };
-  if (EXC && me == 0) s_nx = 0;  // published by the prologue's barrier
   for (int t = me; t < VI_MAX * VIB_STRIDE / 2; t += T) tab[t] = reinterpret_cast<const double2*>(bdict)[t];
   if (FP) {
     for (int t = me; t < 3 * VI_MAX; t += T) s_jdd[t] = fp.jdd[t];
@@ -2427,12 +2477,9 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
 #pragma unroll
       for (int m = 0; m < NL; m++) xstore(s, m, xload(k0 - 1 + s, m));
   }
-  auto exc_defer = [&](int k) -> bool {  // this thread's node of plane k onto the tile's list
-    const int q = atomicAdd(&s_nx, 1);
-    if (q >= min(XL, zt.xlist)) return false;
-    s_xl[q] = (k - k0) * T + me;
-    return true;
-  };
+  // EXC: this wave's list entries so far (wave-uniform) and its segment's capacity
+  const int wcap = EXC ? min(SEG, (min(XL, zt.xlist) + NW - 1) / NW) : 0;
+  int wn = 0;
   u32x4 c0 = {0u, 0u, 0u, 0u}, c1 = c0, n0 = c0, n1 = c0;
   iload(k0, c0, c1);
   __syncthreads();
@@ -2464,10 +2511,27 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       unsigned diff = 0u;
 #pragma unroll
       for (int q = 0; q < 7; q++) diff |= (q < 4 ? c0[q] : c1[q - 4]) ^ sw[q];
-      uni = __all(inxy && diff == 0u && (!EXC || c1[3] == 0u)) || (zt.dbg & 1);
+      // exact rows (!FMA): the scalar path's fixed inode pairing needs every neighbour present
+      uni = __all(inxy && diff == 0u && (!EXC || c1[3] == 0u) &&
+                  (FMA || present_mask(g, i, j, k) == PRES_ALL)) || (zt.dbg & 1);
+    }
+    // EXC: the wave's exception lanes of this plane take the next positions of its segment in
+    // lane order (ballot + mbcnt, converged here); those beyond the capacity stay in the plane
+    bool deferred = false;
+    if constexpr (EXC) {
+      const bool xh = !(UNI && uni) && inxy && c1[3] != 0u;
+      const unsigned long long xm = __ballot(xh);
+      if (xm) {  // uniform
+        const int pos = wn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(xm >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((unsigned)xm, 0u));
+        deferred = xh && pos < wcap;
+        if (deferred) s_xl[wv * SEG + pos] = (k - k0) * T + me;
+        wn = min(wcap, wn + (int)__popcll(xm));
+      }
     }
     if (UNI && uni) {  // (every lane is inxy)
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+      InodeRows<true> acc;  // !FMA: the inode pairs of a node whose 27 neighbours are present
       typedef const volatile __attribute__((address_space(3))) double lds_vdouble;
       lds_vdouble* xsv = (lds_vdouble*)&xs[0][0];
       // blocks in groups of 3 (one dy row of the stencil): the 3 blocks' scalar loads are issued
@@ -2511,17 +2575,19 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
           for (int q = 0; q < 9; q++) {
             const int r = q / 3, cc = q % 3;
             double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
-            yr = FMA ? __builtin_fma(av[t][q], xv[t][cc], yr) : yr + av[t][q] * xv[t][cc];
+            if constexpr (FMA) yr = __builtin_fma(av[t][q], xv[t][cc], yr);
+            else acc.term(nb0 + t, r, cc, av[t][q] * xv[t][cc]);
           }
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+      if constexpr (!FMA) y0 = acc.row(0), y1 = acc.row(1), y2 = acc.row(2);
       const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
       __builtin_nontemporal_store(y0, &y[3 * n + 0]);
       __builtin_nontemporal_store(y1, &y[3 * n + 1]);
       __builtin_nontemporal_store(y2, &y[3 * n + 2]);
       if (DOT) dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
-    } else if (EXC && inxy && c1[3] && exc_defer(k)) {
+    } else if (EXC && deferred) {
       // deferred to the block's exception pass below
     } else if (EXC && inxy && c1[3]) {
       // an exception node (EXC instantiations only) that found the tile's list full: its 27
@@ -2530,6 +2596,8 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       // Blocks in groups of 3 (one dy row): the group's 27 values are loaded together, one
       // round trip per group instead of per block.
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+      InodeRows<false> acc;
+      if constexpr (!FMA) acc.pres = present_mask(g, i, j, k);
       const double* eb = exc + (int64_t)(c1[3] - 1) * 243;
 #pragma unroll 1
       for (int nb0 = 0; nb0 < 27; nb0 += 3) {
@@ -2550,10 +2618,12 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
           for (int q = 0; q < 9; q++) {
             const int r = q / 3, cc = q % 3;
             double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
-            yr = FMA ? __builtin_fma(av[t * 9 + q], xv[cc], yr) : yr + av[t * 9 + q] * xv[cc];
+            if constexpr (FMA) yr = __builtin_fma(av[t * 9 + q], xv[cc], yr);
+            else acc.term(nb0 + t, r, cc, av[t * 9 + q] * xv[cc]);
           }
         }
       }
+      if constexpr (!FMA) y0 = acc.row(0), y1 = acc.row(1), y2 = acc.row(2);
       const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
       __builtin_nontemporal_store(y0, &y[3 * n + 0]);
       __builtin_nontemporal_store(y1, &y[3 * n + 1]);
@@ -2561,6 +2631,8 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       if (DOT) dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
     } else if (inxy) {
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+      InodeRows<false> acc;
+      if constexpr (!FMA) acc.pres = present_mask(g, i, j, k);
       // x as separate 8-B LDS reads (ds_read_b64: 2 LDS cycles each): the compiler would pair
       // them into ds_read2_b64, 8 cycles for the same 16 B (MI355X_MICROARCH.md, LDS table);
       // volatile reads are not paired.
@@ -2597,9 +2669,11 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
         for (int q = 0; q < 9; q++) {
           const int r = q / 3, cc = q % 3;
           double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
-          yr = FMA ? __builtin_fma(a[q], xv[cc], yr) : yr + a[q] * xv[cc];
+          if constexpr (FMA) yr = __builtin_fma(a[q], xv[cc], yr);
+          else acc.term(nb, r, cc, a[q] * xv[cc]);
         }
       }
+      if constexpr (!FMA) y0 = acc.row(0), y1 = acc.row(1), y2 = acc.row(2);
       const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
       __builtin_nontemporal_store(y0, &y[3 * n + 0]);
       __builtin_nontemporal_store(y1, &y[3 * n + 1]);
@@ -2624,10 +2698,15 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
     // the exception pass: one listed node per thread, x gathered from the padded vector (the
     // values the ring held), rows in the indexed path's order and products: y bit-identical.
     // Only the block's dot partial adds these nodes' terms in another order.
+    if (ln == 0) s_wn[wv] = wn;
     __syncthreads();
-    const int ne = min(s_nx, min(XL, zt.xlist));
+    int ne = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) ne += s_wn[w];
     for (int t = me; t < ne; t += T) {
-      const int code = s_xl[t];
+      int w = 0, o = t;  // entry t of the segments in wave order
+      while (o >= s_wn[w]) o -= s_wn[w++];
+      const int code = s_xl[w * SEG + o];
       const int kk = k0 + code / T;
       int ex, ey;
       lane_xy(code % T, ex, ey);
@@ -2636,6 +2715,8 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       const unsigned slot = I[(int64_t)(n >> 6) * (2 * 64) + (n & 63) + 64][3];
       const double* eb = exc + (int64_t)(slot - 1) * 243;
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+      InodeRows<false> acc;
+      if constexpr (!FMA) acc.pres = present_mask(g, ei, ej, kk);
 #pragma unroll 1
       for (int nb0 = 0; nb0 < 27; nb0 += 3) {
         double av[27];
@@ -2658,10 +2739,12 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
           for (int q = 0; q < 9; q++) {
             const int r = q / 3, cc = q % 3;
             double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
-            yr = FMA ? __builtin_fma(av[t3 * 9 + q], xv[cc], yr) : yr + av[t3 * 9 + q] * xv[cc];
+            if constexpr (FMA) yr = __builtin_fma(av[t3 * 9 + q], xv[cc], yr);
+            else acc.term(nb0 + t3, r, cc, av[t3 * 9 + q] * xv[cc]);
           }
         }
       }
+      if constexpr (!FMA) y0 = acc.row(0), y1 = acc.row(1), y2 = acc.row(2);
       __builtin_nontemporal_store(y0, &y[3 * n + 0]);
       __builtin_nontemporal_store(y1, &y[3 * n + 1]);
       __builtin_nontemporal_store(y2, &y[3 * n + 2]);
@@ -2754,7 +2837,9 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vim(Geo g, const u32x4* __rest
       iload(k + 1, nxt);
     }
     if (inxy) {
-      double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+      double xc0 = 0., xc1 = 0., xc2 = 0.;
+      InodeRows<false> acc;
+      acc.pres = present_mask(g, i, j, k);
 #pragma unroll
       for (int nb = 0; nb < 27; nb++) {
         const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
@@ -2769,11 +2854,10 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vim(Geo g, const u32x4* __rest
         for (int q = 0; q < 9; q++) {
           const int S = nb * 9 + q, r = q / 3, cc = q % 3;
           const double v = tab[vi_entry<NIB>(S, vi_index<NIB>(cur, S))];
-          if (r == 0) y0 += v * xv[cc];
-          else if (r == 1) y1 += v * xv[cc];
-          else y2 += v * xv[cc];
+          acc.term(nb, r, cc, v * xv[cc]);
         }
       }
+      const double y0 = acc.row(0), y1 = acc.row(1), y2 = acc.row(2);
       const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
       __builtin_nontemporal_store(y0, &y[3 * n + 0]);
       __builtin_nontemporal_store(y1, &y[3 * n + 1]);
@@ -3215,7 +3299,8 @@ __global__ __launch_bounds__(UTPB) void k_cg_update_x(Geo g, const double* __res
       const int q = 3 * n + d;
       const double rv = r[q] + ma * w[q];
       st<NT>(&r[q], rv);
-      const double zv = rv * jdd[3 * jx + d];
+      // jix 255: the node's entry of the Jacobi vector behind the dictionary's (jac_inv<true>)
+      const double zv = rv * (jx == 255u ? jdd[3 * VI_MAX + q] : jdd[3 * jx + d]);
       zz += zv * zv;
       zr += zv * rv;
     }

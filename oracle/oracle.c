@@ -53,6 +53,7 @@ struct orc_problem {
   int64_t *dir;
   int64_t ndir;
   double *r, *z, *pp, *w, *dinv; /* CG work vectors */
+  int spmv_order;                /* ORC_SPMV_INODE (MATAIJ default) | ORC_SPMV_SEQAIJ (plain; SBAIJ mirror) */
 };
 
 /* ------------------------------------------------------------------------------------
@@ -980,26 +981,58 @@ void orc_assembly_jac(orc_problem* P) {
   }
 }
 
-/* MatMult: rows summed in ascending column order (MatMult_SeqAIJ); with several ranks the
-   MPIAIJ split is emulated: owned-column block first, then off-rank columns [ext] */
-void orc_spmv(const orc_problem* P, const double* x, double* y) {
+/* One row's part of MatMult, sum0 + the terms of its columns col in [lo, hi) or outside it
+   (own = 0), in ascending column order.
+   ORC_SPMV_INODE — MatMult_SeqAIJ_Inode / MatMultAdd_SeqAIJ_Inode [ext] (PETSc
+   src/mat/impls/aij/seq/inode.c, the kernel a MATAIJ with identical consecutive row patterns
+   runs: MatSeqAIJCheckInode groups the 3 rows of a DMDA node, dof 3, into one inode, and
+   KSPSolve's MatMult dispatches to it).  Its unrolled loop adds the row's terms in column
+   pairs, `sum += v[0]*x[i1] + v[1]*x[i2]`, then an odd last term, `sum += v[0]*x[i1]`; the x86
+   build has no FMA, so every product and sum is rounded as written:
+     sum = sum0 + (t0 + t1) + (t2 + t3) + ... [+ t_last],   t = a * x.
+   The pairs run over the row's stored columns, so a column clipped by the DMDA stencil at the
+   domain boundary shifts the pairing of the columns after it, and the zeroed (MatZeroRowsColumns)
+   entries, which stay in the pattern, take part.
+   ORC_SPMV_SEQAIJ — MatMult_SeqAIJ's plain loop, sum += a * x term by term. */
+static double row_part(const orc_problem* P, int64_t row, int64_t lo, int64_t hi, int own, double sum0,
+                       const double* x, int order) {
+  double sum = sum0, pend = 0.;
+  int have = 0;
+  for (int64_t q = P->rowptr[row]; q < P->rowptr[row + 1]; q++) {
+    const int64_t col = P->colidx[q];
+    if ((col >= lo && col < hi) != own) continue;
+    const double t = P->val[q] * x[col];
+    if (order == ORC_SPMV_SEQAIJ) {
+      sum += t;
+    } else if (!have) {
+      pend = t;
+      have = 1;
+    } else {
+      sum += pend + t;
+      have = 0;
+    }
+  }
+  if (have) sum += pend;
+  return sum;
+}
+
+/* MatMult (KSPSolve's, src/assembly.c:185): one rank = the SeqAIJ kernel above over the row;
+   several ranks = MatMult_MPIAIJ, the diagonal (owned-column) block first, then MatMultAdd of
+   the off-diagonal block (its columns, the compressed ghosts, in ascending global order)
+   starting from that sum [ext]. */
+void orc_spmv_order(const orc_problem* P, const double* x, double* y, int order) {
 #pragma omp parallel for schedule(static)
   for (int r = 0; r < P->nranks; r++) {
     int64_t c0 = 3 * P->node_off[r], c1 = 3 * P->node_off[r + 1];
     for (int64_t row = c0; row < c1; row++) {
-      double sum = 0.;
-      for (int64_t q = P->rowptr[row]; q < P->rowptr[row + 1]; q++) {
-        int64_t col = P->colidx[q];
-        if (col >= c0 && col < c1) sum += P->val[q] * x[col];
-      }
-      for (int64_t q = P->rowptr[row]; q < P->rowptr[row + 1]; q++) {
-        int64_t col = P->colidx[q];
-        if (!(col >= c0 && col < c1)) sum += P->val[q] * x[col];
-      }
+      double sum = row_part(P, row, c0, c1, 1, 0., x, order);
+      if (P->nranks > 1) sum = row_part(P, row, c0, c1, 0, sum, x, order);
       y[row] = sum;
     }
   }
 }
+
+void orc_spmv(const orc_problem* P, const double* x, double* y) { orc_spmv_order(P, x, y, P->spmv_order); }
 
 /* KSPConvergedDefault [ext] */
 static int converged_default(double rnorm, double ttol, double abstol, double divtol, double rnorm0) {
@@ -1317,6 +1350,9 @@ int orc_petsc_numbering(int64_t M, int64_t N, int64_t P, int size, int m, int n,
    (global column >= row) of what assembly_jac inserts and MatMult uses its transpose for the
    lower triangle (MatMult_SeqSBAIJ_3).  Emulated by mirroring the assembled AIJ values. */
 void orc_sbaij_mirror(orc_problem* P) {
+  /* MatMult_SeqSBAIJ_3's order (a block-row scatter) is not restated: the mirrored matrix is
+     multiplied in plain ascending column order (the GPU SBAIJ kernels are held to rounding) */
+  P->spmv_order = ORC_SPMV_SEQAIJ;
   for (int64_t row = 0; row < P->ndofs; row++)
     for (int64_t q = P->rowptr[row]; q < P->rowptr[row + 1]; q++) {
       int64_t col = P->colidx[q];

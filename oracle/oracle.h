@@ -18,7 +18,7 @@
  * unpinned — restated from PETSc's public source):
  *   DMDA 3-D partition (PETSC_DECIDE heuristic, ownership split, rank-contiguous
  *   global ordering), DMDAGetElements Q1 connectivity, DMDA box-stencil AIJ pattern,
- *   MatZeroRowsColumns, MatMult_SeqAIJ/MPIAIJ row-sum order, PCJacobi, KSPSolve_CG with
+ *   MatZeroRowsColumns, MatMult_SeqAIJ_Inode/MPIAIJ row-sum order, PCJacobi, KSPSolve_CG with
  *   KSP_NORM_PRECONDITIONED and KSPConvergedDefault.
  * MicroPP (the Gauss-point callback, not vendored) is replaced by an isotropic
  * linear-elastic material (both reference materials are E=1e7, nu=0.25, src/init.c:31-32).
@@ -126,7 +126,10 @@ void orc_assembly_res(orc_problem* P);
 double orc_norm2(const orc_problem* P, const double* v);
 void orc_assembly_jac(orc_problem* P);
 void orc_sbaij_mirror(orc_problem* P);
-void orc_spmv(const orc_problem* P, const double* x, double* y);
+/* MatMult row-sum orders: the MATAIJ inode kernel (default) or MatMult_SeqAIJ's plain loop */
+enum { ORC_SPMV_INODE = 0, ORC_SPMV_SEQAIJ = 1 };
+void orc_spmv(const orc_problem* P, const double* x, double* y);  /* the problem's order */
+void orc_spmv_order(const orc_problem* P, const double* x, double* y, int order);
 /* KSPSolve(CG, Jacobi) of A du = b; hist (len maxits+1, may be NULL) = residual history */
 int orc_solve(orc_problem* P, int* its, double* rnorm, int* reason, double* hist);
 void orc_update_u(orc_problem* P);

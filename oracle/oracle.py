@@ -86,6 +86,7 @@ def lib(path=None):
         L.orc_norm2.argtypes = [P, d]
         L.orc_norm2.restype = C.c_double
         L.orc_spmv.argtypes = [P, d, d]
+        L.orc_spmv_order.argtypes = [P, d, d, C.c_int]
         L.orc_solve.argtypes = [P, C.POINTER(C.c_int), C.POINTER(C.c_double), C.POINTER(C.c_int), d]
         L.orc_dmda_decide.argtypes = [C.c_int64, C.c_int64, C.c_int64, C.c_int,
                                       C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
@@ -282,10 +283,15 @@ class Problem:
         """-dm_mat_type sbaij semantics: lower triangle := transpose of the upper triangle."""
         lib().orc_sbaij_mirror(self._p)
 
-    def spmv(self, x):
+    def spmv(self, x, order=None):
+        """MatMult.  order None: the problem's (the MATAIJ inode kernel's column pairs; after
+        sbaij_mirror the plain loop), "inode", or "plain" (MatMult_SeqAIJ, one term at a time)."""
         x = np.ascontiguousarray(x, dtype=np.float64)
         y = np.zeros(self.ndofs)
-        lib().orc_spmv(self._p, _dp(x), _dp(y))
+        if order is None:
+            lib().orc_spmv(self._p, _dp(x), _dp(y))
+        else:
+            lib().orc_spmv_order(self._p, _dp(x), _dp(y), {"inode": 0, "plain": 1}[order])
         return y
 
     def solve(self, history=False):

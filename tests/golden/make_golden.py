@@ -283,6 +283,49 @@ class System:
         return x, its, hist
 
 
+# ----------------------------------------------------------------- MatMult row orders
+def _row_sums(indptr, t, sel, s0, inode):
+    """Per row: s0 + the selected terms (CSR order = ascending column) of t, either one at a time
+    (MatMult_SeqAIJ) or in column pairs, sum + (t0 + t1) + (t2 + t3) + ... + t_last
+    (MatMult_SeqAIJ_Inode's unrolled loop [ext]).  Vectorised over rows: pair sums first, then
+    one pass per pair index, so every row's additions happen in its own order."""
+    n = len(indptr) - 1
+    rows = np.repeat(np.arange(n), np.diff(indptr))
+    r, tt = rows[sel], t[sel]
+    cnt = np.bincount(r, minlength=n)
+    start = np.concatenate([[0], np.cumsum(cnt)[:-1]]).astype(np.int64)
+    pos = np.arange(len(r)) - start[r]
+    s = np.array(s0, dtype=np.float64, copy=True)
+    if not inode:
+        for k in range(int(cnt.max()) if n else 0):
+            m = pos == k
+            s[r[m]] = s[r[m]] + tt[m]
+        return s
+    first = np.nonzero((pos % 2 == 0) & (pos + 1 < cnt[r]))[0]
+    ps, pr, pk = tt[first] + tt[first + 1], r[first], pos[first] // 2
+    for k in range(int(pk.max()) + 1 if len(pk) else 0):
+        m = pk == k
+        s[pr[m]] = s[pr[m]] + ps[m]
+    odd = cnt % 2 == 1
+    s[odd] = s[odd] + tt[(start + cnt - 1)[odd]]
+    return s
+
+
+def spmv(indptr, indices, data, x, dof_off=None, inode=True):
+    """MatMult of a CSR matrix in PETSc numbering, restated independently of oracle.c: one rank
+    (dof_off None) = the SeqAIJ kernel over each row; several = MatMult_MPIAIJ, the owned-column
+    block then MatMultAdd of the off-diagonal block from that sum."""
+    t = data * x[indices]
+    n = len(indptr) - 1
+    if dof_off is None:
+        return _row_sums(indptr, t, np.ones(len(t), dtype=bool), np.zeros(n), inode)
+    rows = np.repeat(np.arange(n), np.diff(indptr))
+    rk = np.searchsorted(dof_off, rows, side="right") - 1
+    own = (indices >= dof_off[rk]) & (indices < dof_off[rk + 1])
+    s = _row_sums(indptr, t, own, np.zeros(n), inode)
+    return _row_sums(indptr, t, ~own, s, inode)
+
+
 # ----------------------------------------------------------------- fixtures
 CASES = [
     # name, grid, nranks, decomposition (0 = decide), ksp_rtol
@@ -341,6 +384,14 @@ def generate(write=True, verbose=True):
         Aref = S.A
         Aorc = P.A_values()
         assert np.allclose(Aorc, Aref.data, rtol=1e-12, atol=1e-13 * np.abs(Aref.data).max()), name
+        # MatMult row orders: the oracle's inode (default) and plain kernels vs this restatement,
+        # bit for bit on the oracle's matrix; the inode order differs from the plain one
+        xr = np.random.default_rng(7).uniform(-1, 1, P.ndofs)
+        off = None if nr == 1 else np.array([P.dof_offset(r) for r in range(nr)] + [P.ndofs])
+        y_in = P.spmv(xr)
+        assert np.array_equal(y_in, spmv(rp, ci, Aorc, xr, off, inode=True)), name
+        assert np.array_equal(P.spmv(xr, "plain"), spmv(rp, ci, Aorc, xr, off, inode=False)), name
+        assert np.allclose(y_in, Aref @ xr, rtol=1e-12, atol=1e-12 * np.abs(Aref.data).max()), name
         du_direct = spla.spsolve(Aref.tocsc(), b_ref)
         du_orc = P.du()
         rel_direct = np.linalg.norm(du_orc - du_direct) / np.linalg.norm(du_direct)

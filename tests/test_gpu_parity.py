@@ -279,6 +279,56 @@ def test_aij_vi_exception_nodes(grid, stage, vi_tx, tile):
         assert np.array_equal(m.dump_csr()[2], v1)
 
 
+def _exc_waves_per_plane(P, NX, NY, NZ, TX=64, TY=16):
+    """Host restatement of which staged-SpMV waves hold exception nodes: the owned nodes of the
+    elements with a Gauss-point tangent other than the elastic branch's (the mode of ctan), mapped
+    to (tile, plane) -> set of 16x4-patch waves under the Latin-square layout (vi_wmap 1)."""
+    ct = P.ctan().reshape(-1, 8, 36)
+    vals, counts = np.unique(ct.reshape(-1, 36), axis=0, return_counts=True)
+    cref = vals[np.argmax(counts)]
+    nonplain = np.nonzero(np.any(np.any(ct != cref, axis=2), axis=1))[0]
+    ex, ey, ez = nonplain % (NX - 1), (nonplain // (NX - 1)) % (NY - 1), nonplain // ((NX - 1) * (NY - 1))
+    waves = {}
+    for a in (0, 1):
+        for b_ in (0, 1):
+            for c in (0, 1):
+                for i, j, k in zip(ex + a, ey + b_, ez + c):
+                    lx, ly = i % TX, j % TY
+                    px, py = lx // 16, ly // 4
+                    wq = py * 4 + ((px + py) & 3) + 16 * (px // 4)
+                    waves.setdefault((i // TX, j // TY, k), set()).add(wq)
+    return waves
+
+
+def test_aij_vi_exception_pass_deterministic():
+    """The staged SpMV's block-wide exception pass is deterministic by construction: each wave
+    fills its own segment of the tile's list in (plane, lane) order (ballot), so the list, the
+    pass's thread -> node map and the block's p.w partial do not depend on wave scheduling.
+    Precondition asserted: some tile plane holds exception nodes in two or more waves.  Repeated
+    solves (default FMA rows, and -mat_vi_fma 0) are bitwise equal, with equal iteration counts."""
+    NX, NY, NZ = 130, 9, 12
+    rtol = 1e-10
+    P, u = plastic_state(NX, NY, NZ, rtol=rtol)
+    waves = _exc_waves_per_plane(P, NX, NY, NZ)
+    assert max(len(w) for w in waves.values()) >= 2, waves
+    argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-dt", 0.01, "-mat_law", "plastic",
+            "-ksp_rtol", repr(rtol)]
+    with M.Macroc(argv) as m:
+        m.set_u(u)
+        m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
+        info = m.get_info()
+        assert info["storage"] == 3 and info["vi_exc_nodes"] > 0 and (info["spmv_tx"], info["spmv_ty"]) == (64, 16)
+        for fma in (1, 0):
+            m.set_option("vi_fma", fma)
+            runs = []
+            for _ in range(3):
+                its, rn, reason = m.solve_Ax()
+                runs.append((its, rn, m.du().copy()))
+            assert reason > 0
+            for its, rn, du in runs[1:]:
+                assert its == runs[0][0] and rn == runs[0][1] and np.array_equal(du, runs[0][2]), fma
+
+
 @pytest.mark.parametrize("name", SINGLE)
 def test_aij_split_single_rank(name):
     """AIJ-split storage: upper blocks + bf16 lower corrections.  Every AIJ value is

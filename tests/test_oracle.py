@@ -39,6 +39,52 @@ def test_calc_B_fixture():
     assert np.array_equal(Bo, load("calc_B")["B"])
 
 
+def _golden_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_golden", os.path.join(GOLDEN, "make_golden.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_inode_pairing_by_hand():
+    """MatMult_SeqAIJ_Inode's unrolled loop [ext]: sum += v0*x0 + v1*x1 per column pair, then the odd
+    last term.  Terms chosen so the pairing shows in the rounding: (t0 + t1) + (t2 + t3) keeps the two
+    sub-half-ulp terms' sum, ((t0 + t1) + t2) + t3 loses both; an odd row ends with its last term."""
+    G = _golden_module()
+    t = np.array([1.0, 0.0, 0.75e-16, 0.75e-16, 0.5, 0.25, 3.0])
+    indptr = np.array([0, 4, 7])
+    y_in = G.spmv(indptr, np.array([0, 1, 2, 3, 0, 1, 2]), t, np.ones(4), inode=True)
+    y_pl = G.spmv(indptr, np.array([0, 1, 2, 3, 0, 1, 2]), t, np.ones(4), inode=False)
+    assert y_in[0] == 1.0 + 2.0 ** -52 and y_pl[0] == 1.0
+    assert y_in[1] == (0.0 + (0.5 + 0.25)) + 3.0
+
+
+@pytest.mark.parametrize("grid,nranks", [((6, 5, 4), 1), ((6, 5, 4), 2), ((7, 4, 5), 3), ((6, 6, 6), 8)])
+def test_spmv_orders_vs_numpy(grid, nranks):
+    """The oracle's MatMult in both row orders (the MATAIJ inode kernel, the default; the plain
+    SeqAIJ loop) against make_golden.py's independent numpy restatement, bit for bit, on an
+    assembled matrix with Dirichlet rows and clipped boundary stencils; MPIAIJ = owned block
+    then off-diagonal block.  The two orders differ, and both agree with scipy to rounding."""
+    G = _golden_module()
+    P = O.Problem(*grid, nranks=nranks)
+    P.apply_bc_u(P.get_displacement(1))
+    P.set_strains(); P.homogenize(); P.assembly_jac()
+    rp, ci = P.csr()
+    v = P.A_values()
+    x = np.random.default_rng(11).uniform(-1, 1, P.ndofs)
+    off = None if nranks == 1 else np.array([P.dof_offset(r) for r in range(nranks)] + [P.ndofs])
+    y_in, y_pl = P.spmv(x), P.spmv(x, "plain")
+    assert np.array_equal(y_in, P.spmv(x, "inode"))
+    assert np.array_equal(y_in, G.spmv(rp, ci, v, x, off, inode=True))
+    assert np.array_equal(y_pl, G.spmv(rp, ci, v, x, off, inode=False))
+    assert not np.array_equal(y_in, y_pl)
+    import scipy.sparse as sp
+    ys = sp.csr_matrix((v, ci, rp), shape=(P.ndofs, P.ndofs)) @ x
+    assert np.allclose(y_in, ys, rtol=1e-12, atol=1e-12 * np.abs(v).max())
+    P.close()
+
+
 @pytest.mark.parametrize("name", CASES)
 def test_oracle_vs_golden(name):
     fx = load(name)

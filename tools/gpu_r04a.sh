@@ -1,0 +1,8 @@
+#!/bin/bash
+# round 4a: parity + multirank suites after the inode row order and the deterministic exception
+# list, then the config-5 determinism check (defaults twice in one process)
+set -euo pipefail
+export TMPDIR=/tmp; mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_multirank.py -x -v --timeout 300 \
+  --timeout-method thread > gpurun_out/r04a_pytest.log 2>&1
+timeout -k 10 300 python -u tools/determinism_check.py --grid 128 --ts 3 --opts ';' > gpurun_out/r04_determinism_128.log 2>&1
