@@ -131,65 +131,67 @@ def host_cores():
     return n
 
 
-def oracle_timing_build():
-    """-O3 -march=native build of the oracle for this host (timing only; -ffp-contract=off kept,
-    so it computes the same numbers as the checker build).  Falls back to the in-tree -O2 build."""
+MPI_DIR = "/opt/conda"  # MPICH (its mpicc wrapper names a compiler that is not installed: gcc + its flags)
+
+
+def cpu_mpi_build():
+    """-O3 -march=native build of oracle/cpu_mpi.c for this host (timing only; -ffp-contract=off
+    kept: the arithmetic of the reference's x86-64 build).  Falls back to the in-tree -O2 build."""
     here = os.path.dirname(os.path.abspath(__file__))
-    out = os.path.join(tempfile.mkdtemp(prefix="mcx_oracle_"), "liboracle_native.so")
-    cmd = ["gcc", "-O3", "-march=native", "-fPIC", "-ffp-contract=off", "-fopenmp", "-std=gnu11", "-shared", "-o",
-           out, os.path.join(here, "oracle", "oracle.c"), "-lm"]
+    out = os.path.join(tempfile.mkdtemp(prefix="mcx_cpu_mpi_"), "macroc_cpu_mpi")
+    cmd = ["gcc", "-O3", "-march=native", "-ffp-contract=off", "-std=gnu11", "-o", out,
+           os.path.join(here, "oracle", "cpu_mpi.c"), os.path.join(here, "oracle", "oracle.c"), "-lm",
+           f"-I{MPI_DIR}/include", "-Wl,-rpath-link,/usr/lib/x86_64-linux-gnu", f"{MPI_DIR}/lib/libmpi.so",
+           f"-Wl,-rpath,{MPI_DIR}/lib"]
     try:
         subprocess.run(cmd, check=True, timeout=120, capture_output=True)
         return out, "gcc -O3 -march=native -ffp-contract=off"
     except (OSError, subprocess.SubprocessError):
-        return None, "gcc -O2 (in-tree build; the -march=native build failed)"
+        exe = os.path.join(here, "oracle", "macroc_cpu_mpi")
+        return (exe if os.path.exists(exe) else None), "gcc -O2 (in-tree build; the -march=native build failed)"
 
 
-def cpu_baseline(N, threads, gpu_its, rtol, ndofs_target, nelem_target, nnz_target, cg_cap):
-    """The oracle — the C restatement of the reference path, its MPI ranks run as OpenMP threads
-    (one emulated rank per host core, PETSc stash / per-rank dot semantics) — on an N^3 sample of
-    the same workload: full assembly + homogenize + residual, then `cg_cap` CG iterations.  Its
-    per-element assembly time and per-(CG iteration x nonzero) time are scaled to the target
-    grid with the GPU run's CG iteration count."""
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from oracle import oracle as O
-
-    path, build = oracle_timing_build()
-    if path:
-        O.use_library(path)
-    used = O.set_threads(threads)
-    P = O.Problem(N, N, N, nranks=used, rtol=rtol, maxits=cg_cap)
-    P.apply_bc_u(P.get_displacement(0))
-    P.apply_bc_u(P.get_displacement(1))
+def cpu_baseline(G, cores, rtol, gpu_its, G_target, timeout):
+    """The reference's path on the host cores the way the reference runs: oracle/cpu_mpi.c (the
+    Newton step of src/main.c:61-79 with MPIAIJ storage, the inode MatMult, KSPSolve_CG + PCJacobi,
+    MPI halo exchange and all-reduces) under `mpirun -np <cores>` with PETSC_DECIDE's processor
+    grid, one full step to rtol on a G^3 grid: measured, not extrapolated.  The same step at the
+    headline grid is estimated beside it (`extrapolated_target`): the measured per-element
+    assembly time and per-(CG iteration x nonzero) solve time scaled with the GPU run's iteration
+    count."""
+    exe, build = cpu_mpi_build()
+    mpirun = os.path.join(MPI_DIR, "bin", "mpirun")
+    if not exe or not os.path.exists(mpirun):
+        return {"error": "MPICH (mpirun) or the cpu_mpi build is not available"}
+    cmd = [mpirun, "-np", str(cores), exe, "-da_grid_x", str(G), "-da_grid_y", str(G), "-da_grid_z", str(G),
+           "-ksp_rtol", repr(rtol), "-steps", "1", "-warmup", "0"]
     t0 = time.perf_counter()
-    P.set_strains()
-    P.homogenize()
-    P.assembly_res()
-    P.norm_b()
-    t1 = time.perf_counter()
-    P.assembly_jac()
-    t2 = time.perf_counter()
-    out = P.solve()
-    t3 = time.perf_counter()
-    P.update_u()
-    t4 = time.perf_counter()
-    nelem = (N - 1) ** 3
-    t_elem = (t2 - t0) / nelem
-    t_it_nnz = (t3 - t2) / max(out["its"], 1) / P.nnz
-    t_vec = (t4 - t3) / P.ndofs
-    t_target = t_elem * nelem_target + t_it_nnz * gpu_its * nnz_target + t_vec * ndofs_target
-    P.close()
+    out = subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=timeout)
+    wall = time.perf_counter() - t0
+    rec = json.loads(out.stdout.strip().splitlines()[-1])
+    ph = rec["phases_s"]
+    f = (G_target - 1) ** 3 / (G - 1) ** 3
+    t_asm = ph["strains"] + ph["homogenize"] + ph["residual"] + ph["jacobian"] + ph["update"]
+    t_target = t_asm * f + ph["solve"] * f * gpu_its / max(rec["its"], 1)
     return {
-        "value": ndofs_target / t_target,
+        "value": 3 * G ** 3 / rec["step_s"],
         "unit": "DOF/s",
-        "cores": used,
+        "cores": cores,
         "kind": "port",
-        "sample": (f"oracle/ (C restatement of the reference path, {build}, {used} OpenMP threads = {used} emulated "
-                   f"MPI ranks, one per usable host core) on {N}^3: assembly {t2 - t0:.1f} s, {out['its']} CG its "
-                   f"{t3 - t2:.1f} s; per-element and per-(CG-iteration x nonzero) times scaled to the GPU workload "
-                   f"with its {gpu_its} CG iterations"),
-        "sample_seconds": t4 - t0,
-        "extrapolated_step_seconds": t_target,
+        "sample": (f"oracle/cpu_mpi.c ({build}): `mpirun -np {cores}` (MPICH, one rank per usable host core, "
+                   f"processors {'x'.join(map(str, rec['procs']))}), one full Newton step at {G}^3 to rtol {rtol:g}: "
+                   f"{rec['its']} CG its, measured (assembly {t_asm:.1f} s, solve {ph['solve']:.1f} s); the value is "
+                   f"that grid's Newton-iter DOF/s"),
+        "grid": [G, G, G],
+        "measured_step_seconds": rec["step_s"],
+        "cg_its": rec["its"],
+        "reason": rec["reason"],
+        "phases_s": ph,
+        "mpirun_wall_seconds": wall,
+        "extrapolated_target": {"grid": [G_target] * 3, "step_seconds": t_target,
+                                "value": 3 * G_target ** 3 / t_target,
+                                "how": f"assembly x (elements ratio {f:.2f}), solve x elements ratio x GPU CG its "
+                                       f"{gpu_its} / {rec['its']}"},
     }
 
 
@@ -322,9 +324,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--grid", type=int, default=256, help="nodes per direction per GPU")
     ap.add_argument("--rtol", type=float, default=1e-8)
-    ap.add_argument("--cpu-sample", type=int, default=128, help="oracle sample grid (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="oracle threads (0 = every usable host core)")
-    ap.add_argument("--cpu-cg-its", type=int, default=240, help="CG iterations of the oracle sample")
+    ap.add_argument("--cpu-grid", type=int, default=128, help="grid of the CPU baseline's full MPI step (0 = skip)")
+    ap.add_argument("--cpu-ranks", type=int, default=0, help="MPI ranks of the CPU baseline (0 = every usable core)")
+    ap.add_argument("--cpu-timeout", type=float, default=600.0, help="seconds the CPU baseline may take")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--mat-type", default="aij", choices=list(STORAGE_ARGS), help="matrix storage of the headline")
     ap.add_argument("--variants", default=None,
@@ -395,11 +397,11 @@ def main():
             log("config5 " + json.dumps(config5))
     if rank == 0:
         cpu = None
-        if world == 1 and args.cpu_sample > 0:
+        if world == 1 and args.cpu_grid > 0:
             try:
-                threads = args.cpu_threads or host_cores()
-                cpu = cpu_baseline(args.cpu_sample, threads, its, args.rtol, ndofs, (NX - 1) * (NY - 1) * (NZ - 1),
-                                   info["nnz_global"], args.cpu_cg_its)
+                log(f"cpu_baseline: mpirun, {args.cpu_grid}^3 ...")
+                cpu = cpu_baseline(args.cpu_grid, args.cpu_ranks or host_cores(), args.rtol, its, G, args.cpu_timeout)
+                log("cpu_baseline " + json.dumps(cpu))
             except Exception as e:  # the baseline is reported, never the product path
                 cpu = {"error": repr(e)}
         csr_ms_at_peak = r["csr_bytes"] / (PEAK_HBM_GBS * 1e9) * 1e3
