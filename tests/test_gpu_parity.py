@@ -279,6 +279,29 @@ def test_aij_vi_exception_nodes(grid, stage, vi_tx, tile):
         assert np.array_equal(m.dump_csr()[2], v1)
 
 
+@pytest.mark.parametrize("grid", [(130, 9, 12), (70, 20, 7)])
+def test_aij_vi_exact_rows_end_to_end(grid):
+    """-mat_vi_fma 0 (the exact rows: products and sums in the inode kernel's order, as the
+    reference's MatMult) through the whole Newton step on the production 64x16 tiles: every
+    SpMV of the solve equals the oracle's bit for bit, so only the CG's dot-product reduction
+    order differs — the iteration count equals the oracle's and du is within 1e-10."""
+    NX, NY, NZ = grid
+    rtol = 1e-12
+    P = O.Problem(NX, NY, NZ, rtol=rtol)
+    out = P.newton_step1()
+    with M.Macroc(argv_for(NX, NY, NZ, rtol, ["-mat_vi_fma", 0])) as m:
+        for ts in (0, 1):
+            m.apply_bc_on_u(m.get_displacement(ts))
+        m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
+        info = m.get_info()
+        assert info["storage"] == 3 and (info["spmv_tx"], info["spmv_ty"]) == (64, 16), info
+        x = np.random.default_rng(3).uniform(-1, 1, m.n)
+        assert np.array_equal(m.spmv(x), P.spmv(x))
+        its, rn, reason = m.solve_Ax()
+        assert reason == out["reason"] and its == out["its"], (its, out["its"])
+        assert np.linalg.norm(m.du() - P.du()) <= 1e-10 * np.linalg.norm(P.du())
+
+
 def _exc_waves_per_plane(P, NX, NY, NZ, TX=64, TY=16):
     """Host restatement of which staged-SpMV waves hold exception nodes: the owned nodes of the
     elements with a Gauss-point tangent other than the elastic branch's (the mode of ctan), mapped
