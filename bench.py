@@ -45,7 +45,7 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # matrix storages: the reference's -dm_mat_type aij (DMSetMatType(da, MATAIJ), src/init.c:92) held
 # value-indexed (one index byte per value into the matrix's <= 256 distinct values; the default,
 # with fallback), as upper blocks + exact bf16 lower corrections (aij-split) or as plain AIJ blocks
-# summed in the CPU AIJ order; -dm_mat_type sbaij through DMSetFromOptions (src/init.c:93)
+# summed in the reference's MatMult order (inode column pairs); -dm_mat_type sbaij through DMSetFromOptions (src/init.c:93)
 STORAGE_ARGS = {"aij": ["-dm_mat_type", "aij"], "aij-vi-exact": ["-dm_mat_type", "aij", "-mat_vi_fma", 0],
                 "aij-split": ["-dm_mat_type", "aij", "-mat_aij_vi", 0],
                 "aij-blocks": ["-dm_mat_type", "aij", "-mat_aij_vi", 0, "-mat_aij_split", 0],
@@ -290,13 +290,13 @@ def measure(argv, rank, world, comm_id, args, steps, warmup):
             "warmup_s": t_warm}
 
 
-def nonlinear_leg(G, ts, dt, rtol, device):
+def nonlinear_leg(G, ts, dt, rtol, device, extra=()):
     """BASELINE config 5's path (G^3, the J2 Gauss-point law, non-linear Newton; tools/bench_nonlinear.py):
     time steps 0 .. ts-1 of src/main.c:49-109 in this process, default AIJ storage.  Reported beside
     the headline (config5 in the line), never the headline: per-GP tangents keep the plastic zone's
     nodes as exception nodes."""
     m = M.Macroc(["-da_grid_x", G, "-da_grid_y", G, "-da_grid_z", G, "-mat_law", "plastic", "-ksp_rtol", repr(rtol),
-                  "-ts", ts, "-dt", dt, "-micro_n", 10, "-device", device])
+                  "-ts", ts, "-dt", dt, "-micro_n", 10, "-device", device, *extra])
     try:
         m.set_timing(True)
         steps, t0 = [], time.perf_counter()
@@ -311,8 +311,10 @@ def nonlinear_leg(G, ts, dt, rtol, device):
     finally:
         m.finish()
     nits = sum(s["newton_its"] for s in steps)
-    return {"workload": f"config 5 path: {G}^3 J2 law, {ts} time steps (step 0: zero load), dt {dt}, rtol {rtol:g}",
-            "mat_type": "aij", "storage": {0: "aij-blocks", 1: "sbaij", 2: "aij-split", 3: "aij-vi"}[steps[-1]["storage"]],
+    mt = "sbaij" if "sbaij" in [str(e) for e in extra] else "aij"
+    bc = "BC_BENDING" if "-bc_type" in [str(e) for e in extra] else "BC_CIRCLE"
+    return {"workload": f"config 5 path: {G}^3 J2 law, {bc}, {ts} time steps (step 0: zero load), dt {dt}, rtol {rtol:g}",
+            "mat_type": mt, "storage": {0: "aij-blocks", 1: "sbaij", 2: "aij-split", 3: "aij-vi"}[steps[-1]["storage"]],
             "newton_its": nits, "cg_its": sum(sum(s["ksp_its"]) for s in steps), "seconds": sec,
             "ms_per_newton_iter": sec / max(nits, 1) * 1e3, "dof_per_s": 3 * G ** 3 * nits / sec, "steps": steps}
 
@@ -337,6 +339,9 @@ def main():
     ap.add_argument("--config5", type=int, default=None,
                     help="grid of the config-5 leg (J2 law, non-linear Newton, 3 time steps) reported as 'config5' "
                          "(default 128 on one GPU, 0 = skip; within --budget)")
+    ap.add_argument("--bending", type=int, default=None,
+                    help="grid of the uniformly plastic leg (J2 law under -bc_type 0, BC_BENDING: the whole body "
+                         "yields; default AIJ storage and SBAIJ) reported as 'bending' (default 128 on one GPU, 0 = skip)")
     ap.add_argument("--wall", type=float, default=570.0,
                     help="wall seconds the invocation must fit: warmup steps after the first are skipped when the "
                          "timed steps would not fit (reported as warmup_run); the timed steps are never cut")
@@ -395,6 +400,19 @@ def main():
         else:
             config5 = nonlinear_leg(c5, 3, 0.01, args.rtol, local)
             log("config5 " + json.dumps(config5))
+    bending = None
+    bg = args.bending if args.bending is not None else (128 if world == 1 else 0)
+    if bg > 0 and rank == 0:
+        # BC_BENDING plasticises the whole body (src/bcs.c:61-91): every node an exception node, so
+        # the AIJ storage is the exact split (upper blocks + lower corrections); SBAIJ beside it
+        bending = {}
+        for mt in ("aij", "sbaij"):
+            if time.perf_counter() - T_START + 60 > args.budget:
+                log(f"bending leg {mt}: skipped (budget {args.budget:.0f}s)")
+                continue
+            bending[mt] = nonlinear_leg(bg, 3, 0.01, args.rtol, local,
+                                        ["-bc_type", 0] + (["-dm_mat_type", "sbaij"] if mt == "sbaij" else []))
+            log(f"bending {mt} " + json.dumps(bending[mt]))
     if rank == 0:
         cpu = None
         if world == 1 and args.cpu_grid > 0:
@@ -426,7 +444,7 @@ def main():
                        "split_slots": r["split_slots"], "split_bits": r["split_bits"],
                        "vi_values": r["vi_values"], "vi_bits": r["vi_bits"], "vi_blocks": r["vi_blocks"],
                        "spmv_rows": "fused multiply-add (-mat_vi_fma 1)" if r["storage_id"] == 3 and not r["exact"]
-                       else "multiply, add (CPU AIJ order)"},
+                       else "multiply, add (MatMult inode order)"},
             "cg_its": its,
             "ms_per_cg_iter": tm["solve_ms"] / max(its, 1),
             # CG iterations grow ~linearly with the global grid edge (720 at 64^3, 2814 at 256^3),
@@ -449,6 +467,7 @@ def main():
             "check": check,
             "variants": variants,
             "config5": config5,
+            "bending": bending,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -95,16 +95,16 @@ typedef struct {
                                   micro_mat_1's Sy, Ka: MicroPP material type 1) */
   int mat_aij_split;           /* -mat_aij_split 0|1 (1): hold the AIJ matrix exactly as upper blocks +
                                   bf16 lower corrections when all are exact (else plain AIJ blocks);
-                                  0: AIJ blocks, rows summed in the CPU AIJ order (bit-exact SpMV) */
+                                  0: AIJ blocks, rows summed in the reference's MatMult order (inode column pairs) (bit-exact SpMV) */
   int mat_aij_vi;              /* -mat_aij_vi 0|1 (1): hold the AIJ matrix exactly as one index byte per
                                   value into a dictionary of its distinct values when there are at most
-                                  256 (value-indexed AIJ; rows summed in the CPU AIJ order, bit-exact
+                                  256 (value-indexed AIJ; rows summed in the reference's MatMult order (inode column pairs), bit-exact
                                   SpMV); otherwise -mat_aij_split decides */
   int mat_vi_fma;              /* -mat_vi_fma 0|1 (1): the value-indexed SpMV's z-marching kernel sums
                                   each row with fused multiply-adds (one rounding per term, what a
                                   PETSc built with -march=native does in MatMult), rows within
-                                  1e-14 sum|a_ij x_j| of the CPU AIJ order; 0: separate multiply and
-                                  add in the CPU AIJ order (bit-exact SpMV) */
+                                  1e-14 sum|a_ij x_j| of the reference's MatMult order (inode column pairs); 0: separate multiply and
+                                  add in the reference's MatMult order (inode column pairs) (bit-exact SpMV) */
 } mcx_opts;
 
 typedef struct {

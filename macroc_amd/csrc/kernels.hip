@@ -847,7 +847,7 @@ struct InodeRows {
 // y = A x for the owned rows.  One thread = one node = 3 rows; 122 x 16-B coalesced loads of
 // the stencil blocks, x gathered from the padded box (L1/L2 resident neighbours).  Each row
 // adds its slots in ascending (nb, c) = ascending global column on one rank, in the inode
-// kernel's pairs (above), so y is bit-identical to the CPU AIJ product.  DOT: per-block p.w.
+// kernel's pairs (above), so y is bit-identical to the reference's AIJ MatMult (inode order, oracle/oracle.c row_part).  DOT: per-block p.w.
 template <int S>
 __device__ __forceinline__ void slot_acc(double v, const double (&xv)[27][3], InodeRows<false>& acc) {
   constexpr int nb = S / 9, r = (S % 9) / 3, c = S % 3;
@@ -1801,7 +1801,7 @@ __global__ void k_jacobi_vi(Geo g, const u32x4* __restrict__ I, const double* __
 // y = A x on FMT_VI, x gathered: k_spmv with the 122 16-B value pairs replaced by 16 (8) 16-B
 // index chunks and the values read from the dictionary in LDS (interior lanes of a wave share an
 // index: LDS broadcast).  Same node sweep (XCD slabs), same slot order and products as k_spmv, so
-// y is bit-identical to the CPU AIJ product.  DBG (timing-only diagnostics, wrong products):
+// y is bit-identical to the reference's AIJ MatMult (inode order, oracle/oracle.c row_part).  DBG (timing-only diagnostics, wrong products):
 // bit 0 = no dictionary lookups (the index is the value), bit 1 = no x gathers.
 template <bool DOT, bool GATED, int NIB, int DBG = 0>
 __global__ __launch_bounds__(TPB) void k_spmv_vi(Geo g, const u32x4* __restrict__ I, const double* __restrict__ dict,
@@ -2230,7 +2230,7 @@ __global__ void k_jacobi_vib_dict(const double* __restrict__ bdict, double* __re
 
 // y = A x on block-indexed FMT_VI: 2 16-B index chunks per node (27 block bytes), each block's
 // 9 values from the dictionary in LDS (4 x 16-B + 8-B reads), x gathered.  Same slot order and
-// products as k_spmv: bit-identical to the CPU AIJ product.
+// products as k_spmv: bit-identical to the reference's AIJ MatMult (inode order, oracle/oracle.c row_part).
 // EXC: exception nodes (slot + 1 in bytes 28-31) read their blocks from exc [slot][27][9].
 template <bool DOT, bool GATED, bool EXC = false>
 __global__ __launch_bounds__(TPB) void k_spmv_vib(Geo g, const u32x4* __restrict__ I,
@@ -2296,7 +2296,7 @@ __global__ __launch_bounds__(TPB) void k_spmv_vib(Geo g, const u32x4* __restrict
 // planes (rows j0-1 .. j0+TY, prefetched in registers one plane ahead) with the block dictionary
 // in LDS beside it.  The gathered kernel (k_spmv_vib) spends most of its time in the 81 8-B x
 // loads per node at a 24-B lane stride; here x comes from LDS and HBM streams 32 B of indices
-// per node.  Same slot order and products as k_spmv: bit-identical to the CPU AIJ product.
+// per node.  Same slot order and products as k_spmv: bit-identical to the reference's AIJ MatMult (inode order, oracle/oracle.c row_part).
 // FP: the CG's p update (VecAYPX) fused into the SpMV's staging of p (single rank,
 // value-indexed block storage, Jacobi from the diagonal index).  The kernel of CG iteration i
 // reads p(i-1) from pb[(i-1)&1], r and the index bytes while it marches, computes
@@ -2766,7 +2766,7 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
 // contiguous in the padded box), and while plane k is computed the registers already carry plane
 // k+2's x (coalesced 8-B loads, 1.5 x per owned node at TY = 4) and plane k+1's index chunks,
 // written to the ring after the step's barrier.  Same slot order and products as k_spmv:
-// bit-identical to the CPU AIJ product.
+// bit-identical to the reference's AIJ MatMult (inode order, oracle/oracle.c row_part).
 template <bool DOT, bool GATED, int TX, int TY, int NIB>
 __global__ __launch_bounds__(TX * TY) void k_spmv_vim(Geo g, const u32x4* __restrict__ I,
                                                       const double* __restrict__ dict, const double* __restrict__ x,

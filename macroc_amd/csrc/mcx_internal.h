@@ -68,14 +68,14 @@ struct HaloPlan {
 struct Ctx;
 
 // Matrix storage of a context.  FMT_V: AIJ stencil blocks (all 27 blocks per node, every row
-// summed in the CPU AIJ order).  FMT_U: MATSBAIJ (upper blocks, lower mirrored).  FMT_SPLIT:
+// summed in the reference's MatMult order (inode column pairs)).  FMT_U: MATSBAIJ (upper blocks, lower mirrored).  FMT_SPLIT:
 // the AIJ matrix held exactly as its upper blocks U plus, per owned node, the bf16 correction
 // lower - mirror(upper) of the correction slots that are non-zero somewhere in the matrix
 // (every AIJ value reconstructs bit for bit; rows summed in the z-marching order).
 // FMT_VI: the AIJ matrix held exactly as small indices into dictionaries of its distinct values
 // (value-indexed CSR, Kourtis et al. 2008): a nibble per value into the slot's own dictionary
 // (every slot takes at most 16 values) or a byte per value into one dictionary (at most 256),
-// all 27 blocks per node in FMT_V's slot order — every row summed in the CPU AIJ order.
+// all 27 blocks per node in FMT_V's slot order — every row summed in the reference's MatMult order (inode column pairs).
 enum Fmt { FMT_V = 0, FMT_U = 1, FMT_SPLIT = 2, FMT_VI = 3 };
 constexpr int VI_MAX = 256;     // dictionary entries (one index byte per value)
 constexpr int VI_EXC_LIST = 2048;  // staged value-indexed SpMV: exception nodes a tile defers to its block-wide pass

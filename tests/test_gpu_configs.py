@@ -57,9 +57,9 @@ def test_config3_256_cubed():
         assert res2 == res and its2 == its and np.array_equal(du2, du)
         assert (m.get_info()["spmv_tx"], m.get_info()["spmv_ty"]) == (64, 16)  # the headline instantiation
         # the same 256^3 matrix as AIJ stencil blocks (-mat_aij_vi 0 -mat_aij_split 0: every value
-        # stored, rows in the CPU AIJ order, bit-exact with the oracle at small grids): the
+        # stored, rows in the reference's MatMult order (inode column pairs), bit-exact with the oracle at small grids): the
         # value-indexed product is bit for bit the same
-        # (-mat_vi_fma 0: the value-indexed rows in the CPU AIJ order; the default fused
+        # (-mat_vi_fma 0: the value-indexed rows in the reference's MatMult order (inode column pairs); the default fused
         # multiply-adds differ from them by rounding only)
         m.set_option("vi_fma", 0)
         Ax_exact = m.spmv(x)

@@ -67,14 +67,14 @@ def newton_step(x_global_nat, options=()):
 
 @pytest.mark.parametrize("name", ["g1088_r2", "g888_r8", "g522_r3", "g534_r8"])
 def test_multirank_newton_step(name):
-    """AIJ blocks in the CPU AIJ order (-mat_aij_split 0): SpMV bit-exact on any rank grid."""
+    """AIJ blocks in the reference's MatMult order (inode column pairs) (-mat_aij_split 0): SpMV bit-exact on any rank grid."""
     _multirank(name, sbaij=False, extra=["-mat_aij_vi", 0, "-mat_aij_split", 0])
 
 
 @pytest.mark.parametrize("name", ["g1088_r2", "g888_r8", "g522_r3", "g534_r8"])
 def test_multirank_aij_vi(name):
     """Default AIJ storage for the elastic law: value-indexed (one byte per value + a per-rank
-    dictionary), rows in the CPU AIJ order: matrix and SpMV bit-exact on any rank grid."""
+    dictionary), rows in the reference's MatMult order (inode column pairs): matrix and SpMV bit-exact on any rank grid."""
     _multirank(name, sbaij=False, vi=True)
 
 

@@ -35,7 +35,7 @@ def du_tol(rtol):
 
 @pytest.mark.parametrize("name", SINGLE)
 def test_newton_step_single_rank(name):
-    """-mat_aij_split 0: AIJ stencil blocks, every row summed in the CPU AIJ order."""
+    """-mat_aij_split 0: AIJ stencil blocks, every row summed in the reference's MatMult order (inode column pairs)."""
     fx = load(name)
     NX, NY, NZ = (int(v) for v in fx["grid"])
     rtol = float(fx["rtol"])
@@ -226,7 +226,7 @@ def test_aij_vi_exception_nodes(grid, stage, vi_tx, tile):
     """A per-GP-tangent law (J2) with a few plastic Gauss points stays value-indexed: the nodes
     touching an element with a non-elastic tangent keep their 27 blocks as plain values
     (exception nodes), every other node indexes the elastic blocks' dictionary.  Matrix values
-    bit-exact with the oracle's AIJ; the SpMV bit-exact with the CPU AIJ product under
+    bit-exact with the oracle's AIJ; the SpMV bit-exact with the CPU AIJ product (inode order) under
     -mat_vi_fma 0 (gathered kernel, and the 64x16 / 128x8 / 256x4 staged tiles), within
     1e-14 sum|a||x| with the fused multiply-adds; the solve within the north-star bar."""
     NX, NY, NZ = grid
@@ -620,7 +620,7 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
     """The headline kernel at the tile shapes it runs (k_spmv_vibm 64x16, the default, and the
     selectable 128x8 / 256x4), with partial tiles in x (260 = 4 x 64 + 4 = 256 + 4, 130,
     70) and y (6, 9, 20 rows against 16 / 8 / 4): matrix dump bit-exact, and the SpMV bit-exact with the
-    oracle's CPU AIJ (MatMult_SeqAIJ order, the MATAIJ matrix of src/init.c:92 applied by
+    oracle's CPU AIJ (MatMult_SeqAIJ_Inode order, the MATAIJ matrix of src/init.c:92 applied by
     KSPSolve, src/assembly.c:179-192) under -mat_vi_fma 0 for several z-chunkings and wave
     layouts; the default fused multiply-add rows within 1e-14 sum|a||x|; the solve within the
     north-star bar."""
@@ -644,7 +644,7 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
         absrow = np.add.reduceat(np.abs(v) * np.abs(x[ci]), rp[:-1])
         for zblocks in (0, 1, 2, 3 * NZ):  # chunks of 1, NZ, NZ/2, ... planes per tile
             m.set_option("spmv_zblocks", zblocks)
-            # -mat_vi_fma 0: the CPU AIJ order, bit-exact (scalar-dictionary 16x4 patches, row
+            # -mat_vi_fma 0: the reference's MatMult order (inode column pairs), bit-exact (scalar-dictionary 16x4 patches, row
             # quarters, every block from LDS); the default fused multiply-adds: within rounding
             for uni, patch in ((1, 1), (1, 0), (0, 0)):
                 m.set_option("vi_fma", 0)
