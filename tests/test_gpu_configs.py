@@ -107,6 +107,42 @@ def test_config5_nonlinear_128(capfd):
         assert 0 < counts[1] < counts[2], counts
 
 
+def test_config5_law_32cubed_vs_oracle():
+    """Config 5's path (J2 law, default AIJ storage with exception nodes) against the oracle at
+    32^3 (the one-rank oracle's naive 4-nest assembly is single-threaded: ~40 s here): the state after time step 1's first
+    solved Newton iteration (Gauss points under the load on the plastic branch), then its second
+    Newton iteration: residual and matrix bit-exact, the exception nodes present, the staged SpMV
+    bit-exact under -mat_vi_fma 0 (inode order), and the solve within 50 rtol of the oracle's
+    with the default FMA rows."""
+    from oracle import oracle as O
+
+    N, rtol = 32, 1e-10
+    P = O.Problem(N, N, N, rtol=rtol, law=1, dt=0.01)
+    P.apply_bc_u(P.get_displacement(1))
+    P.set_strains(); P.homogenize(); P.assembly_res(); P.assembly_jac(); P.solve(); P.update_u()
+    u = P.u()
+    P.set_strains(); P.homogenize(); P.assembly_res(); P.assembly_jac()
+    assert P.nonlinear_gps()[0] > 0
+    x = np.random.default_rng(9).uniform(-1, 1, P.ndofs)
+    y_ref = P.spmv(x)
+    ref_its = P.solve()["its"]
+    argv = ["-da_grid_x", N, "-da_grid_y", N, "-da_grid_z", N, "-dt", 0.01, "-mat_law", "plastic",
+            "-ksp_rtol", repr(rtol)]
+    with M.Macroc(argv) as m:
+        m.set_u(u)
+        m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
+        info = m.get_info()
+        assert info["storage"] == 3 and info["vi_exc_nodes"] > 0, info
+        assert np.array_equal(m.b(), P.b())
+        assert np.array_equal(m.dump_csr()[2], P.A_values())
+        m.set_option("vi_fma", 0)
+        assert np.array_equal(m.spmv(x), y_ref)
+        m.set_option("vi_fma", 1)
+        its, rn, reason = m.solve_Ax()
+        assert reason == 2 and abs(its - ref_its) <= 1, (its, ref_its)
+        assert np.linalg.norm(m.du() - P.du()) <= 50 * rtol * np.linalg.norm(P.du())
+
+
 def test_config4_512_cubed_2x2x2_in_process():
     """BASELINE config 4's workload (512^3, -da_processors_x 2 -y 2 -z 2: 256^3 nodes per
     subdomain; tests/CMakeLists.txt:26-28, src/init.c:85-93) on ONE MI355X: the eight subdomain
