@@ -78,6 +78,16 @@ def rank_grid(n):
     return {1: (1, 1, 1), 2: (2, 1, 1), 4: (2, 2, 1), 8: (2, 2, 2), 16: (4, 2, 2)}.get(n) or (n, 1, 1)
 
 
+def pmc_commit(mat_type, NX, NY, NZ):
+    """The commit the committed PMC traffic passes of this kernel were measured at (or None)."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_spmv.json")
+    try:
+        with open(path) as f:
+            return (json.load(f).get(f"{mat_type}:{NX}x{NY}x{NZ}") or {}).get("commit")
+    except (OSError, ValueError):
+        return None
+
+
 def pmc_traffic(mat_type, NX, NY, NZ):
     """HBM bytes per SpMV launch from the committed rocprofv3 PMC passes (profiles/pmc_spmv.json:
     (FETCH_SIZE*2 [gfx950 wide-read correction] + WRITE_SIZE) * 1024 per launch, same kernel and
@@ -112,7 +122,7 @@ def lds_limiter(mat_type, NX, NY, NZ):
                "valu_insts_per_wave_plane": e["valu_insts_per_wave_plane"],
                "lds_insts_per_wave_plane": e["lds_insts_per_wave_plane"],
                "source": "profiles/pmc_vibm.json (committed SQ counter passes, not measured by this run)",
-               "measured": e.get("measured")}
+               "measured": e.get("measured"), "measured_at_commit": e.get("commit")}
         return out
     except (OSError, ValueError, KeyError):
         return None
@@ -455,6 +465,8 @@ def main():
             "device_gb": info["device_bytes"] / 1e9,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                          "frac": achieved / PEAK_HBM_GBS, "traffic": pmc_traffic(r["storage"], NX, NY, NZ),
+                         "traffic_source": "profiles/pmc_spmv.json (committed PMC passes, tools/pmc_spmv.sh)",
+                         "traffic_measured_at_commit": pmc_commit(r["storage"], NX, NY, NZ),
                          "kernel": kernel_name(r), "bytes_per_launch": spmv_bytes,
                          "avg_launch_ms": spmv_avg_ms, "launches_timed": tm["spmv_launches"],
                          # what the reference's MatMult must stream for the same product (PETSc AIJ

@@ -56,7 +56,8 @@ except (OSError, ValueError):
 d[f"{mat}:{grid}x{grid}x{grid}"] = {"hbm_bytes_per_launch": hbm, "fetch_kb_median": fk, "write_kb_median": wk,
                                      "launches": len(f_real), "kernels": kern,
                                      "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes, "
-                                               "--kernel-include-regex, bench.py --steps 1 --warmup 0"}
+                                               "--kernel-include-regex, bench.py --steps 1 --warmup 0",
+                                     "commit": os.environ.get("MCX_COMMIT")}
 with open(path, "w") as f:
     json.dump(d, f, indent=1, sort_keys=True)
 with open(os.path.join(out, "summary.txt"), "w") as f:

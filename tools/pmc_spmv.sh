@@ -17,7 +17,7 @@ OUT=gpurun_out/pmc/$MAT-$G
 mkdir -p $OUT
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 400 rocprofv3 --pmc $C --kernel-include-regex "$RE" -d $OUT/$C -o run --output-format csv -- \
-    python3 bench.py --steps 1 --warmup 0 --grid $G --mat-type $BM --variants '' --cpu-sample 0 --no-check \
+    python3 bench.py --steps 1 --warmup 0 --grid $G --mat-type $BM --variants '' --cpu-grid 0 --config5 0 --bending 0 --no-check \
     > $OUT/$C.log 2>&1
 done
 python3 tools/pmc_parse.py $MAT $G $OUT

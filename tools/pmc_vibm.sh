@@ -35,7 +35,7 @@ with open(OUT + "/summary.txt", "w") as f:
 busy_se, lds_cu = c["SQ_BUSY_CYCLES"] / 32, c["SQ_LDS_IDX_ACTIVE"] / 256
 waves, planes = c["SQ_WAVES"], 64
 d = {"aij-vi:256x256x256": {
-    "kernel": "k_spmv_vibm 256x4 (" + VAR + ")",
+    "kernel": "k_spmv_vibm 64x16 (" + VAR + ")", "commit": os.environ.get("MCX_COMMIT"),
     "method": "rocprofv3 --pmc, two passes of 8 SQ counters, kernel trace only, tools/spmv_ab.py --grid 256 "
               "--iters 5 (tools/pmc_vibm.sh)",
     "counters_per_launch": c, "sq_busy_cycles_per_se": busy_se, "lds_active_cycles_per_cu": lds_cu,
