@@ -1445,6 +1445,14 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.vi_exc_list = (int)value;
     return 0;
   }
+  if (!std::strcmp(name, "vi_mpass")) {
+    if (value < 1. || value > 8. || (double)(int)value != value) {
+      set_error("vi_mpass: 1 .. 8");
+      return 1;
+    }
+    c.vi_mpass = (int)value;
+    return 0;
+  }
   if (!std::strcmp(name, "vi_wmap")) {
     c.vi_wmap = value != 0.;
     return 0;

@@ -1008,6 +1008,7 @@ struct ZTiling {
   int dbg = 0;            // timing-only diagnostics (k_spmv_vibm: 1 = every wave takes the scalar path)
   int wmap = 1;           // k_spmv_vibm PATCH: 1 = patches on SIMDs as a Latin square, 0 = row-major (A/B)
   int xlist = VI_EXC_LIST;  // k_spmv_vibm EXC: exception nodes a tile defers (option vi_exc_list; the rest in their plane)
+  int mpass = 1;          // k_spmv_vibm UNI: scalar passes per wave and plane (option vi_mpass; 1 = whole uniform waves only)
 };
 
 static ZTiling z_tiling(const Geo& g, int ztx, int zty, int want) {
@@ -2503,33 +2504,34 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
     // the dictionary in global memory, scalar cache) and multiplies them as SGPR operands: the
     // dictionary's 486 LDS cycles per wave and plane leave the LDS, which then only serves the x
     // ring.  Other waves read the dictionary from LDS.  Same values, same products, same order.
+    // Round 4 (zt.mpass > 1): a wave with a few distinct id vectors (a tile's x-face patch at the
+    // domain boundary: interior lanes and boundary-column lanes) runs the scalar path once per
+    // vector, each pass under the exec mask of the lanes holding it (the first remaining lane's
+    // vector; at most mpass passes), so those waves no longer read the dictionary from LDS in 27
+    // dependent rounds.  Every lane runs exactly one pass or the LDS path: the same products in
+    // the same order.  mpass 1: round 3's rule (one pass, only when all 64 lanes agree).
     unsigned sw[7] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    bool uni = false;
+    bool rest = inxy;  // this lane still needs its row after the scalar passes
     if (UNI) {
-#pragma unroll
-      for (int q = 0; q < 7; q++) sw[q] = __builtin_amdgcn_readfirstlane(q < 4 ? c0[q] : c1[q - 4]);
-      unsigned diff = 0u;
-#pragma unroll
-      for (int q = 0; q < 7; q++) diff |= (q < 4 ? c0[q] : c1[q - 4]) ^ sw[q];
+      const unsigned wd[7] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2]};
+      const unsigned long long all = __ballot(inxy);
       // exact rows (!FMA): the scalar path's fixed inode pairing needs every neighbour present
-      uni = __all(inxy && diff == 0u && (!EXC || c1[3] == 0u) &&
-                  (FMA || present_mask(g, i, j, k) == PRES_ALL)) || (zt.dbg & 1);
-    }
-    // EXC: the wave's exception lanes of this plane take the next positions of its segment in
-    // lane order (ballot + mbcnt, converged here); those beyond the capacity stay in the plane
-    bool deferred = false;
-    if constexpr (EXC) {
-      const bool xh = !(UNI && uni) && inxy && c1[3] != 0u;
-      const unsigned long long xm = __ballot(xh);
-      if (xm) {  // uniform
-        const int pos = wn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(xm >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((unsigned)xm, 0u));
-        deferred = xh && pos < wcap;
-        if (deferred) s_xl[wv * SEG + pos] = (k - k0) * T + me;
-        wn = min(wcap, wn + (int)__popcll(xm));
-      }
-    }
-    if (UNI && uni) {  // (every lane is inxy)
+      unsigned long long left = __ballot(inxy && (!EXC || c1[3] == 0u) && (FMA || present_mask(g, i, j, k) == PRES_ALL));
+      if (zt.dbg & 1) left = all;  // timing-only diagnostics: every wave takes the first lane's blocks
+      for (int ps = 0; ps < zt.mpass && left; ps++) {  // uniform
+        const int lead = (int)__builtin_ctzll(left);
+        unsigned diff = 0u;
+#pragma unroll
+        for (int q = 0; q < 7; q++) {
+          sw[q] = __builtin_amdgcn_readlane(wd[q], lead);
+          diff |= wd[q] ^ sw[q];
+        }
+        const bool mine = ((left >> ln) & 1ull) && (diff == 0u || (zt.dbg & 1));
+        const unsigned long long mm = __ballot(mine);
+        if (zt.mpass == 1 && mm != all) break;  // round 3: whole waves only
+        left &= ~mm;
+        if (mine) rest = false;
+        if (!mine) continue;
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
       InodeRows<true> acc;  // !FMA: the inode pairs of a node whose 27 neighbours are present
       typedef const volatile __attribute__((address_space(3))) double lds_vdouble;
@@ -2587,9 +2589,27 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       __builtin_nontemporal_store(y1, &y[3 * n + 1]);
       __builtin_nontemporal_store(y2, &y[3 * n + 2]);
       if (DOT) dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
+      }
+    }
+    // EXC: the wave's exception lanes of this plane take the next positions of its segment in
+    // lane order (ballot + mbcnt, converged here); those beyond the capacity stay in the plane
+    bool deferred = false;
+    if constexpr (EXC) {
+      const bool xh = rest && c1[3] != 0u;
+      const unsigned long long xm = __ballot(xh);
+      if (xm) {  // uniform
+        const int pos = wn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(xm >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((unsigned)xm, 0u));
+        deferred = xh && pos < wcap;
+        if (deferred) s_xl[wv * SEG + pos] = (k - k0) * T + me;
+        wn = min(wcap, wn + (int)__popcll(xm));
+      }
+    }
+    if (!rest) {
+      // computed by a scalar pass
     } else if (EXC && deferred) {
       // deferred to the block's exception pass below
-    } else if (EXC && inxy && c1[3]) {
+    } else if (EXC && c1[3]) {
       // an exception node (EXC instantiations only) that found the tile's list full: its 27
       // plain blocks from exc [slot][27][9], a rolled loop of its own so the indexed path below
       // keeps its registers; same order and products as the indexed rows
@@ -2629,7 +2649,7 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       __builtin_nontemporal_store(y1, &y[3 * n + 1]);
       __builtin_nontemporal_store(y2, &y[3 * n + 2]);
       if (DOT) dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
-    } else if (inxy) {
+    } else {
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
       InodeRows<false> acc;
       if constexpr (!FMA) acc.pres = present_mask(g, i, j, k);
@@ -4235,6 +4255,7 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
       zt.dbg = c.split_dbg;
       zt.wmap = c.vi_wmap;
       zt.xlist = c.vi_exc_list;
+      zt.mpass = c.vi_mpass;
       int tx, ty;
       vis_shape(c, tx, ty);
 #define MCX_VIBM(TXV, TYV, XVV, UV, PV, ...)                                                                          \

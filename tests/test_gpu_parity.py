@@ -258,7 +258,9 @@ def test_aij_vi_exception_nodes(grid, stage, vi_tx, tile):
         # their plane (list size 0), or both (a list of 3 that overflows): the same rows
         for xl in (0, 3, 2048):
             m.set_option("vi_exc_list", xl)
-            assert np.array_equal(m.spmv(x), y1), xl
+            for mp in (1, 4):  # scalar passes per distinct id vector of a wave: the same rows
+                m.set_option("vi_mpass", mp)
+                assert np.array_equal(m.spmv(x), y1), (xl, mp)
         m.set_option("vi_fma", 1)
         y = m.spmv(x)
         assert np.all(np.abs(y - y1) <= 1e-14 * absrow + 1e-300)
@@ -651,10 +653,20 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
                 m.set_option("vi_uni", uni)
                 m.set_option("vi_patch", patch)
                 assert np.array_equal(m.spmv(x), y_ref), (zblocks, uni, patch)
+            # scalar passes per distinct id vector of a wave (vi_mpass): the same rows, bit for bit
+            m.set_option("vi_uni", 1)
+            m.set_option("vi_patch", 1)
+            for mp in (1, 2, 8):
+                m.set_option("vi_mpass", mp)
+                assert np.array_equal(m.spmv(x), y_ref), (zblocks, mp)
             m.set_option("vi_fma", 1)
             yf = m.spmv(x)
             assert np.all(np.abs(yf - y_ref) <= 1e-14 * absrow + 1e-300), zblocks
             assert np.array_equal(m.spmv(x), yf)
+            for mp in (1, 2, 8):
+                m.set_option("vi_mpass", mp)
+                assert np.array_equal(m.spmv(x), yf), (zblocks, mp)
+            m.set_option("vi_mpass", 4)
         m.set_option("spmv_zblocks", 1)  # every tile marches all planes: the prefetch ring end to end
         assert m.get_info()["spmv_kc"] == NZ
         its, rn, reason = m.solve_Ax()
