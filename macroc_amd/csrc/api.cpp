@@ -55,7 +55,7 @@ static int free_ctx(Ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
   void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
-                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2, c->xdone, c->elem_plain, c->cref, c->vi_xslot,
+                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2, c->p_pad3, c->p_pad4, c->xdone, c->elem_plain, c->cref, c->vi_xslot,
                   c->vi_xlist, c->vi_exc,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf, c->halo.d_bnd};
@@ -202,6 +202,12 @@ static int cg_solve(Ctx& c, int* its, double* rnorm, int* reason) {
   launch_jacobi(c);  // PCSetUp_Jacobi happens inside KSPSolve in the reference
   c.fusep_used = false;  // set by cg_iteration when the p update runs inside the SpMV
   c.pdb_used = cg_pdb(c);
+  c.pqb_used = c.pdb_used && c.cg_pdb == 4;
+  if (c.pqb_used && !c.p_pad3) {  // the quad-buffered p update's third and fourth buffers
+    const int64_t npad = (int64_t)c.g.PX * c.g.PY * c.g.PZ * 3;
+    int rc = 0;
+    if ((rc = dalloc(c, &c.p_pad3, npad)) || (rc = dalloc(c, &c.p_pad4, npad))) return rc;
+  }
   if (c.pdb_used) MCX_HIP(hipMemsetAsync(c.xdone, 0, sizeof(int), c.stream));
   CgState s{};
   s.rtol = c.o.ksp_rtol;
@@ -1425,8 +1431,12 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.vi_block_on = value != 0.;
     return 0;
   }
-  if (!std::strcmp(name, "cg_pdb")) {
-    c.cg_pdb = value != 0.;
+  if (!std::strcmp(name, "cg_pdb")) {  // 0 | 1 (two p buffers) | 4 (four)
+    if (!(value == 0. || value == 1. || value == 2. || value == 4.)) {
+      set_error("cg_pdb: 0, 1 (two p buffers) or 4 (four)");
+      return 1;
+    }
+    c.cg_pdb = value == 4. ? 4 : (value != 0.);
     return 0;
   }
   if (!std::strcmp(name, "cg_rev")) {

@@ -3192,6 +3192,89 @@ __global__ void k_cg_pupdate_db(Geo g, const double* __restrict__ z, const doubl
   pupdate_node_db<NT, DIX>(g, n, z, dinv, jix, pb0, pb1, x, cg);
 }
 
+// PQB (option cg_pdb 4): p in four buffers, p(i) in pq[i & 3], and VecAXPY(x) on every fourth
+// iteration only: at i = 4m (m >= 1) the four owed terms in PETSc's order,
+// x = (((x + a(i-4) p(i-4)) + a(i-3) p(i-3)) + a(i-2) p(i-2)) + a(i-1) p(i-1), p(i-4) read from
+// p(i)'s buffer before it is overwritten, the alphas from CgState::ah.  x then costs
+// (48 + 3 x 24) / 4 = 30 B per node and iteration instead of PDB's 36.  xdone = the last such i;
+// k_cg_xfinal_qb applies the (at most four) terms still owed.
+// PAR: 1 = an iteration >= 1 without the x terms, 2 = one with them (i = 4m >= 4), 0 = from cg->i
+struct PQ {
+  double* p[4];
+};
+template <bool NT, bool DIX, bool SKIP_SENT = false, int PAR = 0>
+__global__ void k_cg_pupdate_qb(Geo g, const double* __restrict__ z, const double* __restrict__ dinv,
+                                const unsigned char* __restrict__ jix, PQ pq, double* __restrict__ x,
+                                const CgState* __restrict__ cg, int* __restrict__ xdone,
+                                const int* __restrict__ list, int64_t cnt, int rev = 0) {
+  if (cg->reason) return;
+  const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  const int it = cg->i;
+  const bool dox = it >= 4 && (it & 3) == 0;
+  if (t == 0 && dox) *xdone = it;
+  if (t >= cnt) return;
+  const int n = list ? list[t] : (int)(rev ? cnt - 1 - t : t);
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  if (SKIP_SENT && sent_node(g, i, j, k)) return;
+  const int pc = pad_of(g, i, j, k);
+  double* pn = pq.p[it & 3];
+  if (it == 0) {
+#pragma unroll
+    for (int d = 0; d < 3; d++) st<NT>(&pn[3 * pc + d], z_of<DIX>(z, dinv, jix, n, d));
+    return;
+  }
+  // the host's parity guess must match the device's count, else the generic path below
+  const bool par_ok = PAR == 0 || (PAR == 2) == dox;
+  const double* po = pq.p[(it - 1) & 3];
+  const double bc = cg->bcoef;
+  double pv[3], zv[3];
+  if ((PAR == 2 && par_ok) || (PAR == 0 && dox)) {
+    const double* p3 = pq.p[(it - 3) & 3];
+    const double* p2 = pq.p[(it - 2) & 3];
+    const double a4 = cg->ah[(it - 4) & 3], a3 = cg->ah[(it - 3) & 3], a2 = cg->ah[(it - 2) & 3],
+                 a1 = cg->ah[(it - 1) & 3];
+    double xv[3], q4[3], q3[3], q2[3];
+#pragma unroll
+    for (int d = 0; d < 3; d++) {  // every load before any store
+      pv[d] = po[3 * pc + d];
+      zv[d] = z_of<DIX>(z, dinv, jix, n, d);
+      xv[d] = x[3 * n + d];
+      q4[d] = pn[3 * pc + d];
+      q3[d] = p3[3 * pc + d];
+      q2[d] = p2[3 * pc + d];
+    }
+#pragma unroll
+    for (int d = 0; d < 3; d++) st<NT>(&x[3 * n + d], (((xv[d] + a4 * q4[d]) + a3 * q3[d]) + a2 * q2[d]) + a1 * pv[d]);
+  } else {
+#pragma unroll
+    for (int d = 0; d < 3; d++) {
+      pv[d] = po[3 * pc + d];
+      zv[d] = z_of<DIX>(z, dinv, jix, n, d);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < 3; d++) st<NT>(&pn[3 * pc + d], zv[d] + bc * pv[d]);
+}
+
+// PQB: the terms j = xdone .. xp still owed after the loop (at most four), in order
+__global__ void k_cg_xfinal_qb(Geo g, PQ pq, double* __restrict__ x, const CgState* __restrict__ cg,
+                               const int* __restrict__ xdone) {
+  const int xd = *xdone, xp = cg->xp;
+  if (xp < xd) return;
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  const int pc = pad_of(g, i, j, k);
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    double xv = x[3 * n + d];
+    for (int jj = xd; jj <= xp; jj++) xv = xv + cg->ah[jj & 3] * pq.p[jj & 3][3 * pc + d];
+    x[3 * n + d] = xv;
+  }
+}
+
 // SKIP_SENT: the sent nodes were updated before the halo exchange (k_cg_pupdate_list)
 template <bool NT, bool DIX, bool SKIP_SENT = false>
 __global__ void k_cg_pupdate(Geo g, const double* __restrict__ z, const double* __restrict__ dinv,
@@ -3490,6 +3573,7 @@ __device__ void cg_logic_alpha(CgState* s, double dpi) {
   }
   s->alpha_prev = s->alpha;
   s->alpha = s->beta / dpi;
+  s->ah[s->i & 3] = s->alpha;
   s->xpend = 1;
   s->xp = s->i;
 }
@@ -4498,7 +4582,14 @@ int cg_finish_init(Ctx& c) {
   return reduce_and_logic(c, 2, nb, RED_INIT, false, c.partials, c.cg);
 }
 
+static PQ pq_of(const Ctx& c) { return PQ{{c.p_pad, c.p_pad2, c.p_pad3, c.p_pad4}}; }
+
 void launch_cg_xfinal(Ctx& c) {
+  if (c.pqb_used) {
+    hipLaunchKernelGGL(k_cg_xfinal_qb, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, pq_of(c), c.du, c.cg,
+                       c.xdone);
+    return;
+  }
   hipLaunchKernelGGL(k_cg_xfinal, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.p_pad,
                      c.fusep_used || c.pdb_used ? c.p_pad2 : nullptr, c.du, c.cg, c.pdb_used ? c.xdone : nullptr);
 }
@@ -4531,6 +4622,32 @@ void launch_cg_pupdate(Ctx& c, int part) {
   const bool dix = cg_dix(c);
   const double* zs = dix ? c.r : c.z;
   const double* jd = dix ? c.jdd : c.dinv;
+  if (c.pqb_used) {  // p in four buffers, x every fourth iteration
+    const int par = c.cg_par && c.cg_it >= 1 ? 1 + (c.cg_it >= 4 && (c.cg_it & 3) == 0) : 0;
+    const PQ pq = pq_of(c);
+#define MCX_PQB_PAR(SKIPV, GRID, LIST, CNT)                                                                          \
+  MCX_NT_DIX(c.cg_nt, dix, {                                                                                         \
+    if (par == 1)                                                                                                    \
+      hipLaunchKernelGGL((k_cg_pupdate_qb<NT, DX, SKIPV, 1>), dim3(GRID), dim3(TPB), 0, c.stream, c.g, zs, jd, c.jix, \
+                         pq, c.du, c.cg, c.xdone, LIST, CNT, c.cg_rev);                                              \
+    else if (par == 2)                                                                                               \
+      hipLaunchKernelGGL((k_cg_pupdate_qb<NT, DX, SKIPV, 2>), dim3(GRID), dim3(TPB), 0, c.stream, c.g, zs, jd, c.jix, \
+                         pq, c.du, c.cg, c.xdone, LIST, CNT, c.cg_rev);                                              \
+    else                                                                                                             \
+      hipLaunchKernelGGL((k_cg_pupdate_qb<NT, DX, SKIPV, 0>), dim3(GRID), dim3(TPB), 0, c.stream, c.g, zs, jd, c.jix, \
+                         pq, c.du, c.cg, c.xdone, LIST, CNT, c.cg_rev);                                              \
+  })
+    if (part == 1) {
+      if (!c.halo.nbnd) return;
+      MCX_PQB_PAR(false, nblk(c.halo.nbnd), c.halo.d_bnd, c.halo.nbnd);
+    } else if (part == 2) {
+      MCX_PQB_PAR(true, nbn, nullptr, (int64_t)c.g.nown);
+    } else {
+      MCX_PQB_PAR(false, nbn, nullptr, (int64_t)c.g.nown);
+    }
+#undef MCX_PQB_PAR
+    return;
+  }
   if (c.pdb_used) {  // p double-buffered, x every second iteration
     // cg_par: the kernel of the iteration's parity (the host's count; the kernel checks it)
     const int par = c.cg_par && c.cg_it >= 2 ? 1 + (c.cg_it & 1) : 0;
@@ -4616,7 +4733,7 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) 
   }
   // p of this iteration (PDB: buffer it & 1, `it` = the host's count of launched iterations, which
   // is the device's cg->i for every iteration that runs; the fused small-grid path fb has one buffer)
-  double* pcur = c.pdb_used && (c.cg_it & 1) ? c.p_pad2 : c.p_pad;
+  double* pcur = c.pqb_used ? pq_of(c).p[c.cg_it & 3] : (c.pdb_used && (c.cg_it & 1) ? c.p_pad2 : c.p_pad);
   if (fb && !first) {
     MCX_NT_DIX(c.cg_nt, dix,
                hipLaunchKernelGGL((k_cg_pupdate_fb<NT, DX>), dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, zs, jd,

@@ -45,6 +45,7 @@ struct CgState {
   int xpend;  // x += alpha p of the last iteration not yet applied (k_cg_pupdate / k_cg_xfinal apply it)
   int xp;     // the last iteration whose alpha step succeeded (-1: none); the fused path's pending x update
   double alpha_prev;  // alpha of the iteration before (the fused path's every-second-iteration x update)
+  double ah[4];       // alpha of iteration j at ah[j & 3] (quad-buffered p: x every fourth iteration)
 };
 
 struct Material {
@@ -135,10 +136,14 @@ struct Ctx {
   double* u_pad = nullptr;   // displacement, padded ghosted box [PX*PY*PZ][3]
   double* p_pad = nullptr;   // CG search direction, padded
   double* p_pad2 = nullptr;  // its second buffer (single rank: the p update fused into the SpMV, cg_fusep)
+  double* p_pad3 = nullptr;  // third and fourth buffers (cg_pdb 4), allocated at the first solve that uses them
+  double* p_pad4 = nullptr;
   int cg_fusep = 0;          // option cg_fusep: fuse the CG p update into the value-indexed SpMV (single rank; A/B: no gain)
   bool fusep_used = false;   // the last solve ran the fused kernel (timing: its bytes per launch)
-  int cg_pdb = 1;            // option cg_pdb: p double-buffered (p_pad / p_pad2), VecAXPY(x) every second iteration
+  int cg_pdb = 1;            // option cg_pdb: 1 = p double-buffered (p_pad / p_pad2), VecAXPY(x) every second
+                             // iteration; 4 = four buffers, x every fourth iteration; 0 = one buffer, x every iteration
   bool pdb_used = false;     // the current solve runs the double-buffered p update
+  bool pqb_used = false;     // ... the quad-buffered one (cg_pdb 4; pdb_used too)
   int cg_rev = 1;            // option cg_rev: PDB p update from the last node down (the update kernel's last r writes hit the Infinity Cache)
   int cg_par = 1;            // option cg_par: PDB p update specialised per iteration parity (host count cg_it)
   int* xdone = nullptr;      // PDB: the last odd iteration whose p update applied the x terms owed

@@ -245,9 +245,11 @@ def test_cg_pdb_multirank_bitwise(grid, procs):
     on = run_group(argv, px * py * pz, newton_step(x, [("cg_pdb", 1), ("cg_par", 0)]))
     par = run_group(argv, px * py * pz, newton_step(x, [("cg_pdb", 1), ("cg_par", 1)]))
     off = run_group(argv, px * py * pz, newton_step(x, [("cg_pdb", 0)]))
-    for a, b, c in zip(on, off, par):
+    quad = run_group(argv, px * py * pz, newton_step(x, [("cg_pdb", 4), ("cg_par", 1)]))
+    for a, b, c, q in zip(on, off, par, quad):
         assert a["its"] == b["its"] and a["reason"] == b["reason"] and np.array_equal(a["du"], b["du"])
         assert c["its"] == b["its"] and c["reason"] == b["reason"] and np.array_equal(c["du"], b["du"])
+        assert q["its"] == b["its"] and q["reason"] == b["reason"] and np.array_equal(q["du"], b["du"])
 
 
 def test_rccl_transport_one_rank():

@@ -676,14 +676,14 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
 
 
 
-@pytest.mark.parametrize("maxits", [None, 37, 38, 1, 2])
+@pytest.mark.parametrize("maxits", [None, 37, 38, 39, 40, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("storage", ["vi", "vi_staged", "split"])
 def test_cg_pdb_bitwise(maxits, storage):
-    """Option cg_pdb (default): p double-buffered and VecAXPY(x) applied on odd iterations only,
-    both owed terms in PETSc's order, the rest by k_cg_xfinal — bitwise the solve of the
-    single-buffer p update: converged, and stopped by maxits after odd and even iteration
-    counts (1 and 2 included); with and without the parity-specialised kernels (cg_par) and the
-    reversed node order of the p update (cg_rev)."""
+    """Option cg_pdb 1 (default): p double-buffered and VecAXPY(x) applied on odd iterations only,
+    both owed terms in PETSc's order, the rest by k_cg_xfinal; cg_pdb 4: four buffers, the four
+    owed terms every fourth iteration — bitwise the solve of the single-buffer p update:
+    converged, and stopped by maxits at every residue mod 4 (1 to 5 included); with and without
+    the parity-specialised kernels (cg_par) and the reversed node order (cg_rev)."""
     NX, NY, NZ = 70, 20, 12
     extra = ["-mat_aij_vi", 0] if storage == "split" else []
     argv = argv_for(NX, NY, NZ, 1e-12, extra) + (["-ksp_max_it", maxits] if maxits else [])
@@ -694,7 +694,8 @@ def test_cg_pdb_bitwise(maxits, storage):
             m.set_option("vi_stage", 1)
         m.apply_bc_on_u(m.get_displacement(1))
         m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
-        for pdb, par, rev in ((0, 0, 0), (1, 0, 0), (0, 1, 0), (1, 1, 0), (1, 1, 1), (1, 0, 1)):
+        for pdb, par, rev in ((0, 0, 0), (1, 0, 0), (0, 1, 0), (1, 1, 0), (1, 1, 1), (1, 0, 1), (4, 0, 0), (4, 1, 0),
+                              (4, 1, 1)):
             m.set_option("cg_pdb", pdb)
             m.set_option("cg_par", par)
             m.set_option("cg_rev", rev)
