@@ -144,6 +144,8 @@ typedef struct {
   int64_t vi_exc_nodes;         /* value-indexed AIJ, block mode: owned nodes whose 27 blocks are stored as
                                    plain values (a per-GP-tangent law: the nodes touching an element whose
                                    tangent differs from the law's reference tangent) */
+  int64_t split_escapes;        /* AIJ-split with dense bf16 corrections: corrections not exact in bf16, kept as
+                                   their bf16 hi plus an exact double residual (0 otherwise) */
 } mcx_info;
 
 typedef struct {

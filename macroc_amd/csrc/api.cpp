@@ -7,6 +7,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <unordered_map>
+#include <vector>
 
 #include "mcx_internal.h"
 
@@ -55,7 +57,7 @@ static int free_ctx(Ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
   void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
-                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2, c->p_pad3, c->p_pad4, c->xdone, c->elem_plain, c->cref, c->vi_xslot,
+                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2, c->p_pad3, c->p_pad4, c->xdone, c->esc_node, c->esc_res, c->esc_slot, c->elem_plain, c->cref, c->vi_xslot,
                   c->vi_xlist, c->vi_exc,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf, c->halo.d_bnd};
@@ -513,6 +515,7 @@ static void fill_info(const Ctx& c, mcx_info* in) {
   in->vi_bits = c.fmt == FMT_VI ? c.vi_bits : 0;
   in->vi_blocks = c.fmt == FMT_VI && c.vi_block ? c.vi_nblocks : 0;
   in->vi_exc_nodes = c.fmt == FMT_VI && c.vi_block ? c.vi_nexc : 0;
+  in->split_escapes = c.fmt == FMT_SPLIT && c.dsl.esc ? c.dsl.nesc : 0;
   if (c.device >= 0) spmv_tile(c, &in->spmv_tx, &in->spmv_ty, &in->spmv_kc);
   in->ex0 = g.ex0;
   in->ey0 = g.ey0;
@@ -1183,6 +1186,29 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
     }
     MCX_HIP(hipStreamSynchronize(c.stream));
   }
+  // AIJ-split escapes: residual of (owned node, slot) added to its bf16 hi
+  std::unordered_map<int64_t, double> escmap;
+  if (vals && c.fmt == FMT_SPLIT && c.dsl.esc && c.dsl.nesc) {
+    std::vector<unsigned> en(g.nown);
+    std::vector<double> er(c.dsl.nesc);
+    std::vector<unsigned char> es(c.dsl.nesc);
+    MCX_HIP(hipMemcpyAsync(en.data(), c.esc_node, sizeof(unsigned) * en.size(), hipMemcpyDeviceToHost, c.stream));
+    MCX_HIP(hipMemcpyAsync(er.data(), c.esc_res, sizeof(double) * er.size(), hipMemcpyDeviceToHost, c.stream));
+    MCX_HIP(hipMemcpyAsync(es.data(), c.esc_slot, es.size(), hipMemcpyDeviceToHost, c.stream));
+    MCX_HIP(hipStreamSynchronize(c.stream));
+    for (int64_t n = 0; n < g.nown; n++)
+      if (en[n]) {
+        const unsigned m = en[n] >> 24, base = (en[n] & 0xffffffu) - 1u;
+        for (unsigned t = 0; t < m; t++) escmap[n * 128 + es[base + t]] = er[base + t];
+      }
+  }
+  auto escres = [&](int64_t n, int s, double& v) -> bool {
+    if (escmap.empty()) return false;
+    auto it = escmap.find(n * 128 + s);
+    if (it == escmap.end()) return false;
+    v = it->second;
+    return true;
+  };
   // AIJ-split: packed position of each correction slot (-1: no correction stored), stored with
   // the row node (u_of index): nb*9 + r*3 + c
   int dpos[126];
@@ -1219,13 +1245,20 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
             const int64_t pc = 64 + i + (j + 1) * (int64_t)g.UX + (k + 1) * (int64_t)g.UXY;
             const int64_t q = pc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * (int64_t)g.UX + (nb / 9 - 1) * (int64_t)g.UXY;
             static const int dsl[3][3] = {{0, 1, 2}, {1, 3, 4}, {2, 4, 5}};
+            double er = 0.;
             if (nb < 13) {
               v = uval(q, 6 + 9 * (12 - nb) + cc * 3 + r);
-              if (c.fmt == FMT_SPLIT) v = v + corr(pc, nb * 9 + r * 3 + cc);  // exact AIJ lower value
+              if (c.fmt == FMT_SPLIT) {  // exact AIJ lower value (an escape: mirror + (hi + residual))
+                const int s = nb * 9 + r * 3 + cc;
+                v = escres(n, s, er) ? v + (corr(pc, s) + er) : v + corr(pc, s);
+              }
             }
             else if (nb == 13) {
               v = uval(pc, dsl[r][cc]);
-              if (c.fmt == FMT_SPLIT && r > cc) v = v + corr(pc, 13 * 9 + r * 3 + cc);  // lower triangle
+              if (c.fmt == FMT_SPLIT && r > cc) {  // lower triangle
+                const int s = 13 * 9 + r * 3 + cc;
+                v = escres(n, s, er) ? v + (corr(pc, s) + er) : v + corr(pc, s);
+              }
             }
             else v = uval(pc, 6 + 9 * (nb - 14) + r * 3 + cc);
           } else if (vals && c.fmt == FMT_VI) {
@@ -1455,12 +1488,9 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.vi_exc_list = (int)value;
     return 0;
   }
-  if (!std::strcmp(name, "vi_mpass")) {
-    if (value < 1. || value > 8. || (double)(int)value != value) {
-      set_error("vi_mpass: 1 .. 8");
-      return 1;
-    }
-    c.vi_mpass = (int)value;
+  if (!std::strcmp(name, "split_esc")) {  // takes effect at the next mcx_assembly_jac
+    c.split_esc = value != 0.;
+    c.split_declined = false;
     return 0;
   }
   if (!std::strcmp(name, "vi_wmap")) {

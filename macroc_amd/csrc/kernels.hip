@@ -676,7 +676,8 @@ __global__ __launch_bounds__(TPB) void k_gather_matrix_sym(Geo g, Material mat, 
 template <bool TABLE>
 __device__ __forceinline__ void split_block(const Geo& g, const Material& mat, const double* __restrict__ Ke,
                                             const double* __restrict__ U, int n, int nb, unsigned (&f32)[9],
-                                            unsigned& bits, unsigned& bad) {
+                                            unsigned& bits, unsigned& bad, unsigned& esc,
+                                            double* __restrict__ dout = nullptr) {
   int i, j, k;
   node_ijk(g, n, i, j, k);
   bits = bad = 0;
@@ -701,13 +702,24 @@ __device__ __forceinline__ void split_block(const Geo& g, const Material& mat, c
         mir[r * 3 + c] = Um[(s >> 1) * 128 + (s & 1)];
       }
   }
+  esc = 0u;
 #pragma unroll
   for (int q = 0; q < 9; q++) {
     const double d = low[q] - mir[q];
+    if (dout) dout[q] = d;
     f32[q] = __float_as_uint((float)d);
     const unsigned fb = f32[q] & 0xffff0000u;
     const double df = (double)__uint_as_float(f32[q]), db = (double)__uint_as_float(fb);
-    if (db != d || mir[q] + db != low[q]) bad |= 1;  // not exact in bf16
+    const bool strict = nb != 13 || q == 3 || q == 6 || q == 7;
+    if (db != d || mir[q] + db != low[q]) {
+      bad |= 1;  // not exact in bf16
+      // escape (dense bf16 corrections): the truncated bf16 hi plus the exact double residual
+      // d - hi, reconstructing the AIJ value as mirror + (hi + residual)
+      if (strict) {
+        if (db + (d - db) == d && mir[q] + d == low[q]) esc |= 1u << q;
+        else bad |= 4;
+      }
+    }
     if (df != d || mir[q] + df != low[q]) bad |= 2;  // not exact in f32
     if (d != 0.) bits |= 1u << q;
   }
@@ -719,17 +731,22 @@ __device__ __forceinline__ void split_block(const Geo& g, const Material& mat, c
 // in bf16, bit 1 = inexact in f32 (then the matrix is stored as plain AIJ blocks).
 template <bool TABLE>
 __global__ __launch_bounds__(TPB) void k_split_mask(Geo g, Material mat, const double* __restrict__ Ke,
-                                                    const double* __restrict__ U, unsigned* __restrict__ mask) {
+                                                    const double* __restrict__ U, unsigned* __restrict__ mask,
+                                                    unsigned* __restrict__ eflag) {
   __shared__ unsigned s_bits, s_bad;
   if (threadIdx.x == 0) s_bits = s_bad = 0;
   __syncthreads();
   const int n = blockIdx.x * TPB + threadIdx.x;
   const int nb = blockIdx.y;
   if (n < g.nown) {
-    unsigned f32[9], bits, bad;
-    split_block<TABLE>(g, mat, Ke, U, n, nb, f32, bits, bad);
+    unsigned f32[9], bits, bad, esc;
+    split_block<TABLE>(g, mat, Ke, U, n, nb, f32, bits, bad, esc);
     if (bits) atomicOr(&s_bits, bits);
     if (bad) atomicOr(&s_bad, bad);
+    if (esc) {  // dense bf16 corrections with escapes: count them, flag the node
+      atomicAdd(&mask[15], (unsigned)__builtin_popcount(esc));
+      if (eflag) eflag[n] = 1u;
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -748,8 +765,8 @@ __global__ __launch_bounds__(TPB) void k_split_pack(Geo g, Material mat, const d
   const int nb = blockIdx.y;
   const unsigned m9 = dl.m9[nb];
   if (n >= g.nown || !m9) return;
-  unsigned f32[9], bits, bad;
-  split_block<TABLE>(g, mat, Ke, U, n, nb, f32, bits, bad);
+  unsigned f32[9], bits, bad, esc;
+  split_block<TABLE>(g, mat, Ke, U, n, nb, f32, bits, bad, esc);
   int i, j, k;
   node_ijk(g, n, i, j, k);
   const int64_t u = u_of(g, i, j, k);
@@ -764,6 +781,44 @@ __global__ __launch_bounds__(TPB) void k_split_pack(Geo g, Material mat, const d
     }
     p++;
   }
+}
+
+// AIJ-split, dense bf16 corrections with escapes: for every node flagged by k_split_mask (a
+// correction not exact in bf16), its escaped slots' residuals d - hi in slot order (lower block nb
+// ascending, then r*3 + c) at a base taken from an atomic counter: esc_node[n] = count << 24 |
+// (base + 1).  The base order varies run to run, a node's entries and their order do not.
+template <bool TABLE>
+__global__ __launch_bounds__(TPB) void k_split_esc(Geo g, Material mat, const double* __restrict__ Ke,
+                                                   const double* __restrict__ U, unsigned* __restrict__ eflag,
+                                                   unsigned* __restrict__ cnt, unsigned cap, double* __restrict__ esc_res,
+                                                   unsigned char* __restrict__ esc_slot) {
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown || !eflag[n]) return;
+  unsigned m = 0;  // pass 1: the node's escapes (rare: recomputing its blocks twice is cheap)
+  for (int nb = 0; nb < 14; nb++) {
+    unsigned f32[9], bits, bad, esc;
+    split_block<TABLE>(g, mat, Ke, U, n, nb, f32, bits, bad, esc);
+    m += __builtin_popcount(esc);
+  }
+  const unsigned base = atomicAdd(cnt, m);
+  if (base + m > cap || m > 126u) {  // more escapes than the host sized for: the host falls back
+    eflag[n] = 0xffffffffu;
+    return;
+  }
+  unsigned t = base;
+  for (int nb = 0; nb < 14; nb++) {  // pass 2: residuals d - hi in slot order
+    unsigned f32[9], bits, bad, esc;
+    double d[9];
+    split_block<TABLE>(g, mat, Ke, U, n, nb, f32, bits, bad, esc, d);
+    for (int q = 0; q < 9; q++) {
+      if (!(esc >> q & 1u)) continue;
+      const double hi = (double)__uint_as_float(f32[q] & 0xffff0000u);
+      esc_res[t] = d[q] - hi;
+      esc_slot[t] = (unsigned char)(nb * 9 + q);
+      t++;
+    }
+  }
+  eflag[n] = m << 24 | (base + 1u);
 }
 
 // PCSetUp_Jacobi: diag, VecReciprocal (non-zeros only), zeros -> 1
@@ -1008,7 +1063,6 @@ struct ZTiling {
   int dbg = 0;            // timing-only diagnostics (k_spmv_vibm: 1 = every wave takes the scalar path)
   int wmap = 1;           // k_spmv_vibm PATCH: 1 = patches on SIMDs as a Latin square, 0 = row-major (A/B)
   int xlist = VI_EXC_LIST;  // k_spmv_vibm EXC: exception nodes a tile defers (option vi_exc_list; the rest in their plane)
-  int mpass = 1;          // k_spmv_vibm UNI: scalar passes per wave and plane (option vi_mpass; 1 = whole uniform waves only)
 };
 
 static ZTiling z_tiling(const Geo& g, int ztx, int zty, int want) {
@@ -1559,10 +1613,15 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
 // strictly-lower entries — added to the z-march's (lower + upper) sum; with DOT the p.w partials
 // of the finished y.  One thread per owned node: 15 (bf16) or 30 (f32) coalesced 16-B quads, the
 // 13 source nodes' x (3 doubles each) gathered once per block.  No barriers, full occupancy.
+// Escapes (bf16 storage, esc_node set): after the 120 slots, the node's escaped corrections add
+// their residuals d - hi (the bf16 hi is in D), in slot order.
 template <bool DOT, bool GATED, bool WIDE>
 __global__ __launch_bounds__(TPB) void k_split_dense(Geo g, const uint16_t* __restrict__ Dq, int Lq,
                                                      const double* __restrict__ x, double* __restrict__ y,
-                                                     double* __restrict__ part, const CgState* __restrict__ cg) {
+                                                     double* __restrict__ part, const CgState* __restrict__ cg,
+                                                     const unsigned* __restrict__ esc_node = nullptr,
+                                                     const double* __restrict__ esc_res = nullptr,
+                                                     const unsigned char* __restrict__ esc_slot = nullptr) {
   __shared__ double sh[TPB / 64];
   if (GATED && cg->reason) return;
   const int n = blockIdx.x * TPB + threadIdx.x;
@@ -1600,6 +1659,20 @@ __global__ __launch_bounds__(TPB) void k_split_dense(Geo g, const uint16_t* __re
     d1 += corr(117) * x0;  // (1,0)
     d2 += corr(118) * x0;  // (2,0)
     d2 += corr(119) * x1;  // (2,1)
+    if (!WIDE && esc_node) {
+      const unsigned e = esc_node[n];
+      if (e) {  // rare: a branch almost no lane takes
+        const unsigned m = e >> 24, base = (e & 0xffffffu) - 1u;
+        for (unsigned t = 0; t < m; t++) {
+          const int sl = esc_slot[base + t], nb = sl / 9, rc = sl - 9 * nb, r = rc / 3, cc = rc - 3 * r;
+          const int q = nb < 13 ? pc + (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY : pc;
+          const double tv = esc_res[base + t] * x[3 * (int64_t)q + cc];
+          if (r == 0) d0 += tv;
+          else if (r == 1) d1 += tv;
+          else d2 += tv;
+        }
+      }
+    }
     const double y0 = y[3 * (int64_t)n] + d0, y1 = y[3 * (int64_t)n + 1] + d1, y2 = y[3 * (int64_t)n + 2] + d2;
     y[3 * (int64_t)n] = y0;
     y[3 * (int64_t)n + 1] = y1;
@@ -2504,34 +2577,33 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
     // the dictionary in global memory, scalar cache) and multiplies them as SGPR operands: the
     // dictionary's 486 LDS cycles per wave and plane leave the LDS, which then only serves the x
     // ring.  Other waves read the dictionary from LDS.  Same values, same products, same order.
-    // Round 4 (zt.mpass > 1): a wave with a few distinct id vectors (a tile's x-face patch at the
-    // domain boundary: interior lanes and boundary-column lanes) runs the scalar path once per
-    // vector, each pass under the exec mask of the lanes holding it (the first remaining lane's
-    // vector; at most mpass passes), so those waves no longer read the dictionary from LDS in 27
-    // dependent rounds.  Every lane runs exactly one pass or the LDS path: the same products in
-    // the same order.  mpass 1: round 3's rule (one pass, only when all 64 lanes agree).
     unsigned sw[7] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    bool rest = inxy;  // this lane still needs its row after the scalar passes
+    bool uni = false;
     if (UNI) {
-      const unsigned wd[7] = {c0[0], c0[1], c0[2], c0[3], c1[0], c1[1], c1[2]};
-      const unsigned long long all = __ballot(inxy);
-      // exact rows (!FMA): the scalar path's fixed inode pairing needs every neighbour present
-      unsigned long long left = __ballot(inxy && (!EXC || c1[3] == 0u) && (FMA || present_mask(g, i, j, k) == PRES_ALL));
-      if (zt.dbg & 1) left = all;  // timing-only diagnostics: every wave takes the first lane's blocks
-      for (int ps = 0; ps < zt.mpass && left; ps++) {  // uniform
-        const int lead = (int)__builtin_ctzll(left);
-        unsigned diff = 0u;
 #pragma unroll
-        for (int q = 0; q < 7; q++) {
-          sw[q] = __builtin_amdgcn_readlane(wd[q], lead);
-          diff |= wd[q] ^ sw[q];
-        }
-        const bool mine = ((left >> ln) & 1ull) && (diff == 0u || (zt.dbg & 1));
-        const unsigned long long mm = __ballot(mine);
-        if (zt.mpass == 1 && mm != all) break;  // round 3: whole waves only
-        left &= ~mm;
-        if (mine) rest = false;
-        if (!mine) continue;
+      for (int q = 0; q < 7; q++) sw[q] = __builtin_amdgcn_readfirstlane(q < 4 ? c0[q] : c1[q - 4]);
+      unsigned diff = 0u;
+#pragma unroll
+      for (int q = 0; q < 7; q++) diff |= (q < 4 ? c0[q] : c1[q - 4]) ^ sw[q];
+      // exact rows (!FMA): the scalar path's fixed inode pairing needs every neighbour present
+      uni = __all(inxy && diff == 0u && (!EXC || c1[3] == 0u) &&
+                  (FMA || present_mask(g, i, j, k) == PRES_ALL)) || (zt.dbg & 1);
+    }
+    // EXC: the wave's exception lanes of this plane take the next positions of its segment in
+    // lane order (ballot + mbcnt, converged here); those beyond the capacity stay in the plane
+    bool deferred = false;
+    if constexpr (EXC) {
+      const bool xh = !(UNI && uni) && inxy && c1[3] != 0u;
+      const unsigned long long xm = __ballot(xh);
+      if (xm) {  // uniform
+        const int pos = wn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(xm >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((unsigned)xm, 0u));
+        deferred = xh && pos < wcap;
+        if (deferred) s_xl[wv * SEG + pos] = (k - k0) * T + me;
+        wn = min(wcap, wn + (int)__popcll(xm));
+      }
+    }
+    if (UNI && uni) {  // (every lane is inxy)
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
       InodeRows<true> acc;  // !FMA: the inode pairs of a node whose 27 neighbours are present
       typedef const volatile __attribute__((address_space(3))) double lds_vdouble;
@@ -2589,27 +2661,9 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       __builtin_nontemporal_store(y1, &y[3 * n + 1]);
       __builtin_nontemporal_store(y2, &y[3 * n + 2]);
       if (DOT) dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
-      }
-    }
-    // EXC: the wave's exception lanes of this plane take the next positions of its segment in
-    // lane order (ballot + mbcnt, converged here); those beyond the capacity stay in the plane
-    bool deferred = false;
-    if constexpr (EXC) {
-      const bool xh = rest && c1[3] != 0u;
-      const unsigned long long xm = __ballot(xh);
-      if (xm) {  // uniform
-        const int pos = wn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(xm >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((unsigned)xm, 0u));
-        deferred = xh && pos < wcap;
-        if (deferred) s_xl[wv * SEG + pos] = (k - k0) * T + me;
-        wn = min(wcap, wn + (int)__popcll(xm));
-      }
-    }
-    if (!rest) {
-      // computed by a scalar pass
     } else if (EXC && deferred) {
       // deferred to the block's exception pass below
-    } else if (EXC && c1[3]) {
+    } else if (EXC && inxy && c1[3]) {
       // an exception node (EXC instantiations only) that found the tile's list full: its 27
       // plain blocks from exc [slot][27][9], a rolled loop of its own so the indexed path below
       // keeps its registers; same order and products as the indexed rows
@@ -2649,7 +2703,7 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       __builtin_nontemporal_store(y1, &y[3 * n + 1]);
       __builtin_nontemporal_store(y2, &y[3 * n + 2]);
       if (DOT) dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
-    } else {
+    } else if (inxy) {
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
       InodeRows<false> acc;
       if constexpr (!FMA) acc.pres = present_mask(g, i, j, k);
@@ -2930,24 +2984,27 @@ static void launch_symp(Ctx& c, const double* xpad, double* y, bool dot, bool ga
       hipLaunchKernelGGL((k_spmv_symp<false, false, ZTX, ZTY, AIJS>), dim3(nb), dim3(ZTX * ZTY), 0, c.stream, c.g,
                          c.U, xpad, y, c.partials, c.cg, zt, Dq, none);
     const dim3 gd((unsigned)((c.g.nown + TPB - 1) / TPB));
+    const unsigned* en = dl.esc && dl.nesc ? c.esc_node : nullptr;
+    const double* er = c.esc_res;
+    const unsigned char* es = c.esc_slot;
     if (dot && gated && dl.wide)
       hipLaunchKernelGGL((k_split_dense<true, true, true>), gd, dim3(TPB), 0, c.stream, c.g, Dq, dl.Lq, xpad, y,
                          c.partials, c.cg);
     else if (dot && gated)
       hipLaunchKernelGGL((k_split_dense<true, true, false>), gd, dim3(TPB), 0, c.stream, c.g, Dq, dl.Lq, xpad, y,
-                         c.partials, c.cg);
+                         c.partials, c.cg, en, er, es);
     else if (dot && dl.wide)
       hipLaunchKernelGGL((k_split_dense<true, false, true>), gd, dim3(TPB), 0, c.stream, c.g, Dq, dl.Lq, xpad, y,
                          c.partials, c.cg);
     else if (dot)
       hipLaunchKernelGGL((k_split_dense<true, false, false>), gd, dim3(TPB), 0, c.stream, c.g, Dq, dl.Lq, xpad, y,
-                         c.partials, c.cg);
+                         c.partials, c.cg, en, er, es);
     else if (dl.wide)
       hipLaunchKernelGGL((k_split_dense<false, false, true>), gd, dim3(TPB), 0, c.stream, c.g, Dq, dl.Lq, xpad, y,
                          c.partials, c.cg);
     else
       hipLaunchKernelGGL((k_split_dense<false, false, false>), gd, dim3(TPB), 0, c.stream, c.g, Dq, dl.Lq, xpad, y,
-                         c.partials, c.cg);
+                         c.partials, c.cg, en, er, es);
     return;
   }
   if (c.split_dbg) {  // timing-only diagnostics (wrong products): 1 = loads, no corrections; 2 = neither
@@ -3906,18 +3963,33 @@ void launch_gather_matrix_sym(Ctx& c) {
 // the corrections and writes the packed ones, so no per-slot scratch array exists.
 int build_split(Ctx& c, bool* exact) {
   MCX_HIP(hipMemsetAsync(c.d_mask, 0, 16 * sizeof(unsigned), c.stream));
+  if (c.split_esc && !c.esc_node) {  // per owned node: escape flag, then count << 24 | first + 1
+    MCX_HIP(hipMalloc(&c.esc_node, std::max<int64_t>(1, c.g.nown) * sizeof(unsigned)));
+    c.device_bytes += c.g.nown * (int64_t)sizeof(unsigned);
+  }
+  if (c.esc_node) MCX_HIP(hipMemsetAsync(c.esc_node, 0, c.g.nown * sizeof(unsigned), c.stream));
+  unsigned* eflag = c.split_esc ? c.esc_node : nullptr;
   const dim3 grid(nblk(c.g.nown), 14);
   if (table_law(c))
-    hipLaunchKernelGGL(k_split_mask<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.U, c.d_mask);
+    hipLaunchKernelGGL(k_split_mask<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.U, c.d_mask, eflag);
   else
-    hipLaunchKernelGGL(k_split_mask<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.U, c.d_mask);
+    hipLaunchKernelGGL(k_split_mask<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.U, c.d_mask, eflag);
   unsigned hm[16];
   MCX_HIP(hipMemcpyAsync(hm, c.d_mask, sizeof(hm), hipMemcpyDeviceToHost, c.stream));
   MCX_HIP(hipStreamSynchronize(c.stream));
-  *exact = (hm[14] & 2u) == 0;  // f32 always suffices when bf16 does
-  if (!*exact) return 0;
   DSlots dl;
-  dl.wide = (hm[14] & 1u) || c.split_wide ? 1 : 0;
+  // dense bf16 corrections with escapes: every correction not exact in bf16 is escapable (its
+  // truncated bf16 hi plus an exact double residual reconstruct it), dense storage is needed,
+  // and the escapes are few (at most one per 16 owned nodes, < 2^24 entries)
+  int lbf = 0;
+  for (int b = 0; b < 14; b++) lbf += __builtin_popcount(hm[b] & 511u);
+  const bool esc = eflag && (hm[14] & 1u) && !(hm[14] & 4u) && !c.split_wide && c.split_dense &&
+                   (lbf + 7) / 8 > c.split_maxq && (int64_t)hm[15] <= std::min<int64_t>(c.g.nown / 16 + 64, (1 << 24) - 2);
+  *exact = (hm[14] & 2u) == 0 || esc;  // f32 always suffices when bf16 does
+  if (!*exact) return 0;
+  dl.wide = !esc && ((hm[14] & 1u) || c.split_wide) ? 1 : 0;
+  dl.esc = esc ? 1 : 0;
+  dl.nesc = esc ? (int)hm[15] : 0;
   for (int b = 0; b < 14; b++) {
     dl.m9[b] = (unsigned short)(hm[b] & 511u);
     dl.pos[b] = (unsigned char)dl.L;
@@ -3967,6 +4039,27 @@ int build_split(Ctx& c, bool* exact) {
       hipLaunchKernelGGL(k_split_pack<true>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.U, c.D, dl);
     else
       hipLaunchKernelGGL(k_split_pack<false>, grid, dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.U, c.D, dl);
+  }
+  if (dl.esc && dl.nesc) {  // the escapes' residuals, a node's entries contiguous in slot order
+    if (dl.nesc > c.esc_cap) {
+      if (c.esc_res) {
+        MCX_HIP(hipStreamSynchronize(c.stream));
+        MCX_HIP(hipFree(c.esc_res));
+        MCX_HIP(hipFree(c.esc_slot));
+        c.device_bytes -= c.esc_cap * 9;
+      }
+      c.esc_cap = std::max<int64_t>(dl.nesc, 1024);
+      MCX_HIP(hipMalloc(&c.esc_res, c.esc_cap * sizeof(double)));
+      MCX_HIP(hipMalloc(&c.esc_slot, c.esc_cap));
+      c.device_bytes += c.esc_cap * 9;
+    }
+    MCX_HIP(hipMemsetAsync(c.d_mask + 15, 0, sizeof(unsigned), c.stream));  // the entries' allocation counter
+    if (table_law(c))
+      hipLaunchKernelGGL(k_split_esc<true>, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.U,
+                         c.esc_node, c.d_mask + 15, (unsigned)c.esc_cap, c.esc_res, c.esc_slot);
+    else
+      hipLaunchKernelGGL(k_split_esc<false>, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.U,
+                         c.esc_node, c.d_mask + 15, (unsigned)c.esc_cap, c.esc_res, c.esc_slot);
   }
   return 0;
 }
@@ -4339,7 +4432,6 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
       zt.dbg = c.split_dbg;
       zt.wmap = c.vi_wmap;
       zt.xlist = c.vi_exc_list;
-      zt.mpass = c.vi_mpass;
       int tx, ty;
       vis_shape(c, tx, ty);
 #define MCX_VIBM(TXV, TYV, XVV, UV, PV, ...)                                                                          \

@@ -97,6 +97,9 @@ struct DSlots {
   int xc[24];               // slot p < 24: (x offset from 3 * padded index of the row node) * 4 + row
   int dense = 0;            // 1: all 120 slots stored in canonical order (nb*9 + r*3 + c, then the diagonal's
                             // (1,0) (2,0) (2,1)) and applied by a second pass, k_split_dense
+  int esc = 0;              // dense bf16 with escapes: a correction not exact in bf16 keeps its truncated bf16
+                            // hi in D plus the exact residual d - hi in the escape arrays (Ctx::esc_*)
+  int nesc = 0;             // escaped corrections of the current matrix
 };
 
 // In-process transport: several contexts (one host thread each) exchanging halos and partial
@@ -140,7 +143,7 @@ struct Ctx {
   double* p_pad4 = nullptr;
   int cg_fusep = 0;          // option cg_fusep: fuse the CG p update into the value-indexed SpMV (single rank; A/B: no gain)
   bool fusep_used = false;   // the last solve ran the fused kernel (timing: its bytes per launch)
-  int cg_pdb = 1;            // option cg_pdb: 1 = p double-buffered (p_pad / p_pad2), VecAXPY(x) every second
+  int cg_pdb = 4;            // option cg_pdb: 1 = p double-buffered (p_pad / p_pad2), VecAXPY(x) every second
                              // iteration; 4 = four buffers, x every fourth iteration; 0 = one buffer, x every iteration
   bool pdb_used = false;     // the current solve runs the double-buffered p update
   bool pqb_used = false;     // ... the quad-buffered one (cg_pdb 4; pdb_used too)
@@ -161,6 +164,11 @@ struct Ctx {
   double* U = nullptr;       // sbaij upper stencil blocks over the padded box [npgroups][UPAIR][64] double2
   uint16_t* D = nullptr;     // AIJ-split: bf16 corrections of the padded box [u_of/64][dsl.Lq][64] x 8
   int64_t D_bytes = 0;       // allocated bytes of D (grown to the active slots' quads)
+  unsigned* esc_node = nullptr;   // AIJ-split escapes: per owned node count << 24 | (first entry + 1), 0 = none
+  double* esc_res = nullptr;      // escaped corrections' residuals d - hi, a node's entries in slot order
+  unsigned char* esc_slot = nullptr;  // their slots (nb*9 + r*3 + c)
+  int64_t esc_cap = 0;            // allocated escape entries
+  int split_esc = 1;              // option split_esc: dense corrections as bf16 + escapes when some are not bf16-exact
   unsigned* d_mask = nullptr;  // AIJ-split assembly: [0..13] slot masks per lower block, [14] inexact
   // value-indexed AIJ (FMT_VI): index bytes [ngroups][VI_CHUNKS][64] x 16 B, the dictionary
   // (VI_MAX doubles, ascending bit pattern), the build's value set and its slot -> index map
@@ -200,7 +208,7 @@ struct Ctx {
   int64_t vi_exc_bytes = 0;             // allocated bytes of vi_exc
   int64_t vi_nexc = 0;                  // exception nodes of the current matrix
   bool plain_ke = false;                // this assembly formed kref + the non-plain elements' Ke only
-  int vi_exc_max = 250;                 // option vi_exc_max: per-mille of owned nodes beyond which the
+  int vi_exc_max = 300;                 // option vi_exc_max: per-mille of owned nodes beyond which the
                                         // assembly falls back to AIJ-split (0: no exceptions)
   double* ke_uni = nullptr;  // elastic law: the element matrix [8 a][8 b][9], the same for every element
   int aij_vi = 1;            // aij: assemble in FMT_VI when the matrix has at most VI_MAX distinct values
@@ -212,7 +220,6 @@ struct Ctx {
   int vi_wmap = 1;           // staged block-indexed SpMV: 16x4 patches on SIMDs as a Latin square (option vi_wmap; 0: row-major)
   int vi_tx = 0;             // staged block-indexed SpMV tile width 256 | 128 | 64 (0: 64; option vi_tx)
   int vi_uni = 1;            // staged block-indexed SpMV: wave-uniform blocks from scalar loads (option vi_uni)
-  int vi_mpass = 1;          // with vi_uni: scalar passes per wave and plane, one per distinct id vector (option vi_mpass)
   int vi_xread = 1;          // staged block-indexed SpMV: x as unpaired 8-B LDS reads (option vi_xread; 0: compiler's pairs)
   int vi_stage = -1;         // FMT_VI SpMV: 1 = x staged in LDS, z-marching tiles; 0 = x gathered; -1 = by grid (vi_staged)
   bool vi_declined = false;  // a per-GP-tangent law overflowed the dictionary: skip the attempt

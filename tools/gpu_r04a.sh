@@ -6,8 +6,6 @@ set -euo pipefail
 export TMPDIR=/tmp; mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_multirank.py -x -v --timeout 300 \
   --timeout-method thread > gpurun_out/r04a_pytest.log 2>&1
-timeout -k 10 200 python -u tools/spmv_ab.py --grid 256 --variants "vi_mpass=1;vi_mpass=2;vi_mpass=4" --base "" \
-  > gpurun_out/r04_ab_mpass256.log 2>&1
 timeout -k 10 200 python -u tools/cg_ab.py --grid 256 --option cg_pdb --values 1,4 --rounds 3 \
   > gpurun_out/r04_cg_ab_pqb256.log 2>&1
 timeout -k 10 300 python -u tools/determinism_check.py --grid 128 --ts 3 --opts ';' > gpurun_out/r04_determinism_128.log 2>&1
