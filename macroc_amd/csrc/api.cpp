@@ -1493,6 +1493,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.split_declined = false;
     return 0;
   }
+  if (!std::strcmp(name, "vi_ypair")) {
+    c.vi_ypair = value != 0.;
+    return 0;
+  }
   if (!std::strcmp(name, "vi_wmap")) {
     c.vi_wmap = value != 0.;
     return 0;

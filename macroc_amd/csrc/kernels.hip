@@ -1063,6 +1063,7 @@ struct ZTiling {
   int dbg = 0;            // timing-only diagnostics (k_spmv_vibm: 1 = every wave takes the scalar path)
   int wmap = 1;           // k_spmv_vibm PATCH: 1 = patches on SIMDs as a Latin square, 0 = row-major (A/B)
   int xlist = VI_EXC_LIST;  // k_spmv_vibm EXC: exception nodes a tile defers (option vi_exc_list; the rest in their plane)
+  int ypair = 0;          // k_spmv_vibm UNI: y of lane pairs as 16-B stores (option vi_ypair; needs an even nx)
 };
 
 static ZTiling z_tiling(const Geo& g, int ztx, int zty, int want) {
@@ -2657,9 +2658,31 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       }
       if constexpr (!FMA) y0 = acc.row(0), y1 = acc.row(1), y2 = acc.row(2);
       const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
-      __builtin_nontemporal_store(y0, &y[3 * n + 0]);
-      __builtin_nontemporal_store(y1, &y[3 * n + 1]);
-      __builtin_nontemporal_store(y2, &y[3 * n + 2]);
+      if (zt.ypair) {
+        // y of a lane pair (even lane = even node, its odd neighbour in x on the next lane: 48
+        // contiguous, 16-B aligned bytes) as three 16-B stores instead of six 8-B ones: the even
+        // lane (y0, y1) and (y2, the odd lane's y0), the odd lane (y1, y2); the odd lane's y0
+        // moves over by a DPP row shift (ypair needs an even nx and every lane of the wave here)
+        const unsigned long long b0 = __double_as_longlong(y0);
+        const unsigned lo = __builtin_amdgcn_mov_dpp((int)(unsigned)b0, 0x101, 0xf, 0xf, false);        // row_shl:1
+        const unsigned hi = __builtin_amdgcn_mov_dpp((int)(unsigned)(b0 >> 32), 0x101, 0xf, 0xf, false);
+        const double n0 = __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        const bool even = (ln & 1) == 0;
+        d2v a, b;
+        a.x = even ? y0 : y1;
+        a.y = even ? y1 : y2;
+        __builtin_nontemporal_store(a, reinterpret_cast<d2v*>(&y[3 * n + (even ? 0 : 1)]));
+        if (even) {
+          b.x = y2;
+          b.y = n0;
+          __builtin_nontemporal_store(b, reinterpret_cast<d2v*>(&y[3 * n + 2]));
+        }
+      } else {
+        __builtin_nontemporal_store(y0, &y[3 * n + 0]);
+        __builtin_nontemporal_store(y1, &y[3 * n + 1]);
+        __builtin_nontemporal_store(y2, &y[3 * n + 2]);
+      }
       if (DOT) dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
     } else if (EXC && deferred) {
       // deferred to the block's exception pass below
@@ -4432,6 +4455,7 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
       zt.dbg = c.split_dbg;
       zt.wmap = c.vi_wmap;
       zt.xlist = c.vi_exc_list;
+      zt.ypair = c.vi_ypair && (c.g.nx % 2) == 0;
       int tx, ty;
       vis_shape(c, tx, ty);
 #define MCX_VIBM(TXV, TYV, XVV, UV, PV, ...)                                                                          \

@@ -220,6 +220,7 @@ struct Ctx {
   int vi_wmap = 1;           // staged block-indexed SpMV: 16x4 patches on SIMDs as a Latin square (option vi_wmap; 0: row-major)
   int vi_tx = 0;             // staged block-indexed SpMV tile width 256 | 128 | 64 (0: 64; option vi_tx)
   int vi_uni = 1;            // staged block-indexed SpMV: wave-uniform blocks from scalar loads (option vi_uni)
+  int vi_ypair = 0;          // with vi_uni: y of lane pairs as 16-B stores (option vi_ypair; A/B)
   int vi_xread = 1;          // staged block-indexed SpMV: x as unpaired 8-B LDS reads (option vi_xread; 0: compiler's pairs)
   int vi_stage = -1;         // FMT_VI SpMV: 1 = x staged in LDS, z-marching tiles; 0 = x gathered; -1 = by grid (vi_staged)
   bool vi_declined = false;  // a per-GP-tangent law overflowed the dictionary: skip the attempt

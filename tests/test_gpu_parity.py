@@ -693,10 +693,18 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
                 m.set_option("vi_uni", uni)
                 m.set_option("vi_patch", patch)
                 assert np.array_equal(m.spmv(x), y_ref), (zblocks, uni, patch)
+            m.set_option("vi_uni", 1)
+            m.set_option("vi_patch", 1)
+            m.set_option("vi_ypair", 1)  # the scalar path's y as 16-B lane-pair stores: the same rows
+            assert np.array_equal(m.spmv(x), y_ref), (zblocks, "ypair")
+            m.set_option("vi_ypair", 0)
             m.set_option("vi_fma", 1)
             yf = m.spmv(x)
             assert np.all(np.abs(yf - y_ref) <= 1e-14 * absrow + 1e-300), zblocks
             assert np.array_equal(m.spmv(x), yf)
+            m.set_option("vi_ypair", 1)
+            assert np.array_equal(m.spmv(x), yf), (zblocks, "ypair")
+            m.set_option("vi_ypair", 0)
         m.set_option("spmv_zblocks", 1)  # every tile marches all planes: the prefetch ring end to end
         assert m.get_info()["spmv_kc"] == NZ
         its, rn, reason = m.solve_Ax()
