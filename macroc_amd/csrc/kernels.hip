@@ -2578,6 +2578,11 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
     // the dictionary in global memory, scalar cache) and multiplies them as SGPR operands: the
     // dictionary's 486 LDS cycles per wave and plane leave the LDS, which then only serves the x
     // ring.  Other waves read the dictionary from LDS.  Same values, same products, same order.
+    // exact rows (!FMA): a node on the global domain boundary has clipped stencil columns, so its
+    // inode pairing depends on which neighbours exist; those rows are computed by k_spmv_vib_faces
+    // after the march, and every row here has all 27 neighbours: the pairing is fixed at compile
+    // time (InodeRows<true>) on every path
+    const bool full = FMA || present_mask(g, i, j, k) == PRES_ALL;
     unsigned sw[7] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
     bool uni = false;
     if (UNI) {
@@ -2586,15 +2591,13 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       unsigned diff = 0u;
 #pragma unroll
       for (int q = 0; q < 7; q++) diff |= (q < 4 ? c0[q] : c1[q - 4]) ^ sw[q];
-      // exact rows (!FMA): the scalar path's fixed inode pairing needs every neighbour present
-      uni = __all(inxy && diff == 0u && (!EXC || c1[3] == 0u) &&
-                  (FMA || present_mask(g, i, j, k) == PRES_ALL)) || (zt.dbg & 1);
+      uni = __all(inxy && full && diff == 0u && (!EXC || c1[3] == 0u)) || (zt.dbg & 1);
     }
     // EXC: the wave's exception lanes of this plane take the next positions of its segment in
     // lane order (ballot + mbcnt, converged here); those beyond the capacity stay in the plane
     bool deferred = false;
     if constexpr (EXC) {
-      const bool xh = !(UNI && uni) && inxy && c1[3] != 0u;
+      const bool xh = !(UNI && uni) && inxy && full && c1[3] != 0u;
       const unsigned long long xm = __ballot(xh);
       if (xm) {  // uniform
         const int pos = wn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(xm >> 32),
@@ -2686,15 +2689,14 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       if (DOT) dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
     } else if (EXC && deferred) {
       // deferred to the block's exception pass below
-    } else if (EXC && inxy && c1[3]) {
+    } else if (EXC && inxy && full && c1[3]) {
       // an exception node (EXC instantiations only) that found the tile's list full: its 27
       // plain blocks from exc [slot][27][9], a rolled loop of its own so the indexed path below
       // keeps its registers; same order and products as the indexed rows
       // Blocks in groups of 3 (one dy row): the group's 27 values are loaded together, one
       // round trip per group instead of per block.
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
-      InodeRows<false> acc;
-      if constexpr (!FMA) acc.pres = present_mask(g, i, j, k);
+      InodeRows<true> acc;  // !FMA: all 27 neighbours present (full)
       const double* eb = exc + (int64_t)(c1[3] - 1) * 243;
 #pragma unroll 1
       for (int nb0 = 0; nb0 < 27; nb0 += 3) {
@@ -2726,10 +2728,9 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       __builtin_nontemporal_store(y1, &y[3 * n + 1]);
       __builtin_nontemporal_store(y2, &y[3 * n + 2]);
       if (DOT) dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
-    } else if (inxy) {
+    } else if (inxy && full) {
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
-      InodeRows<false> acc;
-      if constexpr (!FMA) acc.pres = present_mask(g, i, j, k);
+      InodeRows<true> acc;  // !FMA: all 27 neighbours present (full)
       // x as separate 8-B LDS reads (ds_read_b64: 2 LDS cycles each): the compiler would pair
       // them into ds_read2_b64, 8 cycles for the same 16 B (MI355X_MICROARCH.md, LDS table);
       // volatile reads are not paired.
@@ -2812,8 +2813,7 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       const unsigned slot = I[(int64_t)(n >> 6) * (2 * 64) + (n & 63) + 64][3];
       const double* eb = exc + (int64_t)(slot - 1) * 243;
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
-      InodeRows<false> acc;
-      if constexpr (!FMA) acc.pres = present_mask(g, ei, ej, kk);
+      InodeRows<true> acc;  // !FMA: listed nodes are full (boundary nodes go to k_spmv_vib_faces)
 #pragma unroll 1
       for (int nb0 = 0; nb0 < 27; nb0 += 3) {
         double av[27];
@@ -2851,6 +2851,118 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
   if (DOT) {
     double s = block_sum<T>(dot, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = s;
+  }
+}
+
+// Owned nodes on the global domain boundary (faces whose stencil the DMDA clips), enumerated
+// without repetition: the z-face planes (whole nx x ny planes), then in the remaining planes the
+// y-face rows (whole nx rows), then in the remaining rows the x-face columns.
+struct FaceEnum {
+  int kz[2], nkz;      // z-face planes (0 and/or nz-1), count
+  int jy[2], njy;      // y-face rows
+  int ix[2], nix;      // x-face columns
+  int k0, kn, j0, jn;  // the other planes [k0, k0+kn), the other rows [j0, j0+jn)
+  int64_t nA, nB, n;   // nodes in the z planes, + the y rows, total
+};
+
+static FaceEnum face_enum(const Geo& g) {
+  FaceEnum f{};
+  auto sides = [](int lo_at_boundary, int hi_at_boundary, int w, int (&v)[2], int& cnt, int& o0, int& on) {
+    cnt = 0;
+    if (lo_at_boundary) v[cnt++] = 0;
+    if (hi_at_boundary && !(cnt && w - 1 == 0)) v[cnt++] = w - 1;
+    o0 = lo_at_boundary ? 1 : 0;
+    on = std::max(0, w - cnt);
+  };
+  int dummy0 = 0, dummy1 = 0;
+  sides(g.zs == 0, g.zs + g.nz == g.NZ, g.nz, f.kz, f.nkz, f.k0, f.kn);
+  sides(g.ys == 0, g.ys + g.ny == g.NY, g.ny, f.jy, f.njy, f.j0, f.jn);
+  sides(g.xs == 0, g.xs + g.nx == g.NX, g.nx, f.ix, f.nix, dummy0, dummy1);
+  f.nA = (int64_t)f.nkz * g.nx * g.ny;
+  f.nB = f.nA + (int64_t)f.kn * f.njy * g.nx;
+  f.n = f.nB + (int64_t)f.kn * f.jn * f.nix;
+  return f;
+}
+
+__device__ __forceinline__ void face_node(const Geo& g, const FaceEnum& f, int64_t t, int& i, int& j, int& k) {
+  if (t < f.nA) {
+    const int64_t pl = (int64_t)g.nx * g.ny;
+    k = f.kz[t / pl];
+    j = (int)((t % pl) / g.nx);
+    i = (int)(t % g.nx);
+  } else if (t < f.nB) {
+    t -= f.nA;
+    const int64_t rows = (int64_t)f.njy * g.nx;
+    k = f.k0 + (int)(t / rows);
+    j = f.jy[(t % rows) / g.nx];
+    i = (int)(t % g.nx);
+  } else {
+    t -= f.nB;
+    const int64_t cols = (int64_t)f.jn * f.nix;
+    k = f.k0 + (int)(t / cols);
+    j = f.j0 + (int)((t % cols) / f.nix);
+    i = f.ix[t % f.nix];
+  }
+}
+
+// Exact rows (-mat_vi_fma 0) of the value-indexed block storage on the global domain boundary:
+// the z-marching kernel leaves them out (their inode pairing follows the present columns, a
+// per-node pattern, which would put runtime pairing on every wave touching the boundary).  One
+// node per thread, x gathered from the padded vector, blocks from the dictionary in global memory
+// (20 KB, cached) or from the exception array, InodeRows with the node's presence mask; the block
+// p.w partial goes after the z-march's partials (part[blockIdx.x] of this grid).
+template <bool DOT, bool GATED, bool EXC>
+__global__ __launch_bounds__(TPB) void k_spmv_vib_faces(Geo g, const u32x4* __restrict__ I,
+                                                        const double* __restrict__ bdict,
+                                                        const double* __restrict__ x, double* __restrict__ y,
+                                                        double* __restrict__ part, const CgState* __restrict__ cg,
+                                                        FaceEnum fe, const double* __restrict__ exc) {
+  __shared__ double sh[TPB / 64];
+  if (GATED && cg->reason) return;
+  const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  double dot = 0.;
+  if (t < fe.n) {
+    int i, j, k;
+    face_node(g, fe, t, i, j, k);
+    const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
+    const int PX = g.PX, PXY = g.PX * g.PY;
+    const int pc = (i + 1) + (j + 1) * PX + (k + 1) * PXY;
+    const u32x4* ip = I + (n >> 6) * (2 * 64) + (n & 63);
+    const u32x4 w0 = ip[0], w1 = ip[64];
+    const unsigned slot = EXC ? w1[3] : 0u;
+    InodeRows<false> acc;
+    acc.pres = present_mask(g, i, j, k);
+    double xc0 = 0., xc1 = 0., xc2 = 0.;
+#pragma unroll
+    for (int nb = 0; nb < 27; nb++) {
+      if (!((acc.pres >> nb) & 1u)) continue;
+      const int off = (nb % 3 - 1) + ((nb / 3) % 3 - 1) * PX + (nb / 9 - 1) * PXY;
+      const double* xp = x + 3 * (int64_t)(pc + off);
+      const double xv[3] = {xp[0], xp[1], xp[2]};
+      if (nb == 13) {
+        xc0 = xv[0];
+        xc1 = xv[1];
+        xc2 = xv[2];
+      }
+      const double* e;
+      if (EXC && slot) {
+        e = exc + ((int64_t)(slot - 1) * 27 + nb) * 9;
+      } else {
+        const unsigned word = nb < 16 ? w0[nb >> 2] : w1[(nb - 16) >> 2];
+        e = bdict + ((word >> (8 * (nb & 3))) & 255u) * VIB_STRIDE;
+      }
+#pragma unroll
+      for (int q = 0; q < 9; q++) acc.term(nb, q / 3, q % 3, e[q] * xv[q % 3]);
+    }
+    const double y0 = acc.row(0), y1 = acc.row(1), y2 = acc.row(2);
+    y[3 * n + 0] = y0;
+    y[3 * n + 1] = y1;
+    y[3 * n + 2] = y2;
+    if (DOT) dot = xc0 * y0 + xc1 * y1 + xc2 * y2;
+  }
+  if (DOT) {
+    const double sm = block_sum<TPB>(dot, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = sm;
   }
 }
 
@@ -3891,9 +4003,16 @@ void spmv_tile(const Ctx& c, int* tx, int* ty, int* kc) {
   }
 }
 
+// exact value-indexed rows on the staged kernel: the boundary-face pass's blocks (their p.w
+// partials follow the z-march's)
+static int64_t faces_blocks(const Ctx& c) {
+  if (!(c.fmt == FMT_VI && c.vi_block && vi_staged(c) && !c.vi_fma)) return 0;
+  return (face_enum(c.g).n + TPB - 1) / TPB;
+}
+
 int64_t spmv_nparts(const Ctx& c) {
   if (c.fmt == FMT_SPLIT && c.dsl.dense) return node_blocks(c);
-  return spmv_grid_blocks(c);
+  return spmv_grid_blocks(c) + faces_blocks(c);
 }
 
 int upload_constants(Ctx& c) {
@@ -4414,7 +4533,7 @@ static void launch_spmv_vi(Ctx& c, const double* xpad, double* y, bool dot, bool
 // the CG iteration's p update fused into the value-indexed SpMV (FP, see FusedP): single rank,
 // block-indexed storage with x staged, Jacobi from the diagonal index, scalar-dictionary patches
 bool fusep(const Ctx& c) {
-  return c.cg_fusep && c.p_pad2 && c.nranks == 1 && !c.comm && !c.lg && c.fmt == FMT_VI && c.vi_block &&
+  return c.cg_fusep && c.vi_fma && c.p_pad2 && c.nranks == 1 && !c.comm && !c.lg && c.fmt == FMT_VI && c.vi_block &&
          !c.vi_nexc && vi_staged(c) && c.cg_dix && c.vi_uni && c.vi_patch;
 }
 
@@ -4520,6 +4639,29 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
         else MCX_VIBM(64, 16, false, false, false);
       }
 #undef MCX_VIBM
+      const int64_t nbf = faces_blocks(c);
+      if (nbf) {  // exact rows: the nodes on the global boundary (skipped by the z-march)
+        const FaceEnum fe = face_enum(c.g);
+        double* pf = c.partials + nb;
+        if (dot && gated && c.vi_nexc)
+          hipLaunchKernelGGL((k_spmv_vib_faces<true, true, true>), dim3(nbf), dim3(TPB), 0, c.stream, c.g, I, c.vi_bdict,
+                             xpad, y, pf, c.cg, fe, c.vi_exc);
+        else if (dot && gated)
+          hipLaunchKernelGGL((k_spmv_vib_faces<true, true, false>), dim3(nbf), dim3(TPB), 0, c.stream, c.g, I,
+                             c.vi_bdict, xpad, y, pf, c.cg, fe, c.vi_exc);
+        else if (dot && c.vi_nexc)
+          hipLaunchKernelGGL((k_spmv_vib_faces<true, false, true>), dim3(nbf), dim3(TPB), 0, c.stream, c.g, I,
+                             c.vi_bdict, xpad, y, pf, c.cg, fe, c.vi_exc);
+        else if (dot)
+          hipLaunchKernelGGL((k_spmv_vib_faces<true, false, false>), dim3(nbf), dim3(TPB), 0, c.stream, c.g, I,
+                             c.vi_bdict, xpad, y, pf, c.cg, fe, c.vi_exc);
+        else if (c.vi_nexc)
+          hipLaunchKernelGGL((k_spmv_vib_faces<false, false, true>), dim3(nbf), dim3(TPB), 0, c.stream, c.g, I,
+                             c.vi_bdict, xpad, y, pf, c.cg, fe, c.vi_exc);
+        else
+          hipLaunchKernelGGL((k_spmv_vib_faces<false, false, false>), dim3(nbf), dim3(TPB), 0, c.stream, c.g, I,
+                             c.vi_bdict, xpad, y, pf, c.cg, fe, c.vi_exc);
+      }
       return;
     }
     if (c.vi_nexc) {
