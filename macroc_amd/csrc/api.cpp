@@ -1497,15 +1497,6 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.vi_ypair = value != 0.;
     return 0;
   }
-  if (!std::strcmp(name, "vi_zs")) {
-    const int v = (int)value;
-    if (!(v == 0 || v == 8 || v == 16) || (double)v != value) {
-      set_error("vi_zs: 0 (k_spmv_vibm), 16 or 8 (k_spmv_vibs tile rows)");
-      return 1;
-    }
-    c.vi_zs = v;
-    return 0;
-  }
   if (!std::strcmp(name, "vi_wmap")) {
     c.vi_wmap = value != 0.;
     return 0;

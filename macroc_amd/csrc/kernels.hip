@@ -2966,236 +2966,6 @@ __global__ __launch_bounds__(TPB) void k_spmv_vib_faces(Geo g, const u32x4* __re
   }
 }
 
-// Value-indexed SpMV marching z by SOURCE plane (option vi_zs = TY, 16 or 8; FMA rows, matrices
-// without exception nodes).  k_spmv_vibm keeps a ring of 3-4 x planes in LDS because a node's 27
-// blocks read x from planes k-1, k and k+1.  Here the tile holds one source plane p (plus the next
-// one streaming in) and every lane adds plane p's terms to three rows kept in registers: node
-// (i,j,p+1) (its dz = -1 blocks, nb 0-8), node p (nb 9-17) and node p-1 (nb 18-26), which is
-// then complete and stored.  A row still receives its terms in nb order, one FMA after another
-// from 0, so y is bit-identical to k_spmv_vibm<FMA>'s.  What changes:
-// - each in-plane neighbour's x is read from LDS once for the three blocks it meets (27
-//   ds_read_b64 per node instead of 81);
-// - the next plane streams into the second LDS buffer by direct-to-LDS loads
-//   (global_load_lds_dwordx4), without staging registers;
-// - two planes + the dictionary (80 KB at TY 16, 53 KB at TY 8) let 2 (3) tiles share a CU: 8 (6)
-//   waves per SIMD instead of 4 to hide the per-group load latency that bounds k_spmv_vibm.
-// A wave takes the scalar-dictionary path when each of its three rows' block indices are the same
-// on all 64 lanes (per node, checked when its indices arrive); else the LDS-dictionary path.
-template <int TY>
-__device__ __forceinline__ void vibs_words(const u32x4* __restrict__ I, int64_t n, u32x4& w0, u32x4& w1) {
-  const u32x4* ip = I + (n >> 6) * (2 * 64) + (n & 63);
-  w0 = __builtin_nontemporal_load(ip);
-  w1 = __builtin_nontemporal_load(ip + 64);
-}
-
-template <bool DOT, bool GATED, int TY>
-__global__ __launch_bounds__(64 * TY) __attribute__((amdgpu_waves_per_eu(TY == 16 ? 8 : 6)))
-void k_spmv_vibs(Geo g, const u32x4* __restrict__ I, const double* __restrict__ bdict, const double* __restrict__ x,
-                 double* __restrict__ y, double* __restrict__ part, const CgState* __restrict__ cg, ZTiling zt) {
-  constexpr int TX = 64, T = TX * TY, RL = vibm_rl<TX, true>(), PR = TY + 2, PLANE = PR * RL;
-  constexpr int NW = T / 64, TYP = TY / 4;
-  static_assert(RL % 2 == 0 && 3 * (TX + 2) <= 256, "two 16-B chunks of 64 lanes per staged row");
-  __shared__ __attribute__((aligned(16))) double xs[2][PLANE];
-  __shared__ double2 tab[VI_MAX * VIB_STRIDE / 2];
-  __shared__ double sh[NW];
-  if (GATED && cg->reason) return;
-  const int b = blockIdx.x;
-  const int xcd = b & 7, t8 = b >> 3;
-  const int slab = (zt.nty + 7) >> 3;
-  const int ty0 = xcd * slab;
-  const int nty_here = min(slab, zt.nty - ty0);
-  const int per = max(nty_here, 0) * zt.ntx * zt.nzc;
-  if (t8 >= per) {  // whole block idle (uniform): still write the partial
-    if (DOT && threadIdx.x == 0) part[blockIdx.x] = 0.;
-    return;
-  }
-  const int txi = t8 % zt.ntx, r8 = t8 / zt.ntx;
-  const int tyi = ty0 + r8 % nty_here, zc = r8 / nty_here;
-  const int i0 = txi * TX, j0 = tyi * TY;
-  const int k0 = zc * zt.kc, k1 = min(g.nz, k0 + zt.kc);
-  const int me = threadIdx.x, wv = me >> 6, ln = me & 63;
-  // 16 x 4 patches, Latin-square SIMD placement (k_spmv_vibm PATCH + wmap)
-  int px = wv % (TX / 16), py = wv / (TX / 16);
-  if (zt.wmap) {
-    py = (wv >> 2) % TYP;
-    px = (wv / (4 * TYP)) * 4 + (((wv & 3) - py) & 3);
-  }
-  const int lx = px * 16 + (ln & 15), ly = py * 4 + (ln >> 4);
-  const int i = i0 + lx, j = j0 + ly;
-  const bool inxy = i < g.nx && j < g.ny;
-  const int PX = g.PX, PXY = g.PX * g.PY;
-  const int len = 3 * min(TX + 2, g.nx + 2 - i0);  // doubles of a staged row inside the padded box
-  const int rows = min(TY + 2, g.ny + 2 - j0);
-  // plane p (-1 .. nz) of the tile into LDS buffer s: row rr = chunk >> 1, 16 B per lane; a wave's
-  // lanes land at consecutive 16 B from the chunk's base (M0), so a row's 1584 B are two chunks
-  constexpr int NCH = (2 * PR + NW - 1) / NW;  // chunks per wave
-  auto stage = [&](int p, int s) {
-    const double* xp = x + 3 * ((int64_t)i0 + (int64_t)j0 * PX + (int64_t)(p + 1) * PXY);
-#pragma unroll
-    for (int m = 0; m < NCH; m++) {
-      const int c = wv + m * NW;  // uniform
-      const int rr = c >> 1, h = c & 1;
-      const int o = h * 128 + 2 * ln;
-      if (c < 2 * PR && rr < rows && o < len)
-        __builtin_amdgcn_global_load_lds((const void*)(xp + 3 * rr * PX + o),
-                                         (__attribute__((address_space(3))) void*)&xs[s][rr * RL + h * 128], 16, 0, 0);
-    }
-  };
-  auto node_of = [&](int k) -> int64_t { return i + g.nx * (j + (int64_t)g.ny * k); };
-  for (int t = me; t < VI_MAX * VIB_STRIDE / 2; t += T) tab[t] = reinterpret_cast<const double2*>(bdict)[t];
-  stage(k0 - 1, 0);
-  // block indices: node p+1's words (hi row), p's (mid), p-1's (lo), as wave-uniform copies where
-  // the node's 64 lanes agree; the per-lane words are re-read by the LDS path
-  u32x4 w0 = {0u, 0u, 0u, 0u}, w1 = w0;
-  if (inxy) vibs_words<TY>(I, node_of(k0), w0, w1);
-  auto uniform_words = [&](const u32x4& a, const u32x4& c, unsigned (&s)[7]) -> bool {
-    unsigned diff = 0u;
-#pragma unroll
-    for (int q = 0; q < 7; q++) {
-      const unsigned v = q < 4 ? a[q] : c[q - 4];
-      s[q] = __builtin_amdgcn_readfirstlane(v);
-      diff |= v ^ s[q];
-    }
-    return __all(inxy && diff == 0u);
-  };
-  unsigned sh_[7], sm_[5] = {0u, 0u, 0u, 0u, 0u}, sl_[3] = {0u, 0u, 0u};
-  bool uh = uniform_words(w0, w1, sh_), um = true, ul = true;
-  double yh0 = 0., yh1 = 0., yh2 = 0., ym0 = 0., ym1 = 0., ym2 = 0., yl0 = 0., yl1 = 0., yl2 = 0.;
-  double xl0 = 0., xl1 = 0., xl2 = 0.;  // own x of node p-1 (the p.w partial)
-  double dot = 0.;
-  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's plane chunks are in LDS
-  __syncthreads();
-  typedef const volatile __attribute__((address_space(3))) double lds_vdouble;
-  for (int p = k0 - 1; p <= k1; p++) {
-    const int s = (p - k0 + 1) & 1;
-    if (p + 1 <= k1) stage(p + 1, s ^ 1);
-    const bool nxt = p + 2 < k1;  // node p+2 becomes the hi row of plane p+1
-    // rows in flight: hi = node p+1 (< k1), mid = node p (>= k0, < k1), lo = node p-1 (>= k0)
-    const bool vh = p + 1 < k1, vm = p >= k0 && p < k1, vl = p - 1 >= k0;
-    lds_vdouble* xsv = (lds_vdouble*)&xs[s][0];
-    const bool uni = (!vh || uh) && (!vm || um) && (!vl || ul);
-    if (uni) {
-      // per in-plane neighbour q = (dy, dx): its x once, then the three rows' blocks (nb q, 9+q,
-      // 18+q): values 0-7 by one s_load_dwordx16 each, value 8 from the LDS copy; the three
-      // blocks' loads go out together and are waited for once
-#pragma unroll
-      for (int q = 0; q < 9; q++) {
-        const int dx = q % 3 - 1, dy = q / 3 - 1;
-        lds_vdouble* xp = xsv + (ly + 1 + dy) * RL + 3 * (lx + 1 + dx);
-        const double xv0 = xp[0], xv1 = xp[1], xv2 = xp[2];
-        const int nbh = q, nbm = 9 + q, nbl = 18 + q;
-        const unsigned idh = (sh_[nbh >> 2] >> (8 * (nbh & 3))) & 255u;
-        const unsigned idm = (sm_[(nbm >> 2) - 2] >> (8 * (nbm & 3))) & 255u;
-        const unsigned idl = (sl_[(nbl >> 2) - 4] >> (8 * (nbl & 3))) & 255u;
-        double ah[9], am[9], al[9];
-        const double* eh = bdict + idh * VIB_STRIDE;
-        const double* em = bdict + idm * VIB_STRIDE;
-        const double* el = bdict + idl * VIB_STRIDE;
-#pragma unroll
-        for (int v = 0; v < 8; v++) ah[v] = eh[v];
-#pragma unroll
-        for (int v = 0; v < 8; v++) am[v] = em[v];
-#pragma unroll
-        for (int v = 0; v < 8; v++) al[v] = el[v];
-        ah[8] = reinterpret_cast<const double*>(tab + idh * (VIB_STRIDE / 2))[8];
-        am[8] = reinterpret_cast<const double*>(tab + idm * (VIB_STRIDE / 2))[8];
-        al[8] = reinterpret_cast<const double*>(tab + idl * (VIB_STRIDE / 2))[8];
-        __builtin_amdgcn_sched_barrier(0);
-        yh0 = __builtin_fma(ah[0], xv0, yh0); yh0 = __builtin_fma(ah[1], xv1, yh0); yh0 = __builtin_fma(ah[2], xv2, yh0);
-        yh1 = __builtin_fma(ah[3], xv0, yh1); yh1 = __builtin_fma(ah[4], xv1, yh1); yh1 = __builtin_fma(ah[5], xv2, yh1);
-        yh2 = __builtin_fma(ah[6], xv0, yh2); yh2 = __builtin_fma(ah[7], xv1, yh2); yh2 = __builtin_fma(ah[8], xv2, yh2);
-        ym0 = __builtin_fma(am[0], xv0, ym0); ym0 = __builtin_fma(am[1], xv1, ym0); ym0 = __builtin_fma(am[2], xv2, ym0);
-        ym1 = __builtin_fma(am[3], xv0, ym1); ym1 = __builtin_fma(am[4], xv1, ym1); ym1 = __builtin_fma(am[5], xv2, ym1);
-        ym2 = __builtin_fma(am[6], xv0, ym2); ym2 = __builtin_fma(am[7], xv1, ym2); ym2 = __builtin_fma(am[8], xv2, ym2);
-        yl0 = __builtin_fma(al[0], xv0, yl0); yl0 = __builtin_fma(al[1], xv1, yl0); yl0 = __builtin_fma(al[2], xv2, yl0);
-        yl1 = __builtin_fma(al[3], xv0, yl1); yl1 = __builtin_fma(al[4], xv1, yl1); yl1 = __builtin_fma(al[5], xv2, yl1);
-        yl2 = __builtin_fma(al[6], xv0, yl2); yl2 = __builtin_fma(al[7], xv1, yl2); yl2 = __builtin_fma(al[8], xv2, yl2);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    } else {
-      // LDS-dictionary path, one row at a time (its nine index bytes re-read as the words
-      // covering them; each neighbour's x read again per row: these waves are the few at the
-      // domain boundary and Dirichlet neighbours)
-#pragma unroll 1
-      for (int r3 = 0; r3 < 3; r3++) {
-        const int pk = p + 1 - r3;  // hi: node p+1, mid: node p, lo: node p-1
-        const bool val = r3 == 0 ? vh : (r3 == 1 ? vm : vl);
-        if (!val) continue;  // uniform
-        // words 2 r3 .. 2 r3 + 2 hold the row's index bytes 9 r3 .. 9 r3 + 8, at byte r3 + q
-        unsigned long long wlo = 0ull;
-        unsigned whi = 0u;
-        if (inxy) {
-          const int64_t n = node_of(pk);
-          const unsigned* ip = reinterpret_cast<const unsigned*>(I + (n >> 6) * (2 * 64) + (n & 63));
-          auto word = [&](int wi) { return ip[(wi >> 2) * 256 + (wi & 3)]; };
-          wlo = (unsigned long long)word(2 * r3) | ((unsigned long long)word(2 * r3 + 1) << 32);
-          whi = word(2 * r3 + 2);
-        }
-        // the row's chain continues (a hi row starts here from 0)
-        double z0 = r3 == 0 ? yh0 : (r3 == 1 ? ym0 : yl0);
-        double z1 = r3 == 0 ? yh1 : (r3 == 1 ? ym1 : yl1);
-        double z2 = r3 == 0 ? yh2 : (r3 == 1 ? ym2 : yl2);
-#pragma unroll
-        for (int q = 0; q < 9; q++) {
-          const int dx = q % 3 - 1, dy = q / 3 - 1;
-          lds_vdouble* xp = xsv + (ly + 1 + dy) * RL + 3 * (lx + 1 + dx);
-          const double xv0 = xp[0], xv1 = xp[1], xv2 = xp[2];
-          const int bq = r3 + q;
-          const unsigned id = (bq < 8 ? (unsigned)(wlo >> (8 * bq)) : whi >> (8 * (bq - 8))) & 255u;
-          const double2* e = tab + id * (VIB_STRIDE / 2);
-          const double2 a01 = e[0], a23 = e[1], a45 = e[2], a67 = e[3];
-          const double a8 = reinterpret_cast<const double*>(e)[8];
-          z0 = __builtin_fma(a01.x, xv0, z0); z0 = __builtin_fma(a01.y, xv1, z0); z0 = __builtin_fma(a23.x, xv2, z0);
-          z1 = __builtin_fma(a23.y, xv0, z1); z1 = __builtin_fma(a45.x, xv1, z1); z1 = __builtin_fma(a45.y, xv2, z1);
-          z2 = __builtin_fma(a67.x, xv0, z2); z2 = __builtin_fma(a67.y, xv1, z2); z2 = __builtin_fma(a8, xv2, z2);
-          __builtin_amdgcn_sched_barrier(0);  // one neighbour's reads at a time (registers)
-        }
-        if (r3 == 0) {
-          yh0 = z0; yh1 = z1; yh2 = z2;
-        } else if (r3 == 1) {
-          ym0 = z0; ym1 = z1; ym2 = z2;
-        } else {
-          yl0 = z0; yl1 = z1; yl2 = z2;
-        }
-      }
-    }
-    // node p+2's indices (the hi row of the next plane), loaded here rather than a plane ahead: 8
-    // registers less across the plane, the latency hidden by the CU's other tiles
-    u32x4 n0 = {0u, 0u, 0u, 0u}, n1 = n0;
-    if (nxt && inxy) vibs_words<TY>(I, node_of(p + 2), n0, n1);
-    if (vl && inxy) {  // node p-1 complete
-      const int64_t n = node_of(p - 1);
-      __builtin_nontemporal_store(yl0, &y[3 * n + 0]);
-      __builtin_nontemporal_store(yl1, &y[3 * n + 1]);
-      __builtin_nontemporal_store(yl2, &y[3 * n + 2]);
-      if (DOT) dot += xl0 * yl0 + xl1 * yl1 + xl2 * yl2;
-    }
-    {  // own x of node p, for its p.w term after the next plane
-      lds_vdouble* xp = xsv + (ly + 1) * RL + 3 * (lx + 1);
-      xl0 = xp[0];
-      xl1 = xp[1];
-      xl2 = xp[2];
-    }
-    // rotate the rows and their indices: lo <- mid <- hi <- node p+2
-    yl0 = ym0; yl1 = ym1; yl2 = ym2;
-    ym0 = yh0; ym1 = yh1; ym2 = yh2;
-    yh0 = yh1 = yh2 = 0.;
-#pragma unroll
-    for (int q = 0; q < 3; q++) sl_[q] = sm_[q + 2];
-#pragma unroll
-    for (int q = 0; q < 5; q++) sm_[q] = sh_[q + 2];
-    ul = um;
-    um = uh;
-    if (nxt) uh = uniform_words(n0, n1, sh_);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): plane p+1's chunks of this wave have landed
-    __syncthreads();
-  }
-  if (DOT) {
-    const double sm = block_sum<T>(dot, sh);
-    if (threadIdx.x == 0) part[blockIdx.x] = sm;
-  }
-}
-
 // y = A x on FMT_VI with x staged in LDS, z-marching.  k_spmv_vi's 81 x gathers per node (8 B
 // at a 24-B lane stride: a third of every fetched line used) are a third of its time
 // (profiles/r02_vi_dbg.log: 1.14 ms, 0.78 without them); staging one plane per block and launch
@@ -4178,19 +3948,7 @@ static void split_shape(const Ctx& c, int& ztx, int& zty) {
 // 128^3 0.0563 vs 0.0589 ms (128x8) per SpMV (profiles/r03_ab_tx{256b,128}.log): a third less
 // halo than 256x4 (66x18 staged nodes per 1024 instead of 258x6), and tiles away from the x
 // faces have no wave that reads the dictionary from LDS.  Option vi_tx selects 256x4 / 128x8.
-// k_spmv_vibs (option vi_zs): FMA rows, no exception nodes, scalar-dictionary patches, 64-wide
-// tiles, an even nx (16-B aligned staged rows), and not the fused p update (its own tiles)
-static bool vibs_on(const Ctx& c) {
-  return (c.vi_zs == 16 || c.vi_zs == 8) && c.fmt == FMT_VI && c.vi_block && c.vi_fma && !c.vi_nexc && c.vi_uni &&
-         c.vi_patch && !c.cg_fusep && c.vi_tx != 128 && c.vi_tx != 256 && c.g.nx % 2 == 0;
-}
-
 static void vis_shape(const Ctx& c, int& tx, int& ty) {
-  if (vibs_on(c)) {
-    tx = 64;
-    ty = c.vi_zs;
-    return;
-  }
   tx = 64;
   if (c.vi_tx == 256 || c.vi_tx == 128 || c.vi_tx == 64) tx = c.vi_tx;
   ty = 1024 / tx;
@@ -4202,9 +3960,7 @@ static ZTiling vis_tiling(const Ctx& c) {
   ZTiling t;
   t.ntx = (c.g.nx + tx - 1) / tx;
   t.nty = (c.g.ny + ty - 1) / ty;
-  // k_spmv_vibs: 2 (TY 16) or 3 (TY 8) tiles per CU
-  const int bpc = vibs_on(c) ? (c.vi_zs == 16 ? 2 : 3) : 1;
-  const int tiles = t.ntx * t.nty, want = c.spmv_zblocks > 0 ? c.spmv_zblocks : bpc * c.g.ncu;
+  const int tiles = t.ntx * t.nty, want = c.spmv_zblocks > 0 ? c.spmv_zblocks : c.g.ncu;
   t.nzc = std::max(1, std::min(c.g.nz, (want + tiles - 1) / tiles));
   t.kc = (c.g.nz + t.nzc - 1) / t.nzc;
   t.nzc = (c.g.nz + t.kc - 1) / t.kc;
@@ -4833,24 +4589,6 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
       hipLaunchKernelGGL((k_spmv_vibm<false, false, TXV, TYV, XVV, UV, PV, ##__VA_ARGS__>), dim3(nb), dim3(1024), 0,      \
                          c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt);                             \
   } while (0)
-      if (vibs_on(c)) {  // marching by source plane
-#define MCX_VIBS(TYV)                                                                                               \
-  do {                                                                                                             \
-    if (dot && gated)                                                                                              \
-      hipLaunchKernelGGL((k_spmv_vibs<true, true, TYV>), dim3(nb), dim3(64 * TYV), 0, c.stream, c.g, I, c.vi_bdict, \
-                         xpad, y, c.partials, c.cg, zt);                                                           \
-    else if (dot)                                                                                                  \
-      hipLaunchKernelGGL((k_spmv_vibs<true, false, TYV>), dim3(nb), dim3(64 * TYV), 0, c.stream, c.g, I, c.vi_bdict, \
-                         xpad, y, c.partials, c.cg, zt);                                                           \
-    else                                                                                                           \
-      hipLaunchKernelGGL((k_spmv_vibs<false, false, TYV>), dim3(nb), dim3(64 * TYV), 0, c.stream, c.g, I,           \
-                         c.vi_bdict, xpad, y, c.partials, c.cg, zt);                                               \
-  } while (0)
-        if (ty == 16) MCX_VIBS(16);
-        else MCX_VIBS(8);
-#undef MCX_VIBS
-        return;
-      }
       if (c.vi_nexc) {  // exception nodes: the default (FMA) or exact rows, UNI + PATCH
 #define MCX_VIBM_X(TXV, TYV, FV)                                                                                    \
   do {                                                                                                             \

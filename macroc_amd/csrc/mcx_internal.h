@@ -221,7 +221,6 @@ struct Ctx {
   int vi_tx = 0;             // staged block-indexed SpMV tile width 256 | 128 | 64 (0: 64; option vi_tx)
   int vi_uni = 1;            // staged block-indexed SpMV: wave-uniform blocks from scalar loads (option vi_uni)
   int vi_ypair = 0;          // with vi_uni: y of lane pairs as 16-B stores (option vi_ypair; A/B)
-  int vi_zs = 0;             // FMA rows: the SpMV marching by source plane, k_spmv_vibs, 64 x vi_zs tiles (16 | 8; 0: k_spmv_vibm)
   int vi_xread = 1;          // staged block-indexed SpMV: x as unpaired 8-B LDS reads (option vi_xread; 0: compiler's pairs)
   int vi_stage = -1;         // FMT_VI SpMV: 1 = x staged in LDS, z-marching tiles; 0 = x gathered; -1 = by grid (vi_staged)
   bool vi_declined = false;  // a per-GP-tangent law overflowed the dictionary: skip the attempt

@@ -714,56 +714,6 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
 
 
 
-@pytest.mark.parametrize("vi_zs", [16, 8])
-@pytest.mark.parametrize("NX,NY,NZ", [(260, 6, 5), (130, 9, 6), (70, 20, 7), (64, 33, 9)])
-def test_aij_vi_source_plane_march(NX, NY, NZ, vi_zs):
-    """Option vi_zs (k_spmv_vibs: the z-march by source plane, two LDS planes, 64 x vi_zs tiles,
-    2-3 tiles per CU): every row gets its 27 block terms in the same nb order of fused
-    multiply-adds as k_spmv_vibm<FMA>, so y is bitwise the default kernel's for every z-chunking
-    (chunk-edge planes, partial tiles in x and y, boundary and Dirichlet-neighbour waves on the
-    LDS-dictionary path); within 1e-14 sum|a||x| of the CPU AIJ order; the CG solve (its p.w
-    partials come from other tiles) within the north-star bar."""
-    rtol = 1e-12
-    P = O.Problem(NX, NY, NZ, rtol=rtol)
-    with M.Macroc(argv_for(NX, NY, NZ, rtol)) as m:
-        m.set_option("vi_stage", 1)
-        for ts in (0, 1):
-            m.apply_bc_on_u(m.get_displacement(ts))
-            P.apply_bc_u(P.get_displacement(ts))
-        m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
-        P.set_strains(); P.homogenize(); P.assembly_res(); P.assembly_jac()
-        assert m.get_info()["storage"] == 3
-        rp, ci, v = m.dump_csr()
-        x = np.random.default_rng(23).uniform(-1, 1, m.n)
-        y_ref = P.spmv(x)
-        absrow = np.add.reduceat(np.abs(v) * np.abs(x[ci]), rp[:-1])
-        for zblocks in (0, 1, 2, 3 * NZ):
-            m.set_option("spmv_zblocks", zblocks)
-            m.set_option("vi_zs", 0)
-            y0 = m.spmv(x)
-            m.set_option("vi_zs", vi_zs)
-            info = m.get_info()
-            assert (info["spmv_tx"], info["spmv_ty"]) == (64, vi_zs), info
-            y1 = m.spmv(x)
-            assert np.array_equal(y1, y0), (zblocks, np.max(np.abs(y1 - y0)))
-            assert np.all(np.abs(y1 - y_ref) <= 1e-14 * absrow + 1e-300), zblocks
-        m.set_option("spmv_zblocks", 0)
-        its, rn, reason = m.solve_Ax()
-        out = P.solve()
-        assert reason == out["reason"] and abs(its - out["its"]) <= 1
-        assert np.linalg.norm(m.du() - P.du()) <= 1e-10 * np.linalg.norm(P.du())
-
-
-def test_vi_zs_option_refused():
-    """vi_zs takes 0, 16 or 8 only; a refused value leaves the kernel choice as it was."""
-    with M.Macroc(argv_for(16, 16, 16, 1e-8)) as m:
-        with pytest.raises(M.MacrocError):
-            m.set_option("vi_zs", 4)
-        m.set_option("vi_zs", 16)
-        with pytest.raises(M.MacrocError):
-            m.set_option("vi_zs", 12)
-
-
 @pytest.mark.parametrize("maxits", [None, 37, 38, 39, 40, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("storage", ["vi", "vi_staged", "split"])
 def test_cg_pdb_bitwise(maxits, storage):
