@@ -56,7 +56,7 @@ static int free_ctx(Ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
-  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
+  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->wd, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
                   c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2, c->p_pad3, c->p_pad4, c->xdone, c->esc_node, c->esc_res, c->esc_slot, c->elem_plain, c->cref, c->vi_xslot,
                   c->vi_xlist, c->vi_exc,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
@@ -829,6 +829,7 @@ int mcx_assembly_jac(void* ctx) {
     if ((rc = ensure_VI(c)) || (rc = build_vi(c, &ok))) return rc;
     if (ok) {
       c.fmt = FMT_VI;
+      if ((rc = build_wdesc(c))) return rc;
       c.assembled = true;
       MCX_HIP(hipGetLastError());
       return 0;
@@ -1375,6 +1376,10 @@ int mcx_get_timing(void* ctx, mcx_timing* t) {
       2 * 3 * (int64_t)c.g.nown * 8;
   if (c.fmt == FMT_SPLIT) t->spmv_bytes_per_launch += (int64_t)c.g.nown * c.dsl.Lq * 16;
   if (c.fmt == FMT_VI && c.vi_block) t->spmv_bytes_per_launch += c.vi_nexc * 27 * 9 * 8;  // exception blocks
+  if (wd_used(c)) {  // wave descriptors: 32 B per wave and plane, index bytes for the waves that are not uniform only
+    const int64_t nwp = (int64_t)c.wd_npx * c.wd_npy * c.g.nz;
+    t->spmv_bytes_per_launch += nwp * 32 - c.nnz_local / 9 + (c.vi_fma ? c.wd_blocks_fma : c.wd_blocks_exact);
+  }
   // the fused p update (cg_fusep): r and the diagonal index read, p(i) written
   if (c.fusep_used) t->spmv_bytes_per_launch += (int64_t)c.g.nown * (24 + 1 + 24);
   return 0;
@@ -1491,6 +1496,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
   if (!std::strcmp(name, "split_esc")) {  // takes effect at the next mcx_assembly_jac
     c.split_esc = value != 0.;
     c.split_declined = false;
+    return 0;
+  }
+  if (!std::strcmp(name, "vi_wdesc")) {
+    c.vi_wdesc = value != 0.;
     return 0;
   }
   if (!std::strcmp(name, "vi_ypair")) {

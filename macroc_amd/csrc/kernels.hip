@@ -1064,6 +1064,8 @@ struct ZTiling {
   int wmap = 1;           // k_spmv_vibm PATCH: 1 = patches on SIMDs as a Latin square, 0 = row-major (A/B)
   int xlist = VI_EXC_LIST;  // k_spmv_vibm EXC: exception nodes a tile defers (option vi_exc_list; the rest in their plane)
   int ypair = 0;          // k_spmv_vibm UNI: y of lane pairs as 16-B stores (option vi_ypair; needs an even nx)
+  const unsigned* wd = nullptr;  // k_spmv_vibm WD: the wave descriptors (build_wdesc), npx x npy 16 x 4 patches per plane
+  int npx = 0, npy = 0;
 };
 
 static ZTiling z_tiling(const Geo& g, int ztx, int zty, int want) {
@@ -2400,7 +2402,7 @@ constexpr int vibm_rl() {
 }
 
 template <bool DOT, bool GATED, int TX, int TY, bool XV = true, bool UNI = false, bool PATCH = false, bool FMA = false,
-          bool FP = false, bool RING3 = false, bool EXC = false>
+          bool FP = false, bool RING3 = false, bool EXC = false, bool WD = false>
 __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __restrict__ I,
                                                        const double* __restrict__ bdict, const double* __restrict__ x,
                                                        double* __restrict__ y, double* __restrict__ part,
@@ -2473,6 +2475,16 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
   const int i = i0 + lx, j = j0 + ly;
   const bool inxy = i < g.nx && j < g.ny;
   const int PX = g.PX, PXY = g.PX * g.PY;
+  // WD: this wave's 16 x 4 patch in the descriptor grid (a patch wholly outside the domain has
+  // none: its planes count as not uniform, and its lanes compute nothing)
+  static_assert(!WD || (UNI && PATCH && !FP && !EXC), "wave descriptors: the scalar-dictionary patch kernels");
+  const int gpx = (i0 + (lx & ~15)) >> 4, gpy = (j0 + (ly & ~3)) >> 2;  // (wave-uniform)
+  const bool wdv = WD && gpx < zt.npx && gpy < zt.npy;
+  // lane ln holds descriptor word ln & 7 of plane k: [flags, the 7 index words]
+  auto dload = [&](int k) -> unsigned {
+    if (!wdv || k >= k1) return 0u;
+    return __builtin_nontemporal_load(zt.wd + ((((int64_t)k * zt.npy + gpy) * zt.npx + gpx) << 3) + (me & 7));
+  };
   const int len = 3 * min(TX + 2, g.nx + 2 - i0);  // doubles of a staged row that exist in the padded box
   const int rows = min(TY + 2, g.ny + 2 - j0);      // staged rows (j0-1 ..) that exist (padded j <= ny)
   auto xload = [&](int p, int m) -> double {        // x of node plane p (-1 .. nz), staged element me + m T
@@ -2556,13 +2568,24 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
   const int wcap = EXC ? min(SEG, (min(XL, zt.xlist) + NW - 1) / NW) : 0;
   int wn = 0;
   u32x4 c0 = {0u, 0u, 0u, 0u}, c1 = c0, n0 = c0, n1 = c0;
-  iload(k0, c0, c1);
+  // WD: descriptors of planes k and k+1 (dc, dn); a plane's per-lane index words are loaded only
+  // where its descriptor says the wave is not uniform
+  unsigned dc = 0u, dn = 0u;
+  auto wflag = [&](unsigned d) -> unsigned { return (unsigned)__builtin_amdgcn_readlane((int)d, 0); };
+  if (WD) {
+    dc = dload(k0);
+    dn = dload(k0 + 1);
+    if (!wdv || !(wflag(dc) & 1u)) iload(k0, c0, c1);
+  } else {
+    iload(k0, c0, c1);
+  }
   __syncthreads();
   double dot = 0.;
   for (int k = k0; k < k1; k++) {
     const bool more = k + 1 < k1;
     double xr[FP ? 1 : NL];
     Fe fe[FP ? NL : 1];
+    unsigned dn2 = 0u;
     if (more) {  // in flight during this plane: x (p) of plane k+2, indices of plane k+1
       if (FP) {
 #pragma unroll
@@ -2571,7 +2594,12 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
 #pragma unroll
         for (int m = 0; m < NL; m++) xr[m] = xload(k + 2, m);
       }
-      iload(k + 1, n0, n1);
+      if (WD) {
+        dn2 = dload(k + 2);
+        if (!wdv || !(wflag(dn) & 1u)) iload(k + 1, n0, n1);  // (uniform)
+      } else {
+        iload(k + 1, n0, n1);
+      }
     }
     // UNI: a wave whose 64 nodes have the same 27 block indices (interior x-lines: no domain
     // boundary, no Dirichlet neighbour) reads the block values with scalar loads (s_load from
@@ -2585,7 +2613,14 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
     const bool full = FMA || present_mask(g, i, j, k) == PRES_ALL;
     unsigned sw[7] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
     bool uni = false;
-    if (UNI) {
+    if (WD) {
+      // the descriptor: bit 0 = the 64 lanes are in the domain with the same 27 block indices
+      // (words 1-7), bit 1 = every lane has all 27 neighbours (exact rows need it)
+      const unsigned f = wdv ? wflag(dc) : 0u;
+#pragma unroll
+      for (int q = 0; q < 7; q++) sw[q] = (unsigned)__builtin_amdgcn_readlane((int)dc, q + 1);
+      uni = (FMA ? (f & 1u) != 0u : f == 3u) || (zt.dbg & 1);
+    } else if (UNI) {
 #pragma unroll
       for (int q = 0; q < 7; q++) sw[q] = __builtin_amdgcn_readfirstlane(q < 4 ? c0[q] : c1[q - 4]);
       unsigned diff = 0u;
@@ -2789,6 +2824,10 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       }
       c0 = n0;
       c1 = n1;
+      if (WD) {
+        dc = dn;
+        dn = dn2;
+      }
       __syncthreads();
     }
   }
@@ -4352,6 +4391,94 @@ static int build_vib(Ctx& c, bool* ok) {
   return 0;
 }
 
+// Wave descriptors of the block-indexed storage (k_spmv_vibm WD): one per 16 x 4 node patch and
+// plane (the node set of one wave of the staged SpMV, whatever the tile shape), 8 words: flags
+// (bit 0: the 64 nodes are in the domain, not exception nodes, with the same 27 block indices;
+// bit 1: each has all 27 neighbours) and the patch's first node's 7 index words.  A uniform wave
+// then reads its block indices from these 32 B (one coalesced load, scalar registers by
+// v_readlane) instead of 32 B per node; the others load their nodes' words as before.  ctr[0] /
+// ctr[1] count the present blocks of the nodes in waves that are not uniform (FMA rows / exact
+// rows): the index bytes the SpMV still reads per node.
+__global__ __launch_bounds__(TPB) void k_vi_wdesc(Geo g, const u32x4* __restrict__ I, unsigned* __restrict__ D,
+                                                  int npx, int npy, unsigned long long* __restrict__ ctr) {
+  const int64_t w = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  const int ln = threadIdx.x & 63;
+  if (w >= (int64_t)npx * npy * g.nz) return;  // (whole wave)
+  const int px = (int)(w % npx);
+  const int64_t r = w / npx;
+  const int py = (int)(r % npy), k = (int)(r / npy);
+  const int i = px * 16 + (ln & 15), j = py * 4 + (ln >> 4);
+  const bool inxy = i < g.nx && j < g.ny;
+  u32x4 w0 = {0u, 0u, 0u, 0u}, w1 = w0;
+  unsigned pres = 0u;
+  if (inxy) {
+    const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
+    const u32x4* ip = I + (n >> 6) * (2 * 64) + (n & 63);
+    w0 = ip[0];
+    w1 = ip[64];
+    pres = present_mask(g, i, j, k);
+  }
+  unsigned sw[7], diff = 0u;
+#pragma unroll
+  for (int q = 0; q < 7; q++) {
+    const unsigned v = q < 4 ? w0[q] : w1[q - 4];
+    sw[q] = __builtin_amdgcn_readfirstlane(v);
+    diff |= v ^ sw[q];
+  }
+  const bool uni = __all(inxy && diff == 0u && w1[3] == 0u);
+  const bool full = __all(inxy && pres == PRES_ALL);
+  if (ln < 8) {
+    unsigned v = (uni ? 1u : 0u) | (full ? 2u : 0u);
+#pragma unroll
+    for (int q = 0; q < 7; q++)
+      if (ln == q + 1) v = sw[q];
+    D[(w << 3) + ln] = v;
+  }
+  const double nbl = wave_sum((double)__popc(pres));
+  if (ln == 0) {
+    if (!uni) atomicAdd(&ctr[0], (unsigned long long)nbl);
+    if (!(uni && full)) atomicAdd(&ctr[1], (unsigned long long)nbl);
+  }
+}
+
+int build_wdesc(Ctx& c) {
+  c.wd_ok = false;
+  if (!(c.fmt == FMT_VI && c.vi_block)) return 0;
+  const int npx = (c.g.nx + 15) / 16, npy = (c.g.ny + 3) / 4;
+  const int64_t nw = (int64_t)npx * npy * c.g.nz;
+  const int64_t bytes = nw * 8 * sizeof(unsigned) + 2 * sizeof(unsigned long long);
+  if (bytes > c.wd_bytes) {
+    if (c.wd) {
+      MCX_HIP(hipFree(c.wd));
+      c.device_bytes -= c.wd_bytes;
+      c.wd = nullptr;
+    }
+    MCX_HIP(hipMalloc(&c.wd, bytes));
+    c.wd_bytes = bytes;
+    c.device_bytes += bytes;
+  }
+  unsigned long long* ctr = reinterpret_cast<unsigned long long*>(c.wd + nw * 8);
+  MCX_HIP(hipMemsetAsync(ctr, 0, 2 * sizeof(unsigned long long), c.stream));
+  hipLaunchKernelGGL(k_vi_wdesc, dim3((unsigned)((nw + TPB / 64 - 1) / (TPB / 64))), dim3(TPB), 0, c.stream, c.g,
+                     reinterpret_cast<const u32x4*>(c.vi_idx), c.wd, npx, npy, ctr);
+  unsigned long long h[2];
+  MCX_HIP(hipMemcpyAsync(h, ctr, sizeof(h), hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  c.wd_npx = npx;
+  c.wd_npy = npy;
+  c.wd_blocks_fma = (int64_t)h[0];
+  c.wd_blocks_exact = (int64_t)h[1];
+  c.wd_ok = true;
+  return 0;
+}
+
+// the staged SpMV reads the wave descriptors (option vi_wdesc): block-indexed storage without
+// exception nodes, scalar-dictionary patches, not the fused p update
+bool wd_used(const Ctx& c) {
+  return c.vi_wdesc && c.wd_ok && c.fmt == FMT_VI && c.vi_block && !c.vi_nexc && c.vi_uni && c.vi_patch &&
+         vi_staged(c) && !fusep(c);
+}
+
 int build_vi(Ctx& c, bool* ok) {
   *ok = false;
   if (c.vi_block_on && c.vi_bits_max == 4 && c.vib_onepass) {
@@ -4615,6 +4742,19 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
           else MCX_VIBM_X(64, 16, false);
         }
 #undef MCX_VIBM_X
+      } else if (wd_used(c) && !(c.vi_fma && c.vi_ring3)) {  // wave descriptors
+        zt.wd = c.wd;
+        zt.npx = c.wd_npx;
+        zt.npy = c.wd_npy;
+        if (c.vi_fma) {
+          if (tx == 256) MCX_VIBM(256, 4, true, true, true, true, false, false, false, true);
+          else if (tx == 128) MCX_VIBM(128, 8, true, true, true, true, false, false, false, true);
+          else MCX_VIBM(64, 16, true, true, true, true, false, false, false, true);
+        } else {
+          if (tx == 256) MCX_VIBM(256, 4, true, true, true, false, false, false, false, true);
+          else if (tx == 128) MCX_VIBM(128, 8, true, true, true, false, false, false, false, true);
+          else MCX_VIBM(64, 16, true, true, true, false, false, false, false, true);
+        }
       } else if (c.vi_fma && c.vi_ring3 && tx == 64) {
         MCX_VIBM(64, 16, true, true, true, true, false, true);
       } else if (c.vi_fma) {
