@@ -1376,9 +1376,10 @@ int mcx_get_timing(void* ctx, mcx_timing* t) {
       2 * 3 * (int64_t)c.g.nown * 8;
   if (c.fmt == FMT_SPLIT) t->spmv_bytes_per_launch += (int64_t)c.g.nown * c.dsl.Lq * 16;
   if (c.fmt == FMT_VI && c.vi_block) t->spmv_bytes_per_launch += c.vi_nexc * 27 * 9 * 8;  // exception blocks
-  if (wd_used(c)) {  // wave descriptors: 32 B per wave and plane, index bytes for the waves that are not uniform only
+  if (wd_used(c)) {  // wave descriptors: 128 B per wave and plane, index bytes for the waves that still read per-lane words
     const int64_t nwp = (int64_t)c.wd_npx * c.wd_npy * c.g.nz;
-    t->spmv_bytes_per_launch += nwp * 32 - c.nnz_local / 9 + (c.vi_fma ? c.wd_blocks_fma : c.wd_blocks_exact);
+    t->spmv_bytes_per_launch += nwp * 128 - c.nnz_local / 9 +
+                                (!c.vi_fma ? c.wd_blocks_exact : c.vi_wdesc == 2 ? c.wd_blocks_two : c.wd_blocks_fma);
   }
   // the fused p update (cg_fusep): r and the diagonal index read, p(i) written
   if (c.fusep_used) t->spmv_bytes_per_launch += (int64_t)c.g.nown * (24 + 1 + 24);
@@ -1499,7 +1500,11 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     return 0;
   }
   if (!std::strcmp(name, "vi_wdesc")) {
-    c.vi_wdesc = value != 0.;
+    if (!(value == 0. || value == 1. || value == 2.)) {
+      set_error("vi_wdesc: 0, 1 or 2");
+      return 1;
+    }
+    c.vi_wdesc = (int)value;
     return 0;
   }
   if (!std::strcmp(name, "vi_ypair")) {

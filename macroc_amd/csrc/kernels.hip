@@ -1066,6 +1066,7 @@ struct ZTiling {
   int ypair = 0;          // k_spmv_vibm UNI: y of lane pairs as 16-B stores (option vi_ypair; needs an even nx)
   const unsigned* wd = nullptr;  // k_spmv_vibm WD: the wave descriptors (build_wdesc), npx x npy 16 x 4 patches per plane
   int npx = 0, npy = 0;
+  int wdm = 1;                   // WD: 1 = uniform waves, 2 = also two-set waves (FMA rows; option vi_wdesc)
 };
 
 static ZTiling z_tiling(const Geo& g, int ztx, int zty, int want) {
@@ -2480,11 +2481,13 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
   static_assert(!WD || (UNI && PATCH && !FP && !EXC), "wave descriptors: the scalar-dictionary patch kernels");
   const int gpx = (i0 + (lx & ~15)) >> 4, gpy = (j0 + (ly & ~3)) >> 2;  // (wave-uniform)
   const bool wdv = WD && gpx < zt.npx && gpy < zt.npy;
-  // lane ln holds descriptor word ln & 7 of plane k: [flags, the 7 index words]
+  // lane ln holds descriptor word ln & 31 of plane k (build_wdesc's layout)
   auto dload = [&](int k) -> unsigned {
     if (!wdv || k >= k1) return 0u;
-    return __builtin_nontemporal_load(zt.wd + ((((int64_t)k * zt.npy + gpy) * zt.npx + gpx) << 3) + (me & 7));
+    return __builtin_nontemporal_load(zt.wd + ((((int64_t)k * zt.npy + gpy) * zt.npx + gpx) << 5) + (me & 31));
   };
+  // the planes whose waves skip the per-lane index words: uniform, or (FMA rows, wdm 2) two-set
+  auto wskip = [&](unsigned f) -> bool { return (f & 1u) || (FMA && zt.wdm == 2 && (f & 4u)); };
   const int len = 3 * min(TX + 2, g.nx + 2 - i0);  // doubles of a staged row that exist in the padded box
   const int rows = min(TY + 2, g.ny + 2 - j0);      // staged rows (j0-1 ..) that exist (padded j <= ny)
   auto xload = [&](int p, int m) -> double {        // x of node plane p (-1 .. nz), staged element me + m T
@@ -2575,7 +2578,7 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
   if (WD) {
     dc = dload(k0);
     dn = dload(k0 + 1);
-    if (!wdv || !(wflag(dc) & 1u)) iload(k0, c0, c1);
+    if (!wdv || !wskip(wflag(dc))) iload(k0, c0, c1);
   } else {
     iload(k0, c0, c1);
   }
@@ -2596,7 +2599,7 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       }
       if (WD) {
         dn2 = dload(k + 2);
-        if (!wdv || !(wflag(dn) & 1u)) iload(k + 1, n0, n1);  // (uniform)
+        if (!wdv || !wskip(wflag(dn))) iload(k + 1, n0, n1);  // (uniform)
       } else {
         iload(k + 1, n0, n1);
       }
@@ -2611,15 +2614,25 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
     // after the march, and every row here has all 27 neighbours: the pairing is fixed at compile
     // time (InodeRows<true>) on every path
     const bool full = FMA || present_mask(g, i, j, k) == PRES_ALL;
-    unsigned sw[7] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
-    bool uni = false;
+    unsigned sw[7] = {0u, 0u, 0u, 0u, 0u, 0u, 0u}, sb[7] = {0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    bool uni = false, two = false;
+    unsigned long long mb = 0ull;
     if (WD) {
       // the descriptor: bit 0 = the 64 lanes are in the domain with the same 27 block indices
-      // (words 1-7), bit 1 = every lane has all 27 neighbours (exact rows need it)
+      // (words 1-7), bit 1 = every lane has all 27 neighbours (exact rows need it), bit 2 = the
+      // lanes hold two index sets, the first lane's (words 1-7) and set B (words 8-14) on the
+      // lanes of mask words 16-17
       const unsigned f = wdv ? wflag(dc) : 0u;
 #pragma unroll
       for (int q = 0; q < 7; q++) sw[q] = (unsigned)__builtin_amdgcn_readlane((int)dc, q + 1);
-      uni = (FMA ? (f & 1u) != 0u : f == 3u) || (zt.dbg & 1);
+      uni = (FMA ? (f & 1u) != 0u : (f & 3u) == 3u) || (zt.dbg & 1);
+      two = !uni && FMA && zt.wdm == 2 && (f & 4u);
+      if (two) {
+#pragma unroll
+        for (int q = 0; q < 7; q++) sb[q] = (unsigned)__builtin_amdgcn_readlane((int)dc, q + 8);
+        mb = (unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)dc, 16) |
+             ((unsigned long long)(unsigned)__builtin_amdgcn_readlane((int)dc, 17) << 32);
+      }
     } else if (UNI) {
 #pragma unroll
       for (int q = 0; q < 7; q++) sw[q] = __builtin_amdgcn_readfirstlane(q < 4 ? c0[q] : c1[q - 4]);
@@ -2642,7 +2655,7 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
         wn = min(wcap, wn + (int)__popcll(xm));
       }
     }
-    if (UNI && uni) {  // (every lane is inxy)
+    if (UNI && (uni || two)) {  // (every lane is inxy)
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
       InodeRows<true> acc;  // !FMA: the inode pairs of a node whose 27 neighbours are present
       typedef const volatile __attribute__((address_space(3))) double lds_vdouble;
@@ -2652,6 +2665,9 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       // a load issued ahead of the block in use would be waited for with it)
       // (FP: one block per group, its SGPRs being needed for the fused p update's scalars)
       constexpr int GB = FP ? 1 : 3;
+      // two-set waves (WD): the pass below runs once per set, each lane in its own set's pass
+      // (exec mask), so every row still gets its 27 terms in nb order
+      auto pass = [&](const unsigned (&sw)[7]) {
 #pragma unroll
       for (int nb0 = 0; nb0 < 27; nb0 += GB) {
         double av[GB][9], xv[GB][3];
@@ -2664,8 +2680,9 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
           xv[t][0] = xp[0];
           xv[t][1] = xp[1];
           xv[t][2] = xp[2];
-          const unsigned id = (sw[nb >> 2] >> (8 * (nb & 3))) & 255u;  // wave-uniform
-          const double* e = bdict + id * VIB_STRIDE;                    // values 0-7: one s_load_dwordx16
+          // wave-uniform (readfirstlane: without it the compiler took set B's run for divergent)
+          const unsigned id = __builtin_amdgcn_readfirstlane((sw[nb >> 2] >> (8 * (nb & 3))) & 255u);
+          const double* e = bdict + id * VIB_STRIDE;  // values 0-7: one s_load_dwordx16
 #pragma unroll
           for (int q = 0; q < 8; q++) av[t][q] = e[q];
           // value 8 from the LDS copy (one broadcast ds_read_b64, 2 LDS cycles): an s_load_dwordx2
@@ -2693,6 +2710,19 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
           }
         }
         __builtin_amdgcn_sched_barrier(0);
+      }
+      };
+      pass(sw);
+      if (WD && two) {  // (uniform) set B's run on every lane; the lanes of set A keep their first run's rows
+        // (FMA rows start from 0 in each run; a loop over the sets, or a branch on the lane's set,
+        // made the compiler turn the dictionary's scalar loads into vector loads)
+        const double a0 = y0, a1 = y1, a2 = y2, ax0 = xc0, ax1 = xc1, ax2 = xc2;
+        y0 = y1 = y2 = 0.;
+        pass(sb);
+        if (!((mb >> ln) & 1ull)) {
+          y0 = a0, y1 = a1, y2 = a2;
+          xc0 = ax0, xc1 = ax1, xc2 = ax2;
+        }
       }
       if constexpr (!FMA) y0 = acc.row(0), y1 = acc.row(1), y2 = acc.row(2);
       const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
@@ -4392,13 +4422,16 @@ static int build_vib(Ctx& c, bool* ok) {
 }
 
 // Wave descriptors of the block-indexed storage (k_spmv_vibm WD): one per 16 x 4 node patch and
-// plane (the node set of one wave of the staged SpMV, whatever the tile shape), 8 words: flags
+// plane (the node set of one wave of the staged SpMV, whatever the tile shape), 32 words: flags
 // (bit 0: the 64 nodes are in the domain, not exception nodes, with the same 27 block indices;
-// bit 1: each has all 27 neighbours) and the patch's first node's 7 index words.  A uniform wave
-// then reads its block indices from these 32 B (one coalesced load, scalar registers by
-// v_readlane) instead of 32 B per node; the others load their nodes' words as before.  ctr[0] /
-// ctr[1] count the present blocks of the nodes in waves that are not uniform (FMA rows / exact
-// rows): the index bytes the SpMV still reads per node.
+// bit 1: each has all 27 neighbours; bit 2: not uniform, but every node holds one of two index
+// sets), the patch's first node's 7 index words (set A), set B's 7 words, and the lane mask of
+// set B.  Such a wave then reads its block indices from this descriptor (one coalesced 128-B load,
+// scalar registers by v_readlane) instead of 32 B per node: a uniform wave runs the
+// scalar-dictionary pass once, a two-set wave (an x- or y-face column or row in a patch: FMA
+// rows) once per set under the set's exec mask; the others load their nodes' words as before.
+// ctr[0..2] count the present blocks of the nodes in waves that still read per-lane words (FMA
+// rows with uniform waves only / exact rows / FMA rows with two-set waves).
 __global__ __launch_bounds__(TPB) void k_vi_wdesc(Geo g, const u32x4* __restrict__ I, unsigned* __restrict__ D,
                                                   int npx, int npy, unsigned long long* __restrict__ ctr) {
   const int64_t w = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
@@ -4418,26 +4451,47 @@ __global__ __launch_bounds__(TPB) void k_vi_wdesc(Geo g, const u32x4* __restrict
     w1 = ip[64];
     pres = present_mask(g, i, j, k);
   }
-  unsigned sw[7], diff = 0u;
+  unsigned sw[7], sb[7], diff = 0u;
 #pragma unroll
   for (int q = 0; q < 7; q++) {
     const unsigned v = q < 4 ? w0[q] : w1[q - 4];
     sw[q] = __builtin_amdgcn_readfirstlane(v);
     diff |= v ^ sw[q];
   }
-  const bool uni = __all(inxy && diff == 0u && w1[3] == 0u);
+  const bool ina = inxy && diff == 0u && w1[3] == 0u;
+  const bool uni = __all(ina);
   const bool full = __all(inxy && pres == PRES_ALL);
-  if (ln < 8) {
-    unsigned v = (uni ? 1u : 0u) | (full ? 2u : 0u);
+  // set B: the first lane outside set A
+  const unsigned long long oa = __ballot(!ina);
+  const int lb = oa ? __builtin_ctzll(oa) : 0;
+  unsigned db = 0u;
 #pragma unroll
-    for (int q = 0; q < 7; q++)
+  for (int q = 0; q < 7; q++) {
+    const unsigned v = q < 4 ? w0[q] : w1[q - 4];
+    sb[q] = (unsigned)__builtin_amdgcn_readlane((int)v, lb);
+    db |= v ^ sb[q];
+  }
+  const bool inb = !ina && inxy && db == 0u && w1[3] == 0u;
+  const bool two = !uni && __all(ina || inb);
+  const unsigned long long mb = __ballot(inb);
+  if (ln < 32) {
+    unsigned v = (uni ? 1u : 0u) | (full ? 2u : 0u) | (two ? 4u : 0u);
+#pragma unroll
+    for (int q = 0; q < 7; q++) {
       if (ln == q + 1) v = sw[q];
-    D[(w << 3) + ln] = v;
+      if (ln == q + 8) v = two ? sb[q] : 0u;
+    }
+    if (ln == 15) v = 0u;
+    if (ln == 16) v = two ? (unsigned)mb : 0u;
+    if (ln == 17) v = two ? (unsigned)(mb >> 32) : 0u;
+    if (ln > 17) v = 0u;
+    D[(w << 5) + ln] = v;
   }
   const double nbl = wave_sum((double)__popc(pres));
   if (ln == 0) {
     if (!uni) atomicAdd(&ctr[0], (unsigned long long)nbl);
     if (!(uni && full)) atomicAdd(&ctr[1], (unsigned long long)nbl);
+    if (!uni && !two) atomicAdd(&ctr[2], (unsigned long long)nbl);
   }
 }
 
@@ -4446,7 +4500,7 @@ int build_wdesc(Ctx& c) {
   if (!(c.fmt == FMT_VI && c.vi_block)) return 0;
   const int npx = (c.g.nx + 15) / 16, npy = (c.g.ny + 3) / 4;
   const int64_t nw = (int64_t)npx * npy * c.g.nz;
-  const int64_t bytes = nw * 8 * sizeof(unsigned) + 2 * sizeof(unsigned long long);
+  const int64_t bytes = nw * 32 * sizeof(unsigned) + 3 * sizeof(unsigned long long);
   if (bytes > c.wd_bytes) {
     if (c.wd) {
       MCX_HIP(hipFree(c.wd));
@@ -4457,17 +4511,18 @@ int build_wdesc(Ctx& c) {
     c.wd_bytes = bytes;
     c.device_bytes += bytes;
   }
-  unsigned long long* ctr = reinterpret_cast<unsigned long long*>(c.wd + nw * 8);
-  MCX_HIP(hipMemsetAsync(ctr, 0, 2 * sizeof(unsigned long long), c.stream));
+  unsigned long long* ctr = reinterpret_cast<unsigned long long*>(c.wd + nw * 32);
+  MCX_HIP(hipMemsetAsync(ctr, 0, 3 * sizeof(unsigned long long), c.stream));
   hipLaunchKernelGGL(k_vi_wdesc, dim3((unsigned)((nw + TPB / 64 - 1) / (TPB / 64))), dim3(TPB), 0, c.stream, c.g,
                      reinterpret_cast<const u32x4*>(c.vi_idx), c.wd, npx, npy, ctr);
-  unsigned long long h[2];
+  unsigned long long h[3];
   MCX_HIP(hipMemcpyAsync(h, ctr, sizeof(h), hipMemcpyDeviceToHost, c.stream));
   MCX_HIP(hipStreamSynchronize(c.stream));
   c.wd_npx = npx;
   c.wd_npy = npy;
   c.wd_blocks_fma = (int64_t)h[0];
   c.wd_blocks_exact = (int64_t)h[1];
+  c.wd_blocks_two = (int64_t)h[2];
   c.wd_ok = true;
   return 0;
 }
@@ -4744,6 +4799,7 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
 #undef MCX_VIBM_X
       } else if (wd_used(c) && !(c.vi_fma && c.vi_ring3)) {  // wave descriptors
         zt.wd = c.wd;
+        zt.wdm = c.vi_wdesc;
         zt.npx = c.wd_npx;
         zt.npy = c.wd_npy;
         if (c.vi_fma) {

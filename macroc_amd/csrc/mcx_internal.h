@@ -221,12 +221,12 @@ struct Ctx {
   int vi_tx = 0;             // staged block-indexed SpMV tile width 256 | 128 | 64 (0: 64; option vi_tx)
   int vi_uni = 1;            // staged block-indexed SpMV: wave-uniform blocks from scalar loads (option vi_uni)
   int vi_ypair = 0;          // with vi_uni: y of lane pairs as 16-B stores (option vi_ypair; A/B)
-  int vi_wdesc = 1;          // staged block-indexed SpMV: uniform waves take their indices from the wave descriptors (option vi_wdesc)
+  int vi_wdesc = 1;          // staged block-indexed SpMV: wave descriptors (option vi_wdesc): 1 = uniform waves, 2 = also two-set waves (FMA rows), 0 = off
   unsigned* wd = nullptr;    // wave descriptors [plane][npy][npx][8] + 2 counters (build_wdesc)
   int64_t wd_bytes = 0;
   bool wd_ok = false;        // descriptors built for the current block indices
   int wd_npx = 0, wd_npy = 0;
-  int64_t wd_blocks_fma = 0, wd_blocks_exact = 0;  // present blocks of the nodes in waves that are not uniform
+  int64_t wd_blocks_fma = 0, wd_blocks_exact = 0, wd_blocks_two = 0;  // present blocks of the nodes in waves that read per-lane words
   int vi_xread = 1;          // staged block-indexed SpMV: x as unpaired 8-B LDS reads (option vi_xread; 0: compiler's pairs)
   int vi_stage = -1;         // FMT_VI SpMV: 1 = x staged in LDS, z-marching tiles; 0 = x gathered; -1 = by grid (vi_staged)
   bool vi_declined = false;  // a per-GP-tangent law overflowed the dictionary: skip the attempt

@@ -712,6 +712,11 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
             m.set_option("vi_ypair", 0)
             m.set_option("vi_wdesc", 0)
             assert np.array_equal(m.spmv(x), yf), (zblocks, "no wdesc")
+            m.set_option("vi_wdesc", 2)  # two-set waves: one scalar pass per set under its exec mask
+            assert np.array_equal(m.spmv(x), yf), (zblocks, "two-set")
+            m.set_option("vi_fma", 0)
+            assert np.array_equal(m.spmv(x), y_ref), (zblocks, "two-set exact")
+            m.set_option("vi_fma", 1)
             m.set_option("vi_wdesc", 1)
         m.set_option("spmv_zblocks", 1)  # every tile marches all planes: the prefetch ring end to end
         assert m.get_info()["spmv_kc"] == NZ
