@@ -2487,7 +2487,9 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
     return __builtin_nontemporal_load(zt.wd + ((((int64_t)k * zt.npy + gpy) * zt.npx + gpx) << 5) + (me & 31));
   };
   // the planes whose waves skip the per-lane index words: uniform, or (FMA rows, wdm 2) two-set
-  auto wskip = [&](unsigned f) -> bool { return (f & 1u) || (FMA && zt.wdm == 2 && (f & 4u)); };
+  auto wskip = [&](unsigned f) -> bool {
+    return FMA ? (f & 1u) || (zt.wdm == 2 && (f & 4u)) : (f & 3u) == 3u;
+  };
   const int len = 3 * min(TX + 2, g.nx + 2 - i0);  // doubles of a staged row that exist in the padded box
   const int rows = min(TY + 2, g.ny + 2 - j0);      // staged rows (j0-1 ..) that exist (padded j <= ny)
   auto xload = [&](int p, int m) -> double {        // x of node plane p (-1 .. nz), staged element me + m T
