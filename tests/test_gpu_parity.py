@@ -661,9 +661,9 @@ def test_aij_split_tile_shapes(NX, NY, NZ):
 def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
     """The headline kernel at the tile shapes it runs (k_spmv_vibm 64x16, the default, and the
     selectable 128x8 / 256x4), with partial tiles in x (260 = 4 x 64 + 4 = 256 + 4, 130,
-    70) and y (6, 9, 20 rows against 16 / 8 / 4), with the wave descriptors (default: a uniform
-    wave's block indices from its patch descriptor) and without (per-lane indices, vi_wdesc 0,
-    bitwise the same rows): matrix dump bit-exact, and the SpMV bit-exact with the
+    70) and y (6, 9, 20 rows against 16 / 8 / 4), with per-lane block indices (default) and the
+    wave descriptors (vi_wdesc 1: a uniform wave's indices from its patch record; 2: two-set waves
+    in one pass per set; bitwise the same rows): matrix dump bit-exact, and the SpMV bit-exact with the
     oracle's CPU AIJ (MatMult_SeqAIJ_Inode order, the MATAIJ matrix of src/init.c:92 applied by
     KSPSolve, src/assembly.c:179-192) under -mat_vi_fma 0 for several z-chunkings and wave
     layouts; the default fused multiply-add rows within 1e-14 sum|a||x|; the solve within the
@@ -697,9 +697,9 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
                 assert np.array_equal(m.spmv(x), y_ref), (zblocks, uni, patch)
             m.set_option("vi_uni", 1)
             m.set_option("vi_patch", 1)
-            m.set_option("vi_wdesc", 0)  # block indices per lane in every wave (before the wave descriptors)
-            assert np.array_equal(m.spmv(x), y_ref), (zblocks, "no wdesc")
-            m.set_option("vi_wdesc", 1)
+            m.set_option("vi_wdesc", 1)  # uniform waves' block indices from the wave descriptors
+            assert np.array_equal(m.spmv(x), y_ref), (zblocks, "wdesc")
+            m.set_option("vi_wdesc", 0)
             m.set_option("vi_ypair", 1)  # the scalar path's y as 16-B lane-pair stores: the same rows
             assert np.array_equal(m.spmv(x), y_ref), (zblocks, "ypair")
             m.set_option("vi_ypair", 0)
@@ -710,14 +710,14 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
             m.set_option("vi_ypair", 1)
             assert np.array_equal(m.spmv(x), yf), (zblocks, "ypair")
             m.set_option("vi_ypair", 0)
-            m.set_option("vi_wdesc", 0)
-            assert np.array_equal(m.spmv(x), yf), (zblocks, "no wdesc")
-            m.set_option("vi_wdesc", 2)  # two-set waves: one scalar pass per set under its exec mask
+            m.set_option("vi_wdesc", 1)
+            assert np.array_equal(m.spmv(x), yf), (zblocks, "wdesc")
+            m.set_option("vi_wdesc", 2)  # two-set waves: one scalar pass per set, each lane keeping its own
             assert np.array_equal(m.spmv(x), yf), (zblocks, "two-set")
             m.set_option("vi_fma", 0)
             assert np.array_equal(m.spmv(x), y_ref), (zblocks, "two-set exact")
             m.set_option("vi_fma", 1)
-            m.set_option("vi_wdesc", 1)
+            m.set_option("vi_wdesc", 0)
         m.set_option("spmv_zblocks", 1)  # every tile marches all planes: the prefetch ring end to end
         assert m.get_info()["spmv_kc"] == NZ
         its, rn, reason = m.solve_Ax()
