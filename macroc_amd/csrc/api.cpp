@@ -1499,6 +1499,14 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.split_declined = false;
     return 0;
   }
+  if (!std::strcmp(name, "cg_ublocks")) {
+    if (value < 0 || value > (1 << 30) || value != (double)(int)value) {
+      set_error("cg_ublocks: 0 (uncapped) or a block count");
+      return 1;
+    }
+    c.cg_ublocks = (int)value;
+    return 0;
+  }
   if (!std::strcmp(name, "vi_wdesc")) {
     if (!(value == 0. || value == 1. || value == 2.)) {
       set_error("vi_wdesc: 0, 1 or 2");

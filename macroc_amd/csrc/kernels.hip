@@ -3606,7 +3606,9 @@ __global__ void k_cg_xfinal(Geo g, const double* __restrict__ ppad, const double
 }
 
 // r += (-a) w; z = D^-1 r; partials z.z, z.r   (x += a p: deferred to k_cg_pupdate)
-// 1024-thread blocks: a quarter of the partials for k_reduce (one block reads them all)
+// 1024-thread blocks: a quarter of the partials for k_reduce (one block reads them all); the grid
+// is capped at cg_ublocks blocks (grid-stride: a thread's nodes n, n + grid, ... summed in that
+// order), so k_reduce sums 2 x 2,048 partials instead of 2 x 16,384 at 256^3
 static constexpr int UTPB = 1024;
 
 template <bool NT, bool DIX>
@@ -3619,9 +3621,8 @@ __global__ __launch_bounds__(UTPB) void k_cg_update(Geo g, const double* __restr
   __shared__ double sh[UTPB / 64];
   if (cg->reason) return;
   const double ma = -cg->alpha;
-  int n = blockIdx.x * UTPB + threadIdx.x;
   double zz = 0., zr = 0.;
-  if (n < g.nown) {
+  for (int n = blockIdx.x * UTPB + threadIdx.x; n < g.nown; n += gridDim.x * UTPB) {
 #pragma unroll
     for (int d = 0; d < 3; d++) {
       const int q = 3 * n + d;
@@ -5216,10 +5217,11 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) 
   }
   rc = reduce_and_logic(c, 1, nbs, RED_ALPHA, true, c.partials, c.cg);
   if (rc) return rc;
+  const int nbg = c.cg_ublocks > 0 ? std::min(nbu, c.cg_ublocks) : nbu;
   MCX_NT_DIX(c.cg_nt, dix,
-             hipLaunchKernelGGL((k_cg_update<NT, DX>), dim3(nbu), dim3(UTPB), 0, c.stream, c.g, c.w, jd, c.jix, c.r,
-                                c.z, c.partials2, nbu, c.cg));
-  return reduce_and_logic(c, 2, nbu, RED_BETA, true, c.partials2, c.cg);
+             hipLaunchKernelGGL((k_cg_update<NT, DX>), dim3(nbg), dim3(UTPB), 0, c.stream, c.g, c.w, jd, c.jix, c.r,
+                                c.z, c.partials2, nbg, c.cg));
+  return reduce_and_logic(c, 2, nbg, RED_BETA, true, c.partials2, c.cg);
 }
 
 }  // namespace mcx
