@@ -3606,9 +3606,11 @@ __global__ void k_cg_xfinal(Geo g, const double* __restrict__ ppad, const double
 }
 
 // r += (-a) w; z = D^-1 r; partials z.z, z.r   (x += a p: deferred to k_cg_pupdate)
-// 1024-thread blocks: a quarter of the partials for k_reduce (one block reads them all); the grid
-// is capped at cg_ublocks blocks (grid-stride: a thread's nodes n, n + grid, ... summed in that
-// order), so k_reduce sums 2 x 2,048 partials instead of 2 x 16,384 at 256^3
+// 1024-thread blocks: a quarter of the partials for k_reduce (one block reads them all).  Option
+// cg_ublocks caps the grid (grid-stride: a thread's nodes n, n + grid, ... summed in that order)
+// so that k_reduce sums fewer partials: 0.8676 (2,048 blocks) / 0.8708 (512) against 0.8492 ms
+// per CG iteration uncapped at 256^3 (profiles/r04_cg_ab_ublocks256.log): the update kernel
+// loses more than the reduction saves
 static constexpr int UTPB = 1024;
 
 template <bool NT, bool DIX>

@@ -221,7 +221,7 @@ struct Ctx {
   int vi_tx = 0;             // staged block-indexed SpMV tile width 256 | 128 | 64 (0: 64; option vi_tx)
   int vi_uni = 1;            // staged block-indexed SpMV: wave-uniform blocks from scalar loads (option vi_uni)
   int vi_ypair = 0;          // with vi_uni: y of lane pairs as 16-B stores (option vi_ypair; A/B)
-  int cg_ublocks = 2048;     // k_cg_update grid cap (grid-stride; option cg_ublocks, 0 = one node per thread)
+  int cg_ublocks = 0;        // k_cg_update grid cap (grid-stride; option cg_ublocks, 0 = one node per thread; A/B)
   int vi_wdesc = 0;          // staged block-indexed SpMV: wave descriptors (option vi_wdesc): 1 = uniform waves, 2 = also two-set waves (FMA rows), 0 = off (A/B)
   unsigned* wd = nullptr;    // wave descriptors [plane][npy][npx][8] + 2 counters (build_wdesc)
   int64_t wd_bytes = 0;
