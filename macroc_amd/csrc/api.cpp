@@ -56,8 +56,9 @@ static int free_ctx(Ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
+  if (c->x_stream) (void)hipStreamSynchronize(c->x_stream);
   void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->wd, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
-                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2, c->p_pad3, c->p_pad4, c->xdone, c->esc_node, c->esc_res, c->esc_slot, c->elem_plain, c->cref, c->vi_xslot,
+                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2, c->p_pad3, c->p_pad4, c->p_pad58[0], c->p_pad58[1], c->p_pad58[2], c->p_pad58[3], c->xdone, c->esc_node, c->esc_res, c->esc_slot, c->elem_plain, c->cref, c->vi_xslot,
                   c->vi_xlist, c->vi_exc,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf, c->halo.d_bnd};
@@ -78,6 +79,9 @@ static int free_ctx(Ctx* c) {
   if (c->ev_pack) (void)hipEventDestroy(c->ev_pack);
   if (c->ev_comm) (void)hipEventDestroy(c->ev_comm);
   if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
+  if (c->x_stream) (void)hipStreamDestroy(c->x_stream);
+  for (hipEvent_t e : {c->ev_xp, c->ev_xd[0], c->ev_xd[1]})
+    if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return 0;
@@ -205,10 +209,21 @@ static int cg_solve(Ctx& c, int* its, double* rnorm, int* reason) {
   c.fusep_used = false;  // set by cg_iteration when the p update runs inside the SpMV
   c.pdb_used = cg_pdb(c);
   c.pqb_used = c.pdb_used && c.cg_pdb == 4;
+  c.xs_used = c.pqb_used && c.cg_xs;
   if (c.pqb_used && !c.p_pad3) {  // the quad-buffered p update's third and fourth buffers
     const int64_t npad = (int64_t)c.g.PX * c.g.PY * c.g.PZ * 3;
     int rc = 0;
     if ((rc = dalloc(c, &c.p_pad3, npad)) || (rc = dalloc(c, &c.p_pad4, npad))) return rc;
+  }
+  if (c.xs_used && !c.p_pad58[0]) {  // cg_xs: buffers 5-8, the side stream and its events
+    const int64_t npad = (int64_t)c.g.PX * c.g.PY * c.g.PZ * 3;
+    int rc = 0;
+    for (int q = 0; q < 4; q++)
+      if ((rc = dalloc(c, &c.p_pad58[q], npad))) return rc;
+    MCX_HIP(hipStreamCreateWithFlags(&c.x_stream, hipStreamNonBlocking));
+    MCX_HIP(hipEventCreateWithFlags(&c.ev_xp, hipEventDisableTiming));
+    MCX_HIP(hipEventCreateWithFlags(&c.ev_xd[0], hipEventDisableTiming));
+    MCX_HIP(hipEventCreateWithFlags(&c.ev_xd[1], hipEventDisableTiming));
   }
   if (c.pdb_used) MCX_HIP(hipMemsetAsync(c.xdone, 0, sizeof(int), c.stream));
   CgState s{};
@@ -257,7 +272,7 @@ static int cg_solve(Ctx& c, int* its, double* rnorm, int* reason) {
     slot ^= 1;
     if (issued > cap) break;
   }
-  launch_cg_xfinal(c);  // the last iteration's VecAXPY(x, alpha, p), deferred by k_cg_pupdate
+  if ((rc = launch_cg_xfinal(c))) return rc;  // the owed VecAXPY(x, alpha, p) terms, deferred by k_cg_pupdate
   MCX_HIP(hipStreamSynchronize(c.stream));
   CgState fin;
   MCX_HIP(hipMemcpy(&fin, c.cg, sizeof(CgState), hipMemcpyDeviceToHost));
@@ -1497,6 +1512,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
   if (!std::strcmp(name, "split_esc")) {  // takes effect at the next mcx_assembly_jac
     c.split_esc = value != 0.;
     c.split_declined = false;
+    return 0;
+  }
+  if (!std::strcmp(name, "cg_xs")) {  // takes effect at the next solve (with cg_pdb 4)
+    c.cg_xs = value != 0.;
     return 0;
   }
   if (!std::strcmp(name, "cg_ublocks")) {

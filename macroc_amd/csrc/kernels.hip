@@ -3462,14 +3462,17 @@ __global__ void k_cg_pupdate_db(Geo g, const double* __restrict__ z, const doubl
 // (48 + 3 x 24) / 4 = 30 B per node and iteration instead of PDB's 36.  xdone = the last such i;
 // k_cg_xfinal_qb applies the (at most four) terms still owed.
 // PAR: 1 = an iteration >= 1 without the x terms, 2 = one with them (i = 4m >= 4), 0 = from cg->i
+// XS (option cg_xs): p in eight buffers, p(i) in pq[i & 7], and the four owed x terms left to
+// k_cg_xwin on a side stream (this kernel only marks the window: xdone = i)
 struct PQ {
-  double* p[4];
+  double* p[8];
 };
-template <bool NT, bool DIX, bool SKIP_SENT = false, int PAR = 0>
+template <bool NT, bool DIX, bool SKIP_SENT = false, int PAR = 0, bool XS = false>
 __global__ void k_cg_pupdate_qb(Geo g, const double* __restrict__ z, const double* __restrict__ dinv,
                                 const unsigned char* __restrict__ jix, PQ pq, double* __restrict__ x,
                                 const CgState* __restrict__ cg, int* __restrict__ xdone,
                                 const int* __restrict__ list, int64_t cnt, int rev = 0) {
+  constexpr int M = XS ? 7 : 3;  // buffer ring mask
   if (cg->reason) return;
   const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
   const int it = cg->i;
@@ -3481,7 +3484,7 @@ __global__ void k_cg_pupdate_qb(Geo g, const double* __restrict__ z, const doubl
   node_ijk(g, n, i, j, k);
   if (SKIP_SENT && sent_node(g, i, j, k)) return;
   const int pc = pad_of(g, i, j, k);
-  double* pn = pq.p[it & 3];
+  double* pn = pq.p[it & M];
   if (it == 0) {
 #pragma unroll
     for (int d = 0; d < 3; d++) st<NT>(&pn[3 * pc + d], z_of<DIX>(z, dinv, jix, n, d));
@@ -3489,14 +3492,14 @@ __global__ void k_cg_pupdate_qb(Geo g, const double* __restrict__ z, const doubl
   }
   // the host's parity guess must match the device's count, else the generic path below
   const bool par_ok = PAR == 0 || (PAR == 2) == dox;
-  const double* po = pq.p[(it - 1) & 3];
+  const double* po = pq.p[(it - 1) & M];
   const double bc = cg->bcoef;
   double pv[3], zv[3];
-  if ((PAR == 2 && par_ok) || (PAR == 0 && dox)) {
+  if (!XS && ((PAR == 2 && par_ok) || (PAR == 0 && dox))) {
     const double* p3 = pq.p[(it - 3) & 3];
     const double* p2 = pq.p[(it - 2) & 3];
-    const double a4 = cg->ah[(it - 4) & 3], a3 = cg->ah[(it - 3) & 3], a2 = cg->ah[(it - 2) & 3],
-                 a1 = cg->ah[(it - 1) & 3];
+    const double a4 = cg->ah[(it - 4) & 7], a3 = cg->ah[(it - 3) & 7], a2 = cg->ah[(it - 2) & 7],
+                 a1 = cg->ah[(it - 1) & 7];
     double xv[3], q4[3], q3[3], q2[3];
 #pragma unroll
     for (int d = 0; d < 3; d++) {  // every load before any store
@@ -3520,9 +3523,42 @@ __global__ void k_cg_pupdate_qb(Geo g, const double* __restrict__ z, const doubl
   for (int d = 0; d < 3; d++) st<NT>(&pn[3 * pc + d], zv[d] + bc * pv[d]);
 }
 
-// PQB: the terms j = xdone .. xp still owed after the loop (at most four), in order
+// XS: the window i0-4 .. i0-1 of VecAXPY(x) terms, on the side stream while the main stream runs
+// the next iterations (it waits for this kernel before p(i0+4) overwrites p(i0-4)'s buffer);
+// skipped unless iteration i0's p update ran (xdone == i0), so a finished solve's window is left
+// to k_cg_xfinal_qb.  The same terms in the same order as k_cg_pupdate_qb's: bitwise the same x.
+__global__ __launch_bounds__(TPB) void k_cg_xwin(Geo g, PQ pq, double* __restrict__ x,
+                                                 const CgState* __restrict__ cg, const int* __restrict__ xdone,
+                                                 int i0) {
+  if (*xdone != i0) return;
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  if (n >= g.nown) return;
+  int i, j, k;
+  node_ijk(g, n, i, j, k);
+  const int pc = pad_of(g, i, j, k);
+  const double a4 = cg->ah[(i0 - 4) & 7], a3 = cg->ah[(i0 - 3) & 7], a2 = cg->ah[(i0 - 2) & 7],
+               a1 = cg->ah[(i0 - 1) & 7];
+  const double* q4 = pq.p[(i0 - 4) & 7];
+  const double* q3 = pq.p[(i0 - 3) & 7];
+  const double* q2 = pq.p[(i0 - 2) & 7];
+  const double* q1 = pq.p[(i0 - 1) & 7];
+  double xv[3], v4[3], v3[3], v2[3], v1[3];
+#pragma unroll
+  for (int d = 0; d < 3; d++) {
+    xv[d] = x[3 * n + d];
+    v4[d] = q4[3 * pc + d];
+    v3[d] = q3[3 * pc + d];
+    v2[d] = q2[3 * pc + d];
+    v1[d] = q1[3 * pc + d];
+  }
+#pragma unroll
+  for (int d = 0; d < 3; d++) x[3 * n + d] = (((xv[d] + a4 * v4[d]) + a3 * v3[d]) + a2 * v2[d]) + a1 * v1[d];
+}
+
+// PQB: the terms j = xdone .. xp still owed after the loop (at most four), in order (m: the
+// buffer ring's mask, 3 or 7)
 __global__ void k_cg_xfinal_qb(Geo g, PQ pq, double* __restrict__ x, const CgState* __restrict__ cg,
-                               const int* __restrict__ xdone) {
+                               const int* __restrict__ xdone, int m) {
   const int xd = *xdone, xp = cg->xp;
   if (xp < xd) return;
   const int n = blockIdx.x * TPB + threadIdx.x;
@@ -3533,7 +3569,7 @@ __global__ void k_cg_xfinal_qb(Geo g, PQ pq, double* __restrict__ x, const CgSta
 #pragma unroll
   for (int d = 0; d < 3; d++) {
     double xv = x[3 * n + d];
-    for (int jj = xd; jj <= xp; jj++) xv = xv + cg->ah[jj & 3] * pq.p[jj & 3][3 * pc + d];
+    for (int jj = xd; jj <= xp; jj++) xv = xv + cg->ah[jj & 7] * pq.p[jj & m][3 * pc + d];
     x[3 * n + d] = xv;
   }
 }
@@ -3839,7 +3875,7 @@ __device__ void cg_logic_alpha(CgState* s, double dpi) {
   }
   s->alpha_prev = s->alpha;
   s->alpha = s->beta / dpi;
-  s->ah[s->i & 3] = s->alpha;
+  s->ah[s->i & 7] = s->alpha;
   s->xpend = 1;
   s->xp = s->i;
 }
@@ -5041,16 +5077,24 @@ int cg_finish_init(Ctx& c) {
   return reduce_and_logic(c, 2, nb, RED_INIT, false, c.partials, c.cg);
 }
 
-static PQ pq_of(const Ctx& c) { return PQ{{c.p_pad, c.p_pad2, c.p_pad3, c.p_pad4}}; }
+static PQ pq_of(const Ctx& c) {
+  return PQ{{c.p_pad, c.p_pad2, c.p_pad3, c.p_pad4, c.p_pad58[0], c.p_pad58[1], c.p_pad58[2], c.p_pad58[3]}};
+}
+static int pq_mask(const Ctx& c) { return c.xs_used ? 7 : 3; }
 
-void launch_cg_xfinal(Ctx& c) {
+int launch_cg_xfinal(Ctx& c) {
   if (c.pqb_used) {
+    if (c.xs_used) {  // the side stream's windows first
+      MCX_HIP(hipStreamWaitEvent(c.stream, c.ev_xd[0], 0));
+      MCX_HIP(hipStreamWaitEvent(c.stream, c.ev_xd[1], 0));
+    }
     hipLaunchKernelGGL(k_cg_xfinal_qb, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, pq_of(c), c.du, c.cg,
-                       c.xdone);
-    return;
+                       c.xdone, pq_mask(c));
+    return 0;
   }
   hipLaunchKernelGGL(k_cg_xfinal, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.p_pad,
                      c.fusep_used || c.pdb_used ? c.p_pad2 : nullptr, c.du, c.cg, c.pdb_used ? c.xdone : nullptr);
+  return 0;
 }
 
 // CG vector kernels' Jacobi form: DIX (block-indexed value storage, option cg_dix) reads one
@@ -5086,7 +5130,10 @@ void launch_cg_pupdate(Ctx& c, int part) {
     const PQ pq = pq_of(c);
 #define MCX_PQB_PAR(SKIPV, GRID, LIST, CNT)                                                                          \
   MCX_NT_DIX(c.cg_nt, dix, {                                                                                         \
-    if (par == 1)                                                                                                    \
+    if (c.xs_used)                                                                                                   \
+      hipLaunchKernelGGL((k_cg_pupdate_qb<NT, DX, SKIPV, 1, true>), dim3(GRID), dim3(TPB), 0, c.stream, c.g, zs, jd,  \
+                         c.jix, pq, c.du, c.cg, c.xdone, LIST, CNT, c.cg_rev);                                       \
+    else if (par == 1)                                                                                               \
       hipLaunchKernelGGL((k_cg_pupdate_qb<NT, DX, SKIPV, 1>), dim3(GRID), dim3(TPB), 0, c.stream, c.g, zs, jd, c.jix, \
                          pq, c.du, c.cg, c.xdone, LIST, CNT, c.cg_rev);                                              \
     else if (par == 2)                                                                                               \
@@ -5192,7 +5239,10 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) 
   }
   // p of this iteration (PDB: buffer it & 1, `it` = the host's count of launched iterations, which
   // is the device's cg->i for every iteration that runs; the fused small-grid path fb has one buffer)
-  double* pcur = c.pqb_used ? pq_of(c).p[c.cg_it & 3] : (c.pdb_used && (c.cg_it & 1) ? c.p_pad2 : c.p_pad);
+  double* pcur = c.pqb_used ? pq_of(c).p[c.cg_it & pq_mask(c)] : (c.pdb_used && (c.cg_it & 1) ? c.p_pad2 : c.p_pad);
+  // XS: p(it) overwrites p(it-8)'s buffer, read by the window kernel of iteration it-4
+  const bool xwin = c.xs_used && c.cg_it >= 4 && (c.cg_it & 3) == 0;
+  if (xwin && c.cg_it >= 8) MCX_HIP(hipStreamWaitEvent(c.stream, c.ev_xd[((c.cg_it >> 2) - 1) & 1], 0));
   if (fb && !first) {
     MCX_NT_DIX(c.cg_nt, dix,
                hipLaunchKernelGGL((k_cg_pupdate_fb<NT, DX>), dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, zs, jd,
@@ -5207,6 +5257,13 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) 
     launch_cg_pupdate(c, 0);
   }
   if (!(c.nranks > 1 && c.overlap && c.halo.nbnd) && (rc = halo_exchange(c, pcur))) return rc;
+  if (xwin) {  // the window it-4 .. it-1 on the side stream, beside this iteration's SpMV and update
+    MCX_HIP(hipEventRecord(c.ev_xp, c.stream));
+    MCX_HIP(hipStreamWaitEvent(c.x_stream, c.ev_xp, 0));
+    hipLaunchKernelGGL(k_cg_xwin, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.x_stream, c.g, pq_of(c), c.du, c.cg, c.xdone,
+                       c.cg_it);
+    MCX_HIP(hipEventRecord(c.ev_xd[(c.cg_it >> 2) & 1], c.x_stream));
+  }
   if (ev0) MCX_HIP(hipEventRecord(ev0, c.stream));
   launch_spmv(c, pcur, c.w, true, true);
   if (ev1) MCX_HIP(hipEventRecord(ev1, c.stream));

@@ -45,7 +45,7 @@ struct CgState {
   int xpend;  // x += alpha p of the last iteration not yet applied (k_cg_pupdate / k_cg_xfinal apply it)
   int xp;     // the last iteration whose alpha step succeeded (-1: none); the fused path's pending x update
   double alpha_prev;  // alpha of the iteration before (the fused path's every-second-iteration x update)
-  double ah[4];       // alpha of iteration j at ah[j & 3] (quad-buffered p: x every fourth iteration)
+  double ah[8];       // alpha of iteration j at ah[j & 7] (quad-buffered p: x every fourth iteration)
 };
 
 struct Material {
@@ -141,6 +141,11 @@ struct Ctx {
   double* p_pad2 = nullptr;  // its second buffer (single rank: the p update fused into the SpMV, cg_fusep)
   double* p_pad3 = nullptr;  // third and fourth buffers (cg_pdb 4), allocated at the first solve that uses them
   double* p_pad4 = nullptr;
+  double* p_pad58[4] = {nullptr, nullptr, nullptr, nullptr};  // buffers 5-8 (cg_xs)
+  int cg_xs = 0;             // quad-buffered p: the four owed VecAXPY(x) terms on a side stream (option cg_xs)
+  bool xs_used = false;      // this solve: eight p buffers, k_cg_xwin on x_stream
+  hipStream_t x_stream = nullptr;
+  hipEvent_t ev_xp = nullptr, ev_xd[2] = {nullptr, nullptr};
   int cg_fusep = 0;          // option cg_fusep: fuse the CG p update into the value-indexed SpMV (single rank; A/B: no gain)
   bool fusep_used = false;   // the last solve ran the fused kernel (timing: its bytes per launch)
   int cg_pdb = 4;            // option cg_pdb: 1 = p double-buffered (p_pad / p_pad2), VecAXPY(x) every second
@@ -332,7 +337,7 @@ int build_vi(Ctx& c, bool* ok);        // value-indexed AIJ (ok = at most VI_MAX
 void launch_jacobi(Ctx& c);
 void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated);
 void launch_update_u(Ctx& c);
-void launch_cg_xfinal(Ctx& c);
+int launch_cg_xfinal(Ctx& c);
 void launch_cg_pupdate(Ctx& c, int part);  // 0 all owned nodes, 1 the sent (subdomain-face) nodes, 2 the rest
 void launch_reduce(Ctx& c, int nvals, int nparts, double* out);
 void launch_cg_init(Ctx& c);

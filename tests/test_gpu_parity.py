@@ -732,7 +732,8 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
 def test_cg_pdb_bitwise(maxits, storage):
     """Option cg_pdb 1 (default): p double-buffered and VecAXPY(x) applied on odd iterations only,
     both owed terms in PETSc's order, the rest by k_cg_xfinal; cg_pdb 4: four buffers, the four
-    owed terms every fourth iteration — bitwise the solve of the single-buffer p update:
+    owed terms every fourth iteration (cg_xs 1: eight buffers, the four terms by k_cg_xwin on a side
+    stream beside the next iterations) — bitwise the solve of the single-buffer p update:
     converged, and stopped by maxits at every residue mod 4 (1 to 5 included); with and without
     the parity-specialised kernels (cg_par) and the reversed node order (cg_rev)."""
     NX, NY, NZ = 70, 20, 12
@@ -745,11 +746,12 @@ def test_cg_pdb_bitwise(maxits, storage):
             m.set_option("vi_stage", 1)
         m.apply_bc_on_u(m.get_displacement(1))
         m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
-        for pdb, par, rev in ((0, 0, 0), (1, 0, 0), (0, 1, 0), (1, 1, 0), (1, 1, 1), (1, 0, 1), (4, 0, 0), (4, 1, 0),
-                              (4, 1, 1)):
+        for pdb, par, rev, xs in ((0, 0, 0, 0), (1, 0, 0, 0), (0, 1, 0, 0), (1, 1, 0, 0), (1, 1, 1, 0), (1, 0, 1, 0),
+                                  (4, 0, 0, 0), (4, 1, 0, 0), (4, 1, 1, 0), (4, 1, 0, 1), (4, 0, 1, 1)):
             m.set_option("cg_pdb", pdb)
             m.set_option("cg_par", par)
             m.set_option("cg_rev", rev)
+            m.set_option("cg_xs", xs)
             its, rn, reason = m.solve_Ax()
             out.append((its, reason, m.du()))
     for its, reason, du in out[1:]:
