@@ -1514,6 +1514,14 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.split_declined = false;
     return 0;
   }
+  if (!std::strcmp(name, "vi_lg")) {
+    if (!(value == 1. || value == 2. || value == 3.)) {
+      set_error("vi_lg: 1, 2 or 3");
+      return 1;
+    }
+    c.vi_lg = (int)value;
+    return 0;
+  }
   if (!std::strcmp(name, "cg_xs")) {  // takes effect at the next solve (with cg_pdb 4)
     c.cg_xs = value != 0.;
     return 0;

@@ -2403,7 +2403,7 @@ constexpr int vibm_rl() {
 }
 
 template <bool DOT, bool GATED, int TX, int TY, bool XV = true, bool UNI = false, bool PATCH = false, bool FMA = false,
-          bool FP = false, bool RING3 = false, bool EXC = false, bool WD = false>
+          bool FP = false, bool RING3 = false, bool EXC = false, bool WD = false, int LG = 1>
 __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __restrict__ I,
                                                        const double* __restrict__ bdict, const double* __restrict__ x,
                                                        double* __restrict__ y, double* __restrict__ part,
@@ -2803,40 +2803,56 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       // volatile reads are not paired.
       typedef const volatile __attribute__((address_space(3))) double lds_vdouble;
       lds_vdouble* xsv = (lds_vdouble*)&xs[0][0];
+      // LG > 1 (option vi_lg): the reads of LG blocks issued together and waited for once (the
+      // compiler otherwise waits for each block's reads before its products: 27 LDS round trips
+      // per wave and plane on these waves, which set the plane's pace at its barrier)
 #pragma unroll
-      for (int nb = 0; nb < 27; nb++) {
-        const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
-        const int xo = ((k + dz - k0 + 1) % R) * PLANE + (ly + 1 + dy) * RL + 3 * (lx + 1 + dx);
-        double xv[3];
-        if (XV) {
-          lds_vdouble* xp = xsv + xo;
-          xv[0] = xp[0];
-          xv[1] = xp[1];
-          xv[2] = xp[2];
-        } else {
-          const double* xp = &xs[0][0] + xo;
-          xv[0] = xp[0];
-          xv[1] = xp[1];
-          xv[2] = xp[2];
-        }
-        if (nb == 13) {
-          xc0 = xv[0];
-          xc1 = xv[1];
-          xc2 = xv[2];
-        }
-        const unsigned word = nb < 16 ? c0[nb >> 2] : c1[(nb - 16) >> 2];
-        const unsigned id = (word >> (8 * (nb & 3))) & 255u;
-        const double2* e = tab + id * (VIB_STRIDE / 2);
-        const double2 a01 = e[0], a23 = e[1], a45 = e[2], a67 = e[3];
-        const double a8 = reinterpret_cast<const double*>(e)[8];  // 8 B, not the padded 16: 18 LDS cycles per block
-        const double a[9] = {a01.x, a01.y, a23.x, a23.y, a45.x, a45.y, a67.x, a67.y, a8};
+      for (int nb0 = 0; nb0 < 27; nb0 += LG) {
+        double xv[LG][3], a[LG][9];
 #pragma unroll
-        for (int q = 0; q < 9; q++) {
-          const int r = q / 3, cc = q % 3;
-          double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
-          if constexpr (FMA) yr = __builtin_fma(a[q], xv[cc], yr);
-          else acc.term(nb, r, cc, a[q] * xv[cc]);
+        for (int t = 0; t < LG; t++) {
+          const int nb = nb0 + t;
+          if (nb >= 27) break;
+          const int dx = nb % 3 - 1, dy = (nb / 3) % 3 - 1, dz = nb / 9 - 1;
+          const int xo = ((k + dz - k0 + 1) % R) * PLANE + (ly + 1 + dy) * RL + 3 * (lx + 1 + dx);
+          if (XV) {
+            lds_vdouble* xp = xsv + xo;
+            xv[t][0] = xp[0];
+            xv[t][1] = xp[1];
+            xv[t][2] = xp[2];
+          } else {
+            const double* xp = &xs[0][0] + xo;
+            xv[t][0] = xp[0];
+            xv[t][1] = xp[1];
+            xv[t][2] = xp[2];
+          }
+          const unsigned word = nb < 16 ? c0[nb >> 2] : c1[(nb - 16) >> 2];
+          const unsigned id = (word >> (8 * (nb & 3))) & 255u;
+          const double2* e = tab + id * (VIB_STRIDE / 2);
+          const double2 a01 = e[0], a23 = e[1], a45 = e[2], a67 = e[3];
+          const double a8 = reinterpret_cast<const double*>(e)[8];  // 8 B, not the padded 16: 18 LDS cycles per block
+          a[t][0] = a01.x, a[t][1] = a01.y, a[t][2] = a23.x, a[t][3] = a23.y, a[t][4] = a45.x;
+          a[t][5] = a45.y, a[t][6] = a67.x, a[t][7] = a67.y, a[t][8] = a8;
         }
+        if (LG > 1) __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < LG; t++) {
+          const int nb = nb0 + t;
+          if (nb >= 27) break;
+          if (nb == 13) {
+            xc0 = xv[t][0];
+            xc1 = xv[t][1];
+            xc2 = xv[t][2];
+          }
+#pragma unroll
+          for (int q = 0; q < 9; q++) {
+            const int r = q / 3, cc = q % 3;
+            double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
+            if constexpr (FMA) yr = __builtin_fma(a[t][q], xv[t][cc], yr);
+            else acc.term(nb, r, cc, a[t][q] * xv[t][cc]);
+          }
+        }
+        if (LG > 1) __builtin_amdgcn_sched_barrier(0);
       }
       if constexpr (!FMA) y0 = acc.row(0), y1 = acc.row(1), y2 = acc.row(2);
       const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
@@ -4854,6 +4870,9 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
         }
       } else if (c.vi_fma && c.vi_ring3 && tx == 64) {
         MCX_VIBM(64, 16, true, true, true, true, false, true);
+      } else if (c.vi_fma && tx == 64 && (c.vi_lg == 2 || c.vi_lg == 3)) {  // LDS-path block groups (A/B)
+        if (c.vi_lg == 2) MCX_VIBM(64, 16, true, true, true, true, false, false, false, false, 2);
+        else MCX_VIBM(64, 16, true, true, true, true, false, false, false, false, 3);
       } else if (c.vi_fma) {
         if (tx == 256) MCX_VIBM(256, 4, true, true, true, true);
         else if (tx == 128) MCX_VIBM(128, 8, true, true, true, true);

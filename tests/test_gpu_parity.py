@@ -710,6 +710,10 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
             m.set_option("vi_ypair", 1)
             assert np.array_equal(m.spmv(x), yf), (zblocks, "ypair")
             m.set_option("vi_ypair", 0)
+            for lg in (2, 3):  # LDS-dictionary waves: the reads of 2 / 3 blocks issued together
+                m.set_option("vi_lg", lg)
+                assert np.array_equal(m.spmv(x), yf), (zblocks, "vi_lg", lg)
+            m.set_option("vi_lg", 1)
             m.set_option("vi_wdesc", 1)
             assert np.array_equal(m.spmv(x), yf), (zblocks, "wdesc")
             m.set_option("vi_wdesc", 2)  # two-set waves: one scalar pass per set, each lane keeping its own
