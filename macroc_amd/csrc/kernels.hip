@@ -4870,9 +4870,13 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
         }
       } else if (c.vi_fma && c.vi_ring3 && tx == 64) {
         MCX_VIBM(64, 16, true, true, true, true, false, true);
-      } else if (c.vi_fma && tx == 64 && (c.vi_lg == 2 || c.vi_lg == 3)) {  // LDS-path block groups (A/B)
+      } else if (c.vi_fma && tx == 64 && (c.vi_lg == 2 || c.vi_lg == 3)) {
+        // LDS-path reads in groups of 2 blocks (default): SpMV 0.3098 vs 0.3228 ms, CG iteration
+        // 0.8295 vs 0.8419 ms; groups of 3 spill (0.3866 ms) (profiles/r04_cg_ab_lg256.log)
         if (c.vi_lg == 2) MCX_VIBM(64, 16, true, true, true, true, false, false, false, false, 2);
         else MCX_VIBM(64, 16, true, true, true, true, false, false, false, false, 3);
+      } else if (!c.vi_fma && c.vi_uni && c.vi_patch && tx == 64 && c.vi_lg == 2) {  // exact rows, the same groups
+        MCX_VIBM(64, 16, true, true, true, false, false, false, false, false, 2);
       } else if (c.vi_fma) {
         if (tx == 256) MCX_VIBM(256, 4, true, true, true, true);
         else if (tx == 128) MCX_VIBM(128, 8, true, true, true, true);
