@@ -2479,6 +2479,9 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
   // WD: this wave's 16 x 4 patch in the descriptor grid (a patch wholly outside the domain has
   // none: its planes count as not uniform, and its lanes compute nothing)
   static_assert(!WD || (UNI && PATCH && !FP && !EXC), "wave descriptors: the scalar-dictionary patch kernels");
+  // FP's fstore reads the Jacobi entry from the dictionary's s_jdd without jac_inv's jix 255
+  // redirect: a matrix with exception nodes never takes the fused p update (fusep checks vi_nexc)
+  static_assert(!(FP && EXC), "the fused p update has no exception-node Jacobi redirect");
   const int gpx = (i0 + (lx & ~15)) >> 4, gpy = (j0 + (ly & ~3)) >> 2;  // (wave-uniform)
   const bool wdv = WD && gpx < zt.npx && gpy < zt.npy;
   // lane ln holds descriptor word ln & 31 of plane k (build_wdesc's layout)
