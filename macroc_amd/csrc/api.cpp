@@ -1522,6 +1522,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.vi_lg = (int)value;
     return 0;
   }
+  if (!std::strcmp(name, "vi_lg_exc")) {
+    c.vi_lg_exc = value != 0.;
+    return 0;
+  }
   if (!std::strcmp(name, "cg_xs")) {  // takes effect at the next solve (with cg_pdb 4)
     c.cg_xs = value != 0.;
     return 0;

@@ -4832,24 +4832,25 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
                          c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt);                             \
   } while (0)
       if (c.vi_nexc) {  // exception nodes: the default (FMA) or exact rows, UNI + PATCH
-#define MCX_VIBM_X(TXV, TYV, FV)                                                                                    \
+#define MCX_VIBM_X(TXV, TYV, FV, ...)                                                                               \
   do {                                                                                                             \
     if (dot && gated)                                                                                              \
-      hipLaunchKernelGGL((k_spmv_vibm<true, true, TXV, TYV, true, true, true, FV, false, false, true>), dim3(nb),       \
-                         dim3(1024), 0, c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt, FusedP{},      \
-                         c.vi_exc);                                                                                \
+      hipLaunchKernelGGL((k_spmv_vibm<true, true, TXV, TYV, true, true, true, FV, false, false, true, ##__VA_ARGS__>),  \
+                         dim3(nb), dim3(1024), 0, c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt,      \
+                         FusedP{}, c.vi_exc);                                                                      \
     else if (dot)                                                                                                  \
-      hipLaunchKernelGGL((k_spmv_vibm<true, false, TXV, TYV, true, true, true, FV, false, false, true>), dim3(nb),      \
-                         dim3(1024), 0, c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt, FusedP{},      \
-                         c.vi_exc);                                                                                \
+      hipLaunchKernelGGL((k_spmv_vibm<true, false, TXV, TYV, true, true, true, FV, false, false, true, ##__VA_ARGS__>), \
+                         dim3(nb), dim3(1024), 0, c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt,      \
+                         FusedP{}, c.vi_exc);                                                                      \
     else                                                                                                           \
-      hipLaunchKernelGGL((k_spmv_vibm<false, false, TXV, TYV, true, true, true, FV, false, false, true>), dim3(nb),     \
-                         dim3(1024), 0, c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt, FusedP{},      \
-                         c.vi_exc);                                                                                \
+      hipLaunchKernelGGL((k_spmv_vibm<false, false, TXV, TYV, true, true, true, FV, false, false, true, ##__VA_ARGS__>),\
+                         dim3(nb), dim3(1024), 0, c.stream, c.g, I, c.vi_bdict, xpad, y, c.partials, c.cg, zt,      \
+                         FusedP{}, c.vi_exc);                                                                      \
   } while (0)
         if (c.vi_fma) {
           if (tx == 256) MCX_VIBM_X(256, 4, true);
           else if (tx == 128) MCX_VIBM_X(128, 8, true);
+          else if (c.vi_lg == 2 && c.vi_lg_exc) MCX_VIBM_X(64, 16, true, false, 2);  // grouped LDS-path reads
           else MCX_VIBM_X(64, 16, true);
         } else {
           if (tx == 256) MCX_VIBM_X(256, 4, false);

@@ -2,7 +2,7 @@
 # round 4n: the final code: the whole GPU suite, smoke(), the driver's bench command, the default bench
 set -euo pipefail
 export TMPDIR=/tmp; mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread \
+AMD_LOG_LEVEL=1 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread \
   > gpurun_out/r04n_pytest_gpu.log 2>&1
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r04n_smoke.log 2>&1
 t0=$SECONDS
