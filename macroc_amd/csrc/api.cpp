@@ -1522,6 +1522,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.vi_lg = (int)value;
     return 0;
   }
+  if (!std::strcmp(name, "cg_p2d")) {
+    c.cg_p2d = value != 0.;
+    return 0;
+  }
   if (!std::strcmp(name, "vi_lg_exc")) {
     c.vi_lg_exc = value != 0.;
     return 0;

@@ -3486,21 +3486,32 @@ __global__ void k_cg_pupdate_db(Geo g, const double* __restrict__ z, const doubl
 struct PQ {
   double* p[8];
 };
-template <bool NT, bool DIX, bool SKIP_SENT = false, int PAR = 0, bool XS = false>
+// P2D (option cg_p2d): grid (ny nz rows, x chunks), the node's row from the block index, so the
+// row / plane split is scalar work instead of two vector integer divisions per node
+template <bool NT, bool DIX, bool SKIP_SENT = false, int PAR = 0, bool XS = false, bool P2D = false>
 __global__ void k_cg_pupdate_qb(Geo g, const double* __restrict__ z, const double* __restrict__ dinv,
                                 const unsigned char* __restrict__ jix, PQ pq, double* __restrict__ x,
                                 const CgState* __restrict__ cg, int* __restrict__ xdone,
                                 const int* __restrict__ list, int64_t cnt, int rev = 0) {
   constexpr int M = XS ? 7 : 3;  // buffer ring mask
   if (cg->reason) return;
-  const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  const int64_t t = P2D ? (int64_t)blockIdx.y * TPB + threadIdx.x : (int64_t)blockIdx.x * TPB + threadIdx.x;
   const int it = cg->i;
   const bool dox = it >= 4 && (it & 3) == 0;
-  if (t == 0 && dox) *xdone = it;
-  if (t >= cnt) return;
-  const int n = list ? list[t] : (int)(rev ? cnt - 1 - t : t);
-  int i, j, k;
-  node_ijk(g, n, i, j, k);
+  if (t == 0 && dox && (!P2D || blockIdx.x == 0)) *xdone = it;
+  int n, i, j, k;
+  if (P2D) {
+    const int row = blockIdx.x;  // (uniform)
+    i = (int)t;
+    if (i >= g.nx) return;
+    j = row % g.ny;
+    k = row / g.ny;
+    n = i + g.nx * row;
+  } else {
+    if (t >= cnt) return;
+    n = list ? list[t] : (int)(rev ? cnt - 1 - t : t);
+    node_ijk(g, n, i, j, k);
+  }
   if (SKIP_SENT && sent_node(g, i, j, k)) return;
   const int pc = pad_of(g, i, j, k);
   double* pn = pq.p[it & M];
@@ -5155,11 +5166,20 @@ void launch_cg_pupdate(Ctx& c, int part) {
   if (c.pqb_used) {  // p in four buffers, x every fourth iteration
     const int par = c.cg_par && c.cg_it >= 1 ? 1 + (c.cg_it >= 4 && (c.cg_it & 3) == 0) : 0;
     const PQ pq = pq_of(c);
+    // P2D: the whole-subdomain update only (not the sent-node list), natural order
+    const bool p2d = c.cg_p2d && part != 1 && !c.cg_rev;
+    const dim3 g2d((unsigned)(c.g.ny * c.g.nz), (unsigned)((c.g.nx + TPB - 1) / TPB));
 #define MCX_PQB_PAR(SKIPV, GRID, LIST, CNT)                                                                          \
   MCX_NT_DIX(c.cg_nt, dix, {                                                                                         \
     if (c.xs_used)                                                                                                   \
       hipLaunchKernelGGL((k_cg_pupdate_qb<NT, DX, SKIPV, 1, true>), dim3(GRID), dim3(TPB), 0, c.stream, c.g, zs, jd,  \
                          c.jix, pq, c.du, c.cg, c.xdone, LIST, CNT, c.cg_rev);                                       \
+    else if (p2d && par == 1)                                                                                        \
+      hipLaunchKernelGGL((k_cg_pupdate_qb<NT, DX, SKIPV, 1, false, true>), g2d, dim3(TPB), 0, c.stream, c.g, zs, jd,  \
+                         c.jix, pq, c.du, c.cg, c.xdone, LIST, CNT, 0);                                              \
+    else if (p2d && par == 2)                                                                                        \
+      hipLaunchKernelGGL((k_cg_pupdate_qb<NT, DX, SKIPV, 2, false, true>), g2d, dim3(TPB), 0, c.stream, c.g, zs, jd,  \
+                         c.jix, pq, c.du, c.cg, c.xdone, LIST, CNT, 0);                                              \
     else if (par == 1)                                                                                               \
       hipLaunchKernelGGL((k_cg_pupdate_qb<NT, DX, SKIPV, 1>), dim3(GRID), dim3(TPB), 0, c.stream, c.g, zs, jd, c.jix, \
                          pq, c.du, c.cg, c.xdone, LIST, CNT, c.cg_rev);                                              \

@@ -753,12 +753,14 @@ def test_cg_pdb_bitwise(maxits, storage):
             m.set_option("vi_stage", 1)
         m.apply_bc_on_u(m.get_displacement(1))
         m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
-        for pdb, par, rev, xs in ((0, 0, 0, 0), (1, 0, 0, 0), (0, 1, 0, 0), (1, 1, 0, 0), (1, 1, 1, 0), (1, 0, 1, 0),
-                                  (4, 0, 0, 0), (4, 1, 0, 0), (4, 1, 1, 0), (4, 1, 0, 1), (4, 0, 1, 1)):
+        for pdb, par, rev, xs, p2d in ((0, 0, 0, 0, 0), (1, 0, 0, 0, 0), (0, 1, 0, 0, 0), (1, 1, 0, 0, 0), (1, 1, 1, 0, 0),
+                                       (1, 0, 1, 0, 0), (4, 0, 0, 0, 0), (4, 1, 0, 0, 0), (4, 1, 1, 0, 0), (4, 1, 0, 1, 0),
+                                       (4, 0, 1, 1, 0), (4, 1, 0, 0, 1)):
             m.set_option("cg_pdb", pdb)
             m.set_option("cg_par", par)
             m.set_option("cg_rev", rev)
             m.set_option("cg_xs", xs)
+            m.set_option("cg_p2d", p2d)
             its, rn, reason = m.solve_Ax()
             out.append((its, reason, m.du()))
     for its, reason, du in out[1:]:
