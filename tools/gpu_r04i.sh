@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 4i: the whole GPU suite and smoke() on the final code
+# round 4i: the whole GPU suite and smoke() on the final code (cg_ublocks A/B appended)
 set -euo pipefail
 export TMPDIR=/tmp; mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread \
