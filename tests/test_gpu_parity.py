@@ -734,6 +734,21 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
 
 
 
+def test_round4_options_refused():
+    """The round-4 A/B options take their documented values only; a refused value raises and
+    leaves the setting as it was (the solve after it matches the one before)."""
+    with M.Macroc(argv_for(24, 20, 12, 1e-10)) as m:
+        m.apply_bc_on_u(m.get_displacement(1))
+        m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
+        its0, _, _ = m.solve_Ax()
+        du0 = m.du()
+        for name, bad in (("vi_lg", 4), ("vi_lg", 0), ("vi_wdesc", 3), ("cg_ublocks", -1), ("cg_ublocks", 2.5)):
+            with pytest.raises(M.MacrocError):
+                m.set_option(name, bad)
+        its1, _, _ = m.solve_Ax()
+        assert its1 == its0 and np.array_equal(m.du(), du0)
+
+
 @pytest.mark.parametrize("maxits", [None, 37, 38, 39, 40, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("storage", ["vi", "vi_staged", "split"])
 def test_cg_pdb_bitwise(maxits, storage):
