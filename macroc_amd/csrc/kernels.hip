@@ -4877,6 +4877,7 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
         if (c.vi_fma) {
           if (tx == 256) MCX_VIBM(256, 4, true, true, true, true, false, false, false, true);
           else if (tx == 128) MCX_VIBM(128, 8, true, true, true, true, false, false, false, true);
+          else if (c.vi_lg == 2) MCX_VIBM(64, 16, true, true, true, true, false, false, false, true, 2);
           else MCX_VIBM(64, 16, true, true, true, true, false, false, false, true);
         } else {
           if (tx == 256) MCX_VIBM(256, 4, true, true, true, false, false, false, false, true);
