@@ -229,7 +229,7 @@ struct Ctx {
   int cg_ublocks = 0;        // k_cg_update grid cap (grid-stride; option cg_ublocks, 0 = one node per thread; A/B)
   int vi_lg = 2;             // staged block-indexed SpMV, LDS-dictionary waves: blocks whose reads are issued together (option vi_lg: 1, 2, 3)
   int cg_p2d = 0;            // quad-buffered p update on a (rows, x chunks) grid: no per-node divisions (option cg_p2d; A/B)
-  int vi_lg_exc = 0;         // vi_lg 2 also in the exception-node kernel (option vi_lg_exc; A/B)
+  int vi_lg_exc = 1;         // vi_lg 2 also in the exception-node kernel (option vi_lg_exc; 0: per-block waits)
   int vi_wdesc = 0;          // staged block-indexed SpMV: wave descriptors (option vi_wdesc): 1 = uniform waves, 2 = also two-set waves (FMA rows), 0 = off (A/B)
   unsigned* wd = nullptr;    // wave descriptors [plane][npy][npx][8] + 2 counters (build_wdesc)
   int64_t wd_bytes = 0;

@@ -262,9 +262,9 @@ def test_aij_vi_exception_nodes(grid, stage, vi_tx, tile):
         m.set_option("vi_fma", 1)
         y = m.spmv(x)
         assert np.all(np.abs(y - y1) <= 1e-14 * absrow + 1e-300)
-        m.set_option("vi_lg_exc", 1)  # the LDS-path reads in pairs in the exception kernel too: the same rows
+        m.set_option("vi_lg_exc", 0)  # per-block waits on the LDS path of the exception kernel: the same rows
         assert np.array_equal(m.spmv(x), y)
-        m.set_option("vi_lg_exc", 0)
+        m.set_option("vi_lg_exc", 1)
         its, rn, reason = m.solve_Ax()
         assert reason > 0 and abs(its - ref_its) <= 1
         assert np.linalg.norm(m.du() - P.du()) <= 50 * rtol * np.linalg.norm(P.du())
