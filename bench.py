@@ -300,6 +300,19 @@ def measure(argv, rank, world, comm_id, args, steps, warmup):
             "warmup_s": t_warm}
 
 
+def cg_iter_roofline(r):
+    """Bytes of one whole CG iteration of this rank (the SpMV's algorithmic bytes + the vector
+    kernels' per iteration, mcx_timing.cg_vec_bytes_per_iter) over the measured solve time per CG
+    iteration (every kernel, the reductions and the host polls included)."""
+    tm, its = r["tm"], max(r["its"], 1)
+    ms = tm["solve_ms"] / its
+    b = tm["spmv_bytes_per_launch"] + tm["cg_vec_bytes_per_iter"]
+    nown = r["info"]["ndofs_local"] // 3
+    return {"bytes_per_iter": b, "bytes_per_node": b / nown, "spmv_bytes": tm["spmv_bytes_per_launch"],
+            "vec_bytes": tm["cg_vec_bytes_per_iter"], "ms_per_cg_iter": ms, "achieved": b / (ms * 1e-3) / 1e9,
+            "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": b / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS}
+
+
 def nonlinear_leg(G, ts, dt, rtol, device, extra=()):
     """BASELINE config 5's path (G^3, the J2 Gauss-point law, non-linear Newton; tools/bench_nonlinear.py):
     time steps 0 .. ts-1 of src/main.c:49-109 in this process, default AIJ storage.  Reported beside
@@ -413,8 +426,9 @@ def main():
     bending = None
     bg = args.bending if args.bending is not None else (128 if world == 1 else 0)
     if bg > 0 and rank == 0:
-        # BC_BENDING plasticises the whole body (src/bcs.c:61-91): every node an exception node, so
-        # the AIJ storage is the exact split (upper blocks + lower corrections); SBAIJ beside it
+        # BC_BENDING (src/bcs.c:61-91) under the J2 law: the plastic zone grows from the clamped and
+        # loaded faces (32,768 exception nodes, 1.6 %, in round 4's line); the AIJ storage stays
+        # value-indexed with exception nodes below vi_exc_max, else AIJ-split; SBAIJ beside it
         bending = {}
         for mt in ("aij", "sbaij"):
             if time.perf_counter() - T_START + 60 > args.budget:
@@ -474,7 +488,11 @@ def main():
                          # this launch is than that bound (not a roofline fraction: it moves fewer bytes)
                          "csr_bytes_per_launch": r["csr_bytes"], "csr_ms_at_peak": csr_ms_at_peak,
                          "speedup_vs_csr_at_peak": csr_ms_at_peak / spmv_avg_ms,
-                         "limiter": lds_limiter(r["storage"], NX, NY, NZ)},
+                         "limiter": lds_limiter(r["storage"], NX, NY, NZ),
+                         # the whole CG iteration: SpMV bytes + the vector kernels'
+                         # (update, p update, amortised x update) per iteration over the measured
+                         # solve time per iteration (reductions and the host polls included)
+                         "cg_iter": cg_iter_roofline(r)},
             "cpu_baseline": cpu,
             "check": check,
             "variants": variants,

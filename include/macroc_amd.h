@@ -4,7 +4,12 @@
  * One context = one MPI-style rank = one GPU subdomain of the DMDA box decomposition.
  * Every entry point returns 0 on success and a non-zero code on failure, mirroring the
  * reference's PetscErrorCode convention (src/assembly.c:37-42 ... CHKERRQ); the message of
- * the last failure is available from mcx_last_error().  Host buffers are caller-owned;
+ * the last failure (per calling thread) is available from mcx_last_error().  No C++ exception
+ * crosses this interface: an internal one (e.g. a failed host allocation) returns 90 with its
+ * message.  Multi-rank host waits (CG polls, all-reduced norms) are bounded: after
+ * MCX_COMM_TIMEOUT seconds (default 300; option "comm_timeout"), or on an RCCL asynchronous
+ * error, the communicator is aborted and the call returns 24 / 25 naming the rank and the
+ * operation; later collectives of that context fail at once.  Host buffers are caller-owned;
  * the context owns all device memory.  A context is not thread-safe; different contexts
  * may be driven from different threads.  No torch / HIP types appear in this interface.
  *
@@ -156,6 +161,11 @@ typedef struct {
   int64_t spmv_launches;
   double spmv_ms_total;
   int64_t spmv_bytes_per_launch; /* algorithmic bytes of one SpMV (values + x once + y once) */
+  /* algorithmic bytes of the CG vector kernels per iteration of the last solve, averaged over the
+     iterations (VecAXPY(r) + PCApply_Jacobi + the two dots, VecAYPX(p), the deferred VecAXPY(x)
+     amortised over the iterations that apply it): with spmv_bytes_per_launch the bytes of one
+     whole CG iteration */
+  int64_t cg_vec_bytes_per_iter;
 } mcx_timing;
 
 const char* mcx_last_error(void);
@@ -186,6 +196,13 @@ int mcx_init(const mcx_opts* o, int rank, int nranks, const void* comm_id, void*
    collective entry point must then be called by all members). */
 int mcx_local_group_create(int nranks, int device, void** group);
 int mcx_local_group_destroy(void* group);
+/* MPI_Barrier(PETSC_COMM_WORLD) of the in-process transport (host only).  Every crossing of the
+   group's barrier — this one and those inside the collective entry points — is tagged with its
+   collective: a member reaching a different collective than the others, or a member missing for
+   MCX_COMM_TIMEOUT seconds (environment at group creation, default 300), fails the crossing with
+   a non-zero code naming the ranks and collectives, and every later crossing of that group fails
+   at once (instead of pairing unrelated collectives or hanging). */
+int mcx_local_group_barrier(void* group, int rank);
 int mcx_init_local(const mcx_opts* o, int rank, void* group, void** ctx);
 int mcx_finalize(void* ctx);
 int mcx_get_info(void* ctx, mcx_info* info);

@@ -31,7 +31,7 @@ KSP_REASONS = {2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL", -3: "DIVERGED_ITS", -4:
 # symbols declared in include/macroc_amd.h (checked by tests/test_abi.py)
 EXPORTS = [
     "mcx_last_error", "mcx_version", "mcx_default_opts", "mcx_parse_args", "mcx_comm_unique_id", "mcx_plan", "mcx_plan_halo", "mcx_init",
-    "mcx_local_group_create", "mcx_local_group_destroy", "mcx_init_local",
+    "mcx_local_group_create", "mcx_local_group_destroy", "mcx_local_group_barrier", "mcx_init_local",
     "mcx_finalize", "mcx_get_info", "mcx_material_set", "mcx_get_displacement", "mcx_zero_u", "mcx_apply_bc_u",
     "mcx_set_strains", "mcx_homogenize", "mcx_assembly_res", "mcx_assembly_jac", "mcx_solve", "mcx_update_u", "mcx_update_vars",
     "mcx_get_nonlinear_stats", "mcx_reduce_nonlinear", "mcx_calc_force", "mcx_write_vtu",
@@ -112,6 +112,7 @@ class Timing(C.Structure):
         ("strains_ms", C.c_double), ("homogenize_ms", C.c_double), ("residual_ms", C.c_double),
         ("jacobian_ms", C.c_double), ("solve_ms", C.c_double), ("update_ms", C.c_double),
         ("spmv_launches", C.c_int64), ("spmv_ms_total", C.c_double), ("spmv_bytes_per_launch", C.c_int64),
+        ("cg_vec_bytes_per_iter", C.c_int64),
     ]
 
     def as_dict(self):
@@ -145,6 +146,7 @@ def lib():
                                 i64, i64, i64, i64, i64, i64]
     L.mcx_local_group_create.argtypes = [C.c_int, C.c_int, C.POINTER(C.c_void_p)]
     L.mcx_local_group_destroy.argtypes = [vp]
+    L.mcx_local_group_barrier.argtypes = [vp, C.c_int]
     L.mcx_init_local.argtypes = [C.POINTER(Opts), C.c_int, vp, C.POINTER(C.c_void_p)]
     L.mcx_finalize.argtypes = [vp]
     L.mcx_get_info.argtypes = [vp, C.POINTER(Info)]
@@ -246,10 +248,14 @@ class LocalGroup:
         self._g = C.c_void_p()
         _check(lib().mcx_local_group_create(nranks, device, C.byref(self._g)), "mcx_local_group_create")
 
+    def barrier(self, rank):
+        """MPI_Barrier of the group (host only): fails on a missing member or a mismatched collective."""
+        _check(lib().mcx_local_group_barrier(self._g, int(rank)), "mcx_local_group_barrier")
+
     def destroy(self):
         if self._g:
-            _check(lib().mcx_local_group_destroy(self._g), "mcx_local_group_destroy")
-            self._g = C.c_void_p()
+            g, self._g = self._g, C.c_void_p()
+            _check(lib().mcx_local_group_destroy(g), "mcx_local_group_destroy")
 
 
 class Macroc:
@@ -276,8 +282,8 @@ class Macroc:
     # ---- lifecycle
     def finish(self):
         if self._ctx:
-            _check(lib().mcx_finalize(self._ctx), "mcx_finalize")
-            self._ctx = C.c_void_p()
+            ctx, self._ctx = self._ctx, C.c_void_p()  # freed even when finalize reports an error
+            _check(lib().mcx_finalize(ctx), "mcx_finalize")
 
     close = finish
 

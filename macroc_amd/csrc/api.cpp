@@ -17,6 +17,19 @@ namespace mcx {
 static thread_local std::string g_err;
 void set_error(const std::string& s) { g_err = s; }
 
+int exc_return(const char* fn, const char* what) {
+  try {
+    g_err = std::string(fn) + ": internal exception: " + what;
+  } catch (...) {
+  }
+  return MCX_EXC;
+}
+
+void test_inject(const char* fn) {
+  const char* e = std::getenv("MCX_TEST_THROW");
+  if (e && !std::strcmp(e, fn)) throw std::bad_alloc();
+}
+
 template <class T>
 static int dalloc(Ctx& c, T** p, int64_t n) {
   if (n <= 0) n = 1;
@@ -110,6 +123,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   c.lg = lg;
   c.rank = rank;
   c.nranks = nranks;
+  c.comm_timeout = comm_timeout_default();
   int ndev = 0;
   MCX_HIP(hipGetDeviceCount(&ndev));
   if (ndev <= 0) {
@@ -120,6 +134,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   MCX_HIP(hipSetDevice(c.device));
   int rc = setup_decomposition(c);
   if (rc) return rc;
+  if (lg && (rc = group_setup(c))) return rc;
   int ncu = 0;
   MCX_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, c.device));
   // z-marching tiles (sbaij and AIJ-split): one resident round of blocks, 256x4 phased tiles
@@ -198,7 +213,10 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   if (lg) {
     lg->members[rank] = &c;
     MCX_HIP(hipMemcpy(lg->d_red_ptrs + rank, &c.red_loc, sizeof(double*), hipMemcpyHostToDevice));
-    group_barrier(lg);
+    if ((rc = group_barrier(lg, rank, BAR_INIT))) {
+      lg->members[rank] = nullptr;
+      return rc;
+    }
   }
   return 0;
 }
@@ -265,7 +283,7 @@ static int cg_solve(Ctx& c, int* its, double* rnorm, int* reason) {
     MCX_HIP(hipMemcpyAsync(&c.h_cg[slot], c.cg, sizeof(CgState), hipMemcpyDeviceToHost, c.stream));
     MCX_HIP(hipEventRecord(c.ev_chunk[slot], c.stream));
     if (pending >= 0) {
-      MCX_HIP(hipEventSynchronize(c.ev_chunk[pending]));
+      if ((rc = comm_wait(c, c.ev_chunk[pending], "CG chunk poll (all-reduced CG scalars)"))) return rc;
       if (c.h_cg[pending].reason) break;
     }
     pending = slot;
@@ -273,7 +291,8 @@ static int cg_solve(Ctx& c, int* its, double* rnorm, int* reason) {
     if (issued > cap) break;
   }
   if ((rc = launch_cg_xfinal(c))) return rc;  // the owed VecAXPY(x, alpha, p) terms, deferred by k_cg_pupdate
-  MCX_HIP(hipStreamSynchronize(c.stream));
+  MCX_HIP(hipEventRecord(c.ev_chunk[slot], c.stream));  // after the last chunk's (gated) all-reduces
+  if ((rc = comm_wait(c, c.ev_chunk[slot], "CG solve end"))) return rc;
   CgState fin;
   MCX_HIP(hipMemcpy(&fin, c.cg, sizeof(CgState), hipMemcpyDeviceToHost));
   if (!fin.reason) {
@@ -353,7 +372,8 @@ void mcx_default_opts(mcx_opts* o) {
   o->mat_vi_fma = 1;
 }
 
-int mcx_parse_args(mcx_opts* o, int argc, const char* const* argv) {
+int mcx_parse_args(mcx_opts* o, int argc, const char* const* argv) try {
+  MCX_ENTRY();
   for (int a = 0; a < argc; a++) {
     const char* k = argv[a];
     const char* v = (a + 1 < argc) ? argv[a + 1] : nullptr;
@@ -431,9 +451,10 @@ int mcx_parse_args(mcx_opts* o, int argc, const char* const* argv) {
     std::fprintf(stderr, "WARNING! There are options you set that were not used: %s\n", k);
   }
   return 0;
-}
+} MCX_CATCH
 
-int mcx_init(const mcx_opts* o, int rank, int nranks, const void* comm_id, void** ctx) {
+int mcx_init(const mcx_opts* o, int rank, int nranks, const void* comm_id, void** ctx) try {
+  MCX_ENTRY();
   if (!o || !ctx || nranks < 1 || rank < 0 || rank >= nranks) {
     set_error("mcx_init: bad arguments");
     return 1;
@@ -449,9 +470,10 @@ int mcx_init(const mcx_opts* o, int rank, int nranks, const void* comm_id, void*
   }
   *ctx = c;
   return 0;
-}
+} MCX_CATCH
 
-int mcx_init_local(const mcx_opts* o, int rank, void* group, void** ctx) {
+int mcx_init_local(const mcx_opts* o, int rank, void* group, void** ctx) try {
+  MCX_ENTRY();
   auto* lg = static_cast<LocalGroup*>(group);
   if (!o || !ctx || !lg || rank < 0 || rank >= lg->nranks) {
     set_error("mcx_init_local: bad arguments");
@@ -468,18 +490,26 @@ int mcx_init_local(const mcx_opts* o, int rank, void* group, void** ctx) {
   }
   *ctx = c;
   return 0;
-}
+} MCX_CATCH
 
-int mcx_finalize(void* ctx) {
+int mcx_finalize(void* ctx) try {
+  MCX_ENTRY();
   Ctx* c = reinterpret_cast<Ctx*>(ctx);
+  int rc = 0;
   if (c && c->lg) {
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    group_barrier(c->lg);  // no member still copies from this context's buffers
+    // no member still copies from this context's buffers: every member drained its streams
+    // before crossing.  If the group broke (a member stopped, or reached another collective),
+    // the members' enqueued copies may still read these buffers: wait for the whole device.
+    if ((rc = group_barrier(c->lg, c->rank, BAR_FINALIZE))) (void)hipDeviceSynchronize();
     c->lg->members[c->rank] = nullptr;
   }
-  return free_ctx(c);
-}
+  const std::string e = g_err;
+  free_ctx(c);
+  if (rc) g_err = e;
+  return rc;
+} MCX_CATCH
 
 static void fill_info(const Ctx& c, mcx_info* in) {
   const Geo& g = c.g;
@@ -541,14 +571,16 @@ static void fill_info(const Ctx& c, mcx_info* in) {
 }
 
 
-int mcx_get_info(void* ctx, mcx_info* in) {
+int mcx_get_info(void* ctx, mcx_info* in) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   fill_info(c, in);
   return 0;
-}
+} MCX_CATCH
 
-int mcx_plan(const mcx_opts* o, int rank, int nranks, mcx_info* in) {
+int mcx_plan(const mcx_opts* o, int rank, int nranks, mcx_info* in) try {
+  MCX_ENTRY();
   if (!o || !in || nranks < 1 || rank < 0 || rank >= nranks) {
     set_error("mcx_plan: bad arguments");
     return 1;
@@ -564,10 +596,11 @@ int mcx_plan(const mcx_opts* o, int rank, int nranks, mcx_info* in) {
   c.nnz_global = count_nnz_rows(c, 0, 0, 0, o->NX, o->NY, o->NZ);
   fill_info(c, in);
   return 0;
-}
+} MCX_CATCH
 
 int mcx_plan_halo(const mcx_opts* o, int rank, int nranks, int* nnbr, int* nbr_rank, int64_t* send_cnt,
-                  int64_t* recv_cnt, int64_t* send_nat, int64_t* recv_nat, int64_t* nsend, int64_t* nrecv) {
+                  int64_t* recv_cnt, int64_t* send_nat, int64_t* recv_nat, int64_t* nsend, int64_t* nrecv) try {
+  MCX_ENTRY();
   if (!o || nranks < 1 || rank < 0 || rank >= nranks) {
     set_error("mcx_plan_halo: bad arguments");
     return 1;
@@ -594,9 +627,10 @@ int mcx_plan_halo(const mcx_opts* o, int rank, int nranks, int* nnbr, int* nbr_r
   if (recv_nat)
     for (int64_t t = 0; t < h.nrecv; t++) recv_nat[t] = pad_to_natural(c, ridx[t]);
   return 0;
-}
+} MCX_CATCH
 
-int mcx_material_set(void* ctx, int id, double E, double nu, double Sy, double Ka, int type) {
+int mcx_material_set(void* ctx, int id, double E, double nu, double Sy, double Ka, int type) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   (void)Sy;
@@ -613,7 +647,7 @@ int mcx_material_set(void* ctx, int id, double E, double nu, double Sy, double K
     return 3;
   }
   return 0;
-}
+} MCX_CATCH
 
 double mcx_get_displacement(void* ctx, int time_s) {
   Ctx& c = *reinterpret_cast<Ctx*>(ctx);
@@ -622,22 +656,25 @@ double mcx_get_displacement(void* ctx, int time_s) {
   return -1.0 * (time / c.o.final_time);
 }
 
-int mcx_zero_u(void* ctx) {
+int mcx_zero_u(void* ctx) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   MCX_HIP(hipMemsetAsync(c.u_pad, 0, sizeof(double) * 3 * (size_t)c.g.PX * c.g.PY * c.g.PZ, c.stream));
   return 0;
-}
+} MCX_CATCH
 
-int mcx_apply_bc_u(void* ctx, double U) {
+int mcx_apply_bc_u(void* ctx, double U) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   launch_apply_bc_u(c, U);
   MCX_HIP(hipGetLastError());
   return 0;
-}
+} MCX_CATCH
 
-int mcx_set_strains(void* ctx) {
+int mcx_set_strains(void* ctx) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   PhaseTimer t(c, PH_STRAINS);
@@ -646,7 +683,7 @@ int mcx_set_strains(void* ctx) {
   launch_strains(c);
   MCX_HIP(hipGetLastError());
   return 0;
-}
+} MCX_CATCH
 
 // -mat_law external: the registered law fills sig and ctan from eps (see macroc_amd.h)
 static int external_homogenize(Ctx& c) {
@@ -693,7 +730,8 @@ static int external_homogenize(Ctx& c) {
   return 0;
 }
 
-int mcx_homogenize(void* ctx) {
+int mcx_homogenize(void* ctx) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   PhaseTimer t(c, PH_HOMOG);
@@ -701,7 +739,7 @@ int mcx_homogenize(void* ctx) {
   launch_homogenize(c);
   MCX_HIP(hipGetLastError());
   return 0;
-}
+} MCX_CATCH
 
 static int need_external(Ctx& c, const char* fn) {
   if (c.mat.law == MCX_LAW_EXTERNAL) return 0;
@@ -709,7 +747,8 @@ static int need_external(Ctx& c, const char* fn) {
   return 7;
 }
 
-int mcx_set_micropp(void* ctx, const mcx_micropp_api* api) {
+int mcx_set_micropp(void* ctx, const mcx_micropp_api* api) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   if (int rc = need_external(c, "mcx_set_micropp")) return rc;
@@ -721,9 +760,10 @@ int mcx_set_micropp(void* ctx, const mcx_micropp_api* api) {
   if (api) c.mpp = *api;
   if (api) c.has_dlaw = false;
   return 0;
-}
+} MCX_CATCH
 
-int mcx_set_device_law(void* ctx, const mcx_device_law* law) {
+int mcx_set_device_law(void* ctx, const mcx_device_law* law) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   if (int rc = need_external(c, "mcx_set_device_law")) return rc;
@@ -735,7 +775,7 @@ int mcx_set_device_law(void* ctx, const mcx_device_law* law) {
   if (law) c.dlaw = *law;
   if (law) c.has_mpp = false;
   return 0;
-}
+} MCX_CATCH
 
 // host [ngp][ncomp] (gpi order) <-> device [ncomp][8][nelem]
 static int gp_upload(Ctx& c, const double* host, double* dev, int ncomp) {
@@ -749,21 +789,24 @@ static int gp_upload(Ctx& c, const double* host, double* dev, int ncomp) {
   return 0;
 }
 
-int mcx_set_gp_stress(void* ctx, const double* host) {
+int mcx_set_gp_stress(void* ctx, const double* host) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   if (int rc = need_external(c, "mcx_set_gp_stress")) return rc;
   return gp_upload(c, host, c.sig, 6);
-}
+} MCX_CATCH
 
-int mcx_set_gp_ctan(void* ctx, const double* host) {
+int mcx_set_gp_ctan(void* ctx, const double* host) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   if (int rc = need_external(c, "mcx_set_gp_ctan")) return rc;
   return gp_upload(c, host, c.ctan, 36);
-}
+} MCX_CATCH
 
-int mcx_get_gp_strain(void* ctx, double* host) {
+int mcx_get_gp_strain(void* ctx, double* host) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   const int64_t E = c.g.nelem, ngp = 8 * E;
@@ -774,9 +817,10 @@ int mcx_get_gp_strain(void* ctx, double* host) {
     for (int gp = 0; gp < 8; gp++)
       for (int k = 0; k < 6; k++) host[(e * 8 + gp) * 6 + k] = soa[(size_t)k * ngp + gp * E + e];
   return 0;
-}
+} MCX_CATCH
 
-int mcx_assembly_res(void* ctx, double* norm2) {
+int mcx_assembly_res(void* ctx, double* norm2) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   {
@@ -787,11 +831,12 @@ int mcx_assembly_res(void* ctx, double* norm2) {
   }
   double nrm = 0.;
   MCX_HIP(hipMemcpyAsync(&c.h_cg[0].dp, c.red, sizeof(double), hipMemcpyDeviceToHost, c.stream));
-  MCX_HIP(hipStreamSynchronize(c.stream));
+  MCX_HIP(hipEventRecord(c.ev_chunk[0], c.stream));
+  if (int rc = comm_wait(c, c.ev_chunk[0], "assembly_res (all-reduced |RES|)")) return rc;
   nrm = c.h_cg[0].dp;
   if (norm2) *norm2 = nrm;
   return 0;
-}
+} MCX_CATCH
 
 // the AIJ stencil-block storage, allocated on first use when the context started with AIJ-split
 static int ensure_V(Ctx& c) {
@@ -820,7 +865,8 @@ static int ensure_VI(Ctx& c) {
   return 0;
 }
 
-int mcx_assembly_jac(void* ctx) {
+int mcx_assembly_jac(void* ctx) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   PhaseTimer t(c, PH_JAC);
@@ -879,9 +925,10 @@ int mcx_assembly_jac(void* ctx) {
   c.assembled = true;
   MCX_HIP(hipGetLastError());
   return 0;
-}
+} MCX_CATCH
 
-int mcx_solve(void* ctx, int* its, double* rnorm, int* reason) {
+int mcx_solve(void* ctx, int* its, double* rnorm, int* reason) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   if (!c.assembled) {
@@ -901,18 +948,20 @@ int mcx_solve(void* ctx, int* its, double* rnorm, int* reason) {
   if (rnorm) *rnorm = n0;
   if (reason) *reason = r0;
   return 0;
-}
+} MCX_CATCH
 
-int mcx_update_u(void* ctx) {
+int mcx_update_u(void* ctx) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   PhaseTimer t(c, PH_UPDATE);
   launch_update_u(c);
   MCX_HIP(hipGetLastError());
   return 0;
-}
+} MCX_CATCH
 
-int mcx_update_vars(void* ctx) {
+int mcx_update_vars(void* ctx) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   if (c.hist_old) std::swap(c.hist_old, c.hist_new);
@@ -925,9 +974,10 @@ int mcx_update_vars(void* ctx) {
     }
   }
   return 0;
-}
+} MCX_CATCH
 
-int mcx_get_nonlinear_stats(void* ctx, int64_t* n_nonlinear, double* f_trial_max) {
+int mcx_get_nonlinear_stats(void* ctx, int64_t* n_nonlinear, double* f_trial_max) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   int64_t n = 0;
@@ -968,7 +1018,7 @@ int mcx_get_nonlinear_stats(void* ctx, int64_t* n_nonlinear, double* f_trial_max
   if (n_nonlinear) *n_nonlinear = n;
   if (f_trial_max) *f_trial_max = fm;
   return 0;
-}
+} MCX_CATCH
 
 }  // extern "C"
 
@@ -981,13 +1031,14 @@ static int host_allreduce(Ctx& c, double* v, int n, int op) {
   rc = op ? allreduce_max(c, c.red_loc, c.red, n) : allreduce_sum(c, c.red_loc, c.red, n);
   if (rc) return rc;
   MCX_HIP(hipMemcpyAsync(v, c.red, sizeof(double) * n, hipMemcpyDeviceToHost, c.stream));
-  MCX_HIP(hipStreamSynchronize(c.stream));
-  return 0;
+  MCX_HIP(hipEventRecord(c.ev_chunk[0], c.stream));
+  return comm_wait(c, c.ev_chunk[0], op ? "host all-reduce (max)" : "host all-reduce (sum)");
 }
 
 extern "C" {
 
-int mcx_reduce_nonlinear(void* ctx, int64_t* n_local, int64_t* n_total, double* f_trial_max) {
+int mcx_reduce_nonlinear(void* ctx, int64_t* n_local, int64_t* n_total, double* f_trial_max) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   int64_t n = 0;
@@ -1000,9 +1051,10 @@ int mcx_reduce_nonlinear(void* ctx, int64_t* n_local, int64_t* n_total, double* 
   if (n_total) *n_total = (int64_t)s;
   if (f_trial_max) *f_trial_max = fm;
   return 0;
-}
+} MCX_CATCH
 
-int mcx_calc_force(void* ctx, double* force) {
+int mcx_calc_force(void* ctx, double* force) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   const Geo& g = c.g;
@@ -1051,9 +1103,10 @@ int mcx_calc_force(void* ctx, double* force) {
   if ((rc = host_allreduce(c, &mpi_force, 1, 0))) return rc;
   if (force) *force = mpi_force;
   return 0;
-}
+} MCX_CATCH
 
-int mcx_time_step(void* ctx, int time_s, int* newton_its, double* res, int* ksp_its, double* ksp_rnorm) {
+int mcx_time_step(void* ctx, int time_s, int* newton_its, double* res, int* ksp_its, double* ksp_rnorm) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   int rc;
@@ -1078,26 +1131,28 @@ int mcx_time_step(void* ctx, int time_s, int* newton_its, double* res, int* ksp_
   if ((rc = mcx_update_vars(ctx))) return rc;  // src/main.c:83
   MCX_HIP(hipStreamSynchronize(c.stream));
   return 0;
-}
+} MCX_CATCH
 
 // ---------------------------------------------------------------- data access
-int mcx_get_u(void* ctx, double* host) {
+int mcx_get_u(void* ctx, double* host) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   launch_copy_pad_to_owned(c, c.u_pad, c.tmp);
   MCX_HIP(hipMemcpyAsync(host, c.tmp, sizeof(double) * 3 * c.g.nown, hipMemcpyDeviceToHost, c.stream));
   MCX_HIP(hipStreamSynchronize(c.stream));
   return 0;
-}
+} MCX_CATCH
 
-int mcx_set_u(void* ctx, const double* host) {
+int mcx_set_u(void* ctx, const double* host) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   MCX_HIP(hipMemcpyAsync(c.tmp, host, sizeof(double) * 3 * c.g.nown, hipMemcpyHostToDevice, c.stream));
   launch_copy_owned_to_pad(c, c.tmp, c.u_pad);
   MCX_HIP(hipStreamSynchronize(c.stream));
   return 0;
-}
+} MCX_CATCH
 
 static int get_owned(Ctx& c, const double* d, double* host) {
   MCX_HIP(hipMemcpyAsync(host, d, sizeof(double) * 3 * c.g.nown, hipMemcpyDeviceToHost, c.stream));
@@ -1105,17 +1160,19 @@ static int get_owned(Ctx& c, const double* d, double* host) {
   return 0;
 }
 
-int mcx_get_b(void* ctx, double* host) {
+int mcx_get_b(void* ctx, double* host) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   return get_owned(c, c.b, host);
-}
+} MCX_CATCH
 
-int mcx_get_du(void* ctx, double* host) {
+int mcx_get_du(void* ctx, double* host) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   return get_owned(c, c.du, host);
-}
+} MCX_CATCH
 
 static int get_gp(Ctx& c, const double* d, double* host) {
   const Geo& g = c.g;
@@ -1140,19 +1197,22 @@ static int get_gp(Ctx& c, const double* d, double* host) {
   return 0;
 }
 
-int mcx_get_strain(void* ctx, double* host) {
+int mcx_get_strain(void* ctx, double* host) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   return get_gp(c, c.eps, host);
-}
+} MCX_CATCH
 
-int mcx_get_stress(void* ctx, double* host) {
+int mcx_get_stress(void* ctx, double* host) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   return get_gp(c, c.sig, host);
-}
+} MCX_CATCH
 
-int mcx_owned_dofs(void* ctx, int64_t* petsc, int64_t* natural) {
+int mcx_owned_dofs(void* ctx, int64_t* petsc, int64_t* natural) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   const Geo& g = c.g;
@@ -1166,9 +1226,10 @@ int mcx_owned_dofs(void* ctx, int64_t* petsc, int64_t* natural) {
     }
   }
   return 0;
-}
+} MCX_CATCH
 
-int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
+int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   if (vals && !c.assembled) {
@@ -1307,9 +1368,10 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) {
     }
   }
   return 0;
-}
+} MCX_CATCH
 
-int mcx_dump_dirichlet(void* ctx, int64_t* idx, int64_t* n) {
+int mcx_dump_dirichlet(void* ctx, int64_t* idx, int64_t* n) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   const Geo& g = c.g;
@@ -1331,9 +1393,10 @@ int mcx_dump_dirichlet(void* ctx, int64_t* idx, int64_t* n) {
   }
   *n = cnt;
   return 0;
-}
+} MCX_CATCH
 
-int mcx_spmv(void* ctx, const double* x_host, double* y_host) {
+int mcx_spmv(void* ctx, const double* x_host, double* y_host) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   if (!c.assembled) {
@@ -1349,9 +1412,10 @@ int mcx_spmv(void* ctx, const double* x_host, double* y_host) {
   MCX_HIP(hipMemcpyAsync(y_host, c.tmp, sizeof(double) * 3 * c.g.nown, hipMemcpyDeviceToHost, c.stream));
   MCX_HIP(hipStreamSynchronize(c.stream));
   return 0;
-}
+} MCX_CATCH
 
-int mcx_get_ksp_history(void* ctx, double* hist, int64_t* n) {
+int mcx_get_ksp_history(void* ctx, double* hist, int64_t* n) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   int64_t have = (int64_t)c.last_hist.size();
@@ -1359,16 +1423,18 @@ int mcx_get_ksp_history(void* ctx, double* hist, int64_t* n) {
   if (hist) std::memcpy(hist, c.last_hist.data(), sizeof(double) * k);
   *n = have;
   return 0;
-}
+} MCX_CATCH
 
-int mcx_set_timing(void* ctx, int on) {
+int mcx_set_timing(void* ctx, int on) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   c.timing = on != 0;
   return 0;
-}
+} MCX_CATCH
 
-int mcx_get_timing(void* ctx, mcx_timing* t) {
+int mcx_get_timing(void* ctx, mcx_timing* t) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   MCX_HIP(hipStreamSynchronize(c.stream));
@@ -1398,10 +1464,12 @@ int mcx_get_timing(void* ctx, mcx_timing* t) {
   }
   // the fused p update (cg_fusep): r and the diagonal index read, p(i) written
   if (c.fusep_used) t->spmv_bytes_per_launch += (int64_t)c.g.nown * (24 + 1 + 24);
+  t->cg_vec_bytes_per_iter = cg_vec_bytes_per_node(c) * (int64_t)c.g.nown;
   return 0;
-}
+} MCX_CATCH
 
-int mcx_set_option(void* ctx, const char* name, double value) {
+int mcx_set_option(void* ctx, const char* name, double value) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   if (!std::strcmp(name, "spmv_subl")) {
@@ -1455,6 +1523,14 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.fuse = value != 0.;
     return 0;
   }
+  if (!std::strcmp(name, "comm_timeout")) {  // seconds a host wait on collective work may take
+    if (!(value > 0.)) {
+      set_error("comm_timeout: seconds > 0");
+      return 1;
+    }
+    c.comm_timeout = value;
+    return 0;
+  }
   if (!std::strcmp(name, "halo_overlap")) {
     c.overlap = value != 0.;
     return 0;
@@ -1485,19 +1561,23 @@ int mcx_set_option(void* ctx, const char* name, double value) {
     c.vi_block_on = value != 0.;
     return 0;
   }
-  if (!std::strcmp(name, "cg_pdb")) {  // 0 | 1 (two p buffers) | 4 (four)
-    if (!(value == 0. || value == 1. || value == 2. || value == 4.)) {
+  if (!std::strcmp(name, "cg_pdb")) {  // 0 | 1 (two p buffers) | 4 (four, the default)
+    if (!(value == 0. || value == 1. || value == 4.)) {
       set_error("cg_pdb: 0, 1 (two p buffers) or 4 (four)");
       return 1;
     }
-    c.cg_pdb = value == 4. ? 4 : (value != 0.);
+    c.cg_pdb = (int)value;
     return 0;
   }
   if (!std::strcmp(name, "cg_rev")) {
     c.cg_rev = value != 0.;
     return 0;
   }
-  if (!std::strcmp(name, "cg_par")) {
+  if (!std::strcmp(name, "cg_par")) {  // 0 | 1 (the host's parity hint) | 2 (a skewed hint: testing)
+    if (!(value == 0. || value == 1. || value == 2.)) {
+      set_error("cg_par: 0, 1 or 2 (testing: a wrong hint)");
+      return 1;
+    }
     c.cg_par = (int)value;
     return 0;
   }
@@ -1654,9 +1734,10 @@ int mcx_set_option(void* ctx, const char* name, double value) {
   }
   set_error(std::string("unknown option ") + name);
   return 2;
-}
+} MCX_CATCH
 
-int mcx_time_spmv(void* ctx, int iters, double* avg_ms) {
+int mcx_time_spmv(void* ctx, int iters, double* avg_ms) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   if (!c.assembled) {
@@ -1672,13 +1753,14 @@ int mcx_time_spmv(void* ctx, int iters, double* avg_ms) {
   MCX_HIP(hipEventElapsedTime(&ms, c.ev_a, c.ev_b));
   *avg_ms = ms / std::max(iters, 1);
   return 0;
-}
+} MCX_CATCH
 
-int mcx_synchronize(void* ctx) {
+int mcx_synchronize(void* ctx) try {
+  MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
   MCX_HIP(hipStreamSynchronize(c.stream));
   return 0;
-}
+} MCX_CATCH
 
 }  // extern "C"

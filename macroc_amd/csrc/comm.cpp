@@ -9,9 +9,12 @@
 // finished (waited for by the compute stream) before the next all-reduce is enqueued.
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <thread>
 
 #include "mcx_internal.h"
 
@@ -50,17 +53,130 @@ void comm_destroy(Ctx& c) {
   }
 }
 
-void group_barrier(LocalGroup* g) {
+double comm_timeout_default() {
+  const char* e = std::getenv("MCX_COMM_TIMEOUT");
+  const double v = e ? std::atof(e) : 0.;
+  return v > 0. ? v : 300.;
+}
+
+static const char* bar_name(int tag) {
+  switch (tag) {
+    case BAR_INIT: return "mcx_init_local";
+    case BAR_HALO_PACKED: return "halo exchange (packed)";
+    case BAR_HALO_DONE: return "halo exchange (copied)";
+    case BAR_RED_IN: return "all-reduce (partials)";
+    case BAR_RED_SUM: return "all-reduce (summed)";
+    case BAR_FINALIZE: return "mcx_finalize";
+    default: return "mcx_local_group_barrier";
+  }
+}
+
+// The in-process group's host barrier.  Members must cross the same sequence of collectives; a
+// crossing carries the collective's tag, and a member arriving with another tag than the first
+// arrival of the open generation breaks the group (the RCCL analogue is a mismatched collective,
+// which hangs).  A generation still open after timeout_s breaks it too (a member that stopped,
+// e.g. after an error of its own).  A broken group fails every later crossing at once, so no
+// member proceeds to read a peer's buffers on an exchange the peer is not part of.
+int group_barrier(LocalGroup* g, int rank, int tag) {
   auto* m = static_cast<std::mutex*>(g->mtx);
   auto* cv = static_cast<std::condition_variable*>(g->cv);
   std::unique_lock<std::mutex> lk(*m);
-  int gen = g->generation;
+  auto fail = [&]() {
+    set_error("in-process group: " + g->why);
+    return 23;
+  };
+  if (g->broken) return fail();
+  if (g->count == 0) {
+    g->cur_tag = tag;
+    g->cur_rank = rank;
+  } else if (g->cur_tag != tag) {
+    g->broken = true;
+    g->why = "mismatched collectives: rank " + std::to_string(rank) + " entered " + bar_name(tag) + ", rank " +
+             std::to_string(g->cur_rank) + " " + bar_name(g->cur_tag);
+    cv->notify_all();
+    return fail();
+  }
+  const int gen = g->generation;
   if (++g->count == g->nranks) {
     g->count = 0;
     g->generation++;
     cv->notify_all();
-  } else {
-    cv->wait(lk, [&] { return g->generation != gen; });
+    return 0;
+  }
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(g->timeout_s);
+  if (!cv->wait_until(lk, deadline, [&] { return g->generation != gen || g->broken; })) {
+    g->broken = true;
+    g->why = "rank " + std::to_string(rank) + " waited " + std::to_string((int)g->timeout_s) + " s in " +
+             bar_name(tag) + ": " + std::to_string(g->count) + " of " + std::to_string(g->nranks) +
+             " members arrived (a member stopped or skipped the collective)";
+    cv->notify_all();
+    return fail();
+  }
+  if (g->generation == gen) return fail();  // broken while waiting
+  return 0;
+}
+
+// events and the partial-sum pointer table of the group (first mcx_init_local; the group itself
+// is host-only, so it can be created and its barrier exercised without a GPU)
+static int group_device_setup(LocalGroup* g) {
+  std::lock_guard<std::mutex> lk(*static_cast<std::mutex*>(g->mtx));
+  if (g->dev_ready) return 0;
+  for (auto* v : {&g->ev_packed, &g->ev_halo_done, &g->ev_red, &g->ev_sum}) {
+    v->assign(g->nranks, nullptr);
+    for (auto& e : *v) MCX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  MCX_HIP(hipMalloc(&g->d_red_ptrs, sizeof(double*) * g->nranks));
+  g->dev_ready = true;
+  return 0;
+}
+int group_setup(Ctx& c) { return group_device_setup(c.lg); }
+
+int comm_check(Ctx& c) {
+  if (!c.comm_broken) return 0;
+  set_error("rank " + std::to_string(c.rank) + ": communicator aborted earlier: " + c.comm_why);
+  return 24;
+}
+
+static void comm_abort(Ctx& c, const std::string& why) {
+  c.comm_broken = true;
+  c.comm_why = why;
+  if (c.comm) {
+    (void)ncclCommAbort((ncclComm_t)c.comm);  // RCCL kernels waiting on peers return
+    c.comm = nullptr;
+  }
+  set_error("rank " + std::to_string(c.rank) + ": " + why);
+}
+
+int comm_wait(Ctx& c, hipEvent_t ev, const char* what) {
+  if (int rc = comm_check(c)) return rc;
+  if (c.nranks <= 1 && !c.comm) {
+    MCX_HIP(hipEventSynchronize(ev));
+    return 0;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int spin = 0;; spin++) {
+    const hipError_t e = hipEventQuery(ev);
+    if (e == hipSuccess) return 0;
+    if (e != hipErrorNotReady) {
+      comm_abort(c, std::string(what) + ": hipEventQuery: " + hipGetErrorString(e));
+      return 10;
+    }
+    if (c.comm) {
+      ncclResult_t ar = ncclSuccess;
+      const ncclResult_t r = ncclCommGetAsyncError((ncclComm_t)c.comm, &ar);
+      if (r != ncclSuccess || (ar != ncclSuccess && ar != ncclInProgress)) {
+        comm_abort(c, std::string(what) + ": RCCL asynchronous error: " +
+                          ncclGetErrorString(r != ncclSuccess ? r : ar) + " (communicator aborted)");
+        return 25;
+      }
+    }
+    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (dt > c.comm_timeout) {
+      comm_abort(c, std::string(what) + " not complete after " + std::to_string((int)c.comm_timeout) +
+                        " s (a peer rank stopped, or the ranks issued different collectives); communicator aborted");
+      return 24;
+    }
+    if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
 }
 
@@ -73,6 +189,7 @@ void group_barrier(LocalGroup* g) {
 // the exchange (cg_iteration: the interior p update).
 int halo_start(Ctx& c, double* xpad) {
   if (c.nranks <= 1 || c.halo.nbr_rank.empty()) return 0;
+  if (int rc = comm_check(c)) return rc;
   HaloPlan& h = c.halo;
   if (c.lg) {
     LocalGroup* g = c.lg;
@@ -83,7 +200,7 @@ int halo_start(Ctx& c, double* xpad) {
     // the copies below overwrite my receive buffer: order them after my compute stream's last
     // reader of it (the previous halo's k_unpack), as the RCCL branch does
     MCX_HIP(hipStreamWaitEvent(c.comm_stream, g->ev_packed[c.rank], 0));
-    group_barrier(g);
+    if (int rc = group_barrier(g, c.rank, BAR_HALO_PACKED)) return rc;
     for (size_t t = 0; t < h.nbr_rank.size(); t++) {
       const Ctx& q = *g->members[h.nbr_rank[t]];
       size_t idx = 0;
@@ -98,7 +215,8 @@ int halo_start(Ctx& c, double* xpad) {
     }
     MCX_HIP(hipEventRecord(g->ev_halo_done[c.rank], c.comm_stream));
     MCX_HIP(hipEventRecord(c.ev_comm, c.comm_stream));
-    group_barrier(g);  // every member recorded ev_halo_done before anyone waits on it again
+    // every member recorded ev_halo_done before anyone waits on it again
+    if (int rc = group_barrier(g, c.rank, BAR_HALO_DONE)) return rc;
     return 0;
   }
   launch_pack(c, xpad);
@@ -129,6 +247,7 @@ int halo_exchange(Ctx& c, double* xpad) {
 }
 
 static int allreduce_op(Ctx& c, const double* in, double* out, int count, int op) {
+  if (int rc = comm_check(c)) return rc;
   if (c.nranks <= 1 && !c.comm) {
     if (in != out) MCX_HIP(hipMemcpyAsync(out, in, sizeof(double) * count, hipMemcpyDeviceToDevice, c.stream));
     return 0;
@@ -136,11 +255,11 @@ static int allreduce_op(Ctx& c, const double* in, double* out, int count, int op
   if (c.lg) {
     LocalGroup* g = c.lg;
     MCX_HIP(hipEventRecord(g->ev_red[c.rank], c.stream));
-    group_barrier(g);
+    if (int rc = group_barrier(g, c.rank, BAR_RED_IN)) return rc;
     for (int q = 0; q < g->nranks; q++) MCX_HIP(hipStreamWaitEvent(c.stream, g->ev_red[q], 0));
     launch_group_sum(c, (const double* const*)g->d_red_ptrs, g->nranks, count, out, op);
     MCX_HIP(hipEventRecord(g->ev_sum[c.rank], c.stream));
-    group_barrier(g);
+    if (int rc = group_barrier(g, c.rank, BAR_RED_SUM)) return rc;
     return 0;
   }
   MCX_NCCL(ncclAllReduce(in, out, count, ncclDouble, op ? ncclMax : ncclSum, (ncclComm_t)c.comm, c.stream));
@@ -160,43 +279,55 @@ int allreduce_prepare(Ctx& c) {
 
 }  // namespace mcx
 
-extern "C" int mcx_local_group_create(int nranks, int device, void** group) {
+extern "C" int mcx_local_group_create(int nranks, int device, void** group) try {
+  MCX_ENTRY();
   using namespace mcx;
   if (nranks < 1 || !group) {
     set_error("mcx_local_group_create: bad arguments");
     return 1;
   }
-  MCX_HIP(hipSetDevice(device));
   auto* g = new LocalGroup();
   g->nranks = nranks;
   g->device = device;
   g->members.assign(nranks, nullptr);
   g->mtx = new std::mutex();
   g->cv = new std::condition_variable();
-  for (auto* v : {&g->ev_packed, &g->ev_halo_done, &g->ev_red, &g->ev_sum}) {
-    v->resize(nranks);
-    for (auto& e : *v) MCX_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  }
-  MCX_HIP(hipMalloc(&g->d_red_ptrs, sizeof(double*) * nranks));
+  g->timeout_s = comm_timeout_default();
   *group = g;
   return 0;
-}
+} MCX_CATCH
 
-extern "C" int mcx_local_group_destroy(void* group) {
+extern "C" int mcx_local_group_destroy(void* group) try {
+  MCX_ENTRY();
   using namespace mcx;
   auto* g = static_cast<LocalGroup*>(group);
   if (!g) return 0;
-  (void)hipSetDevice(g->device);
-  for (auto* v : {&g->ev_packed, &g->ev_halo_done, &g->ev_red, &g->ev_sum})
-    for (auto& e : *v) (void)hipEventDestroy(e);
-  (void)hipFree(g->d_red_ptrs);
+  if (g->dev_ready) {
+    (void)hipSetDevice(g->device);
+    for (auto* v : {&g->ev_packed, &g->ev_halo_done, &g->ev_red, &g->ev_sum})
+      for (auto& e : *v)
+        if (e) (void)hipEventDestroy(e);
+    if (g->d_red_ptrs) (void)hipFree(g->d_red_ptrs);
+  }
   delete static_cast<std::mutex*>(g->mtx);
   delete static_cast<std::condition_variable*>(g->cv);
   delete g;
   return 0;
-}
+} MCX_CATCH
 
-extern "C" int mcx_comm_unique_id(void* id) {
+extern "C" int mcx_local_group_barrier(void* group, int rank) try {
+  MCX_ENTRY();
+  using namespace mcx;
+  auto* g = static_cast<LocalGroup*>(group);
+  if (!g || rank < 0 || rank >= g->nranks) {
+    set_error("mcx_local_group_barrier: bad arguments");
+    return 1;
+  }
+  return group_barrier(g, rank, BAR_USER);
+} MCX_CATCH
+
+extern "C" int mcx_comm_unique_id(void* id) try {
+  MCX_ENTRY();
   ncclUniqueId uid;
   ncclResult_t r = ncclGetUniqueId(&uid);
   if (r != ncclSuccess) {
@@ -205,4 +336,4 @@ extern "C" int mcx_comm_unique_id(void* id) {
   }
   std::memcpy(id, &uid, sizeof(uid));
   return 0;
-}
+} MCX_CATCH

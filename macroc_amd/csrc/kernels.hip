@@ -3520,12 +3520,14 @@ __global__ void k_cg_pupdate_qb(Geo g, const double* __restrict__ z, const doubl
     for (int d = 0; d < 3; d++) st<NT>(&pn[3 * pc + d], z_of<DIX>(z, dinv, jix, n, d));
     return;
   }
-  // the host's parity guess must match the device's count, else the generic path below
-  const bool par_ok = PAR == 0 || (PAR == 2) == dox;
+  // the x terms follow the device's count (dox), whatever the host's parity hint PAR: a wrong
+  // hint costs a kernel built for the other branch, never an x term (a PAR 1 launch
+  // at i = 4m used to mark xdone without applying the four owed terms).  cg_par 2 skews the hint
+  // on purpose (test_cg_par_hint_mismatch_bitwise).
   const double* po = pq.p[(it - 1) & M];
   const double bc = cg->bcoef;
   double pv[3], zv[3];
-  if (!XS && ((PAR == 2 && par_ok) || (PAR == 0 && dox))) {
+  if (!XS && dox) {
     const double* p3 = pq.p[(it - 3) & 3];
     const double* p2 = pq.p[(it - 2) & 3];
     const double a4 = cg->ah[(it - 4) & 7], a3 = cg->ah[(it - 3) & 7], a2 = cg->ah[(it - 2) & 7],
@@ -5165,7 +5167,9 @@ void launch_cg_pupdate(Ctx& c, int part) {
   const double* zs = dix ? c.r : c.z;
   const double* jd = dix ? c.jdd : c.dinv;
   if (c.pqb_used) {  // p in four buffers, x every fourth iteration
-    const int par = c.cg_par && c.cg_it >= 1 ? 1 + (c.cg_it >= 4 && (c.cg_it & 3) == 0) : 0;
+    // the host's hint of the iteration's kind (cg_par 2: deliberately wrong at it = 4m - 1 and 4m)
+    const int hit = c.cg_it + (c.cg_par == 2);
+    const int par = c.cg_par && c.cg_it >= 1 ? 1 + (hit >= 4 && (hit & 3) == 0) : 0;
     const PQ pq = pq_of(c);
     // P2D: the whole-subdomain update only (not the sent-node list), natural order
     const bool p2d = c.cg_p2d && part != 1 && !c.cg_rev;
@@ -5204,7 +5208,7 @@ void launch_cg_pupdate(Ctx& c, int part) {
   }
   if (c.pdb_used) {  // p double-buffered, x every second iteration
     // cg_par: the kernel of the iteration's parity (the host's count; the kernel checks it)
-    const int par = c.cg_par && c.cg_it >= 2 ? 1 + (c.cg_it & 1) : 0;
+    const int par = c.cg_par && c.cg_it >= 2 ? 1 + ((c.cg_it + (c.cg_par == 2)) & 1) : 0;
 #define MCX_PDB_PAR(SKIPV, GRID, LIST, CNT)                                                                          \
   MCX_NT_DIX(c.cg_nt, dix, {                                                                                         \
     if (par == 1)                                                                                                    \
@@ -5256,6 +5260,21 @@ static bool fused(const Ctx& c) { return c.fuse && c.nranks == 1 && !c.comm; }
 bool cg_pdb(const Ctx& c) {
   const int nbu = (int)((c.g.nown + UTPB - 1) / UTPB);
   return c.cg_pdb && c.p_pad2 && c.xdone && !fusep(c) && !(fused(c) && nbu <= 1024);
+}
+
+// algorithmic bytes per owned node of one CG iteration's vector kernels (the last solve's forms):
+// k_cg_update r, w in (+ D^-1 as a vector, + z out) or the Jacobi index byte (DIX), r out; the p
+// update p(i-1), z or r (+ the index byte) in, p(i) out, and x's read + write plus the owed p
+// terms amortised over the iterations that apply them (every 4th: PQB, every 2nd: PDB)
+int64_t cg_vec_bytes_per_node(const Ctx& c) {
+  const bool dix = cg_dix(c);
+  const int64_t upd = dix ? 73 : 120;
+  int64_t pup;
+  if (c.fusep_used) pup = 48;  // p inside the SpMV (counted there); x every second iteration in the update
+  else if (c.pqb_used) pup = (dix ? 73 : 72) + (48 + 3 * 24) / 4;
+  else if (c.pdb_used) pup = (dix ? 73 : 72) + (48 + 24) / 2;
+  else pup = dix ? 121 : 120;
+  return upd + pup;
 }
 
 int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) {

@@ -111,12 +111,22 @@ struct LocalGroup {
   std::vector<hipEvent_t> ev_packed, ev_halo_done, ev_red, ev_sum;
   double** d_red_ptrs = nullptr;   // device array: red_loc of every member
   int device = 0;
-  // host barrier
+  bool dev_ready = false;          // events + d_red_ptrs created (by the first mcx_init_local)
+  // host barrier: every crossing is tagged with the collective it belongs to, so members that
+  // reach different collectives (one rank finalizing while another exchanges a halo) fail
+  // instead of pairing up; a member that never arrives fails the others after timeout_s
   void* mtx = nullptr;
   void* cv = nullptr;
   int count = 0, generation = 0;
+  int cur_tag = 0, cur_rank = -1;  // the first arrival of the open generation
+  double timeout_s = 300.;         // MCX_COMM_TIMEOUT (seconds) at creation
+  bool broken = false;             // a mismatch or a timeout happened: every later crossing fails
+  std::string why;                 // ... and what it was
 };
-void group_barrier(LocalGroup* g);
+// barrier tags (which collective a crossing belongs to)
+enum { BAR_INIT = 1, BAR_HALO_PACKED, BAR_HALO_DONE, BAR_RED_IN, BAR_RED_SUM, BAR_FINALIZE, BAR_USER };
+int group_barrier(LocalGroup* g, int rank, int tag);  // 0, or 23 with the reason in mcx_last_error
+double comm_timeout_default();                       // MCX_COMM_TIMEOUT, default 300 s
 
 struct Ctx {
   mcx_opts o;
@@ -133,6 +143,9 @@ struct Ctx {
   int overlap = 1;                              // CG: interior p update overlaps the halo (option halo_overlap)
   void* comm = nullptr;                         // ncclComm_t when nranks > 1 (RCCL transport)
   LocalGroup* lg = nullptr;                     // in-process transport
+  double comm_timeout = 300.;                   // seconds a host wait on collective work may take (option comm_timeout)
+  bool comm_broken = false;                     // the communicator was aborted (timeout / async error): collectives fail
+  std::string comm_why;
   HaloPlan halo;
 
   // device arrays
@@ -230,7 +243,7 @@ struct Ctx {
   int vi_lg = 2;             // staged block-indexed SpMV, LDS-dictionary waves: blocks whose reads are issued together (option vi_lg: 1, 2, 3)
   int cg_p2d = 0;            // quad-buffered p update on a (rows, x chunks) grid: no per-node divisions (option cg_p2d; A/B)
   int vi_lg_exc = 1;         // vi_lg 2 also in the exception-node kernel (option vi_lg_exc; 0: per-block waits)
-  int vi_wdesc = 0;          // staged block-indexed SpMV: wave descriptors (option vi_wdesc): 1 = uniform waves, 2 = also two-set waves (FMA rows), 0 = off (A/B)
+  int vi_wdesc = 1;          // staged block-indexed SpMV: wave descriptors (option vi_wdesc): 1 = uniform waves (default since round 5: -2.1 % per CG iteration), 2 = also two-set waves (FMA rows), 0 = per-lane index words
   unsigned* wd = nullptr;    // wave descriptors [plane][npy][npx][8] + 2 counters (build_wdesc)
   int64_t wd_bytes = 0;
   bool wd_ok = false;        // descriptors built for the current block indices
@@ -320,6 +333,12 @@ int halo_finish(Ctx& c, double* xpad);     // compute stream waits, unpacks
 int allreduce_sum(Ctx& c, const double* in, double* out, int count);
 int allreduce_max(Ctx& c, const double* in, double* out, int count);
 int allreduce_prepare(Ctx& c);
+// host wait for work that depends on other ranks (CG chunk polls, all-reduced norms): the RCCL
+// transport polls the event and the communicator's asynchronous error against c.comm_timeout and
+// aborts the communicator on either; one rank without a communicator waits plainly
+int comm_wait(Ctx& c, hipEvent_t ev, const char* what);
+int comm_check(Ctx& c);  // a communicator aborted earlier: fail the collective
+int group_setup(Ctx& c);  // the in-process group's events (first member on the device)
 void launch_group_sum(Ctx& c, const double* const* ptrs, int nranks, int count, double* out, int op = 0);
 void launch_vtu_cells(Ctx& c, const int* lo, const int* cnt, double* out);
 void launch_force_layer(Ctx& c, int comp, int fa, int fixed, int a0, int na, int b0, int nb, double* out);
@@ -358,11 +377,31 @@ int build_wdesc(Ctx& c);    // wave descriptors of the block-indexed storage (af
 bool wd_used(const Ctx& c);  // the staged SpMV reads them
 bool fusep(const Ctx& c);  // the CG's p update runs inside the value-indexed SpMV
 bool cg_pdb(const Ctx& c);  // the CG's p update double-buffered (x every second iteration)
+int64_t cg_vec_bytes_per_node(const Ctx& c);  // the last solve's CG vector kernels, bytes per owned node and iteration
 // z-marching SpMV tile of the current storage (tx, ty, planes per chunk); all 0 for gathered kernels
 void spmv_tile(const Ctx& c, int* tx, int* ty, int* kc);
 int dirichlet_mask_host(const Geo& g, int gi, int gj, int gk);
 
 }  // namespace mcx
+
+// Every extern "C" entry is a function-try-block: no C++ exception (std::bad_alloc from a host
+// vector, std::system_error from the group barrier's mutex, ...) crosses the C ABI.  The handler
+// stores the message for mcx_last_error and returns MCX_EXC (the PetscErrorCode contract of the
+// functions the entries replace).  MCX_ENTRY is the test hook: MCX_TEST_THROW=<entry name> in the
+// environment makes that entry throw std::bad_alloc at its start (tests/test_abi.py).
+namespace mcx {
+constexpr int MCX_EXC = 90;
+int exc_return(const char* fn, const char* what);
+void test_inject(const char* fn);
+}  // namespace mcx
+#define MCX_ENTRY() mcx::test_inject(__func__)
+#define MCX_CATCH                                                                      \
+  catch (const std::exception& e_) {                                                   \
+    return mcx::exc_return(__func__, e_.what());                                       \
+  }                                                                                    \
+  catch (...) {                                                                        \
+    return mcx::exc_return(__func__, "unknown exception");                             \
+  }
 
 #define MCX_HIP(call)                                                                  \
   do {                                                                                 \

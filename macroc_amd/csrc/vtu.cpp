@@ -182,7 +182,8 @@ int write_vtu(Ctx& c, const char* prefix) {
 
 }  // namespace mcx
 
-extern "C" int mcx_write_vtu(void* ctx, const char* file_prefix) {
+extern "C" int mcx_write_vtu(void* ctx, const char* file_prefix) try {
+  MCX_ENTRY();
   using namespace mcx;
   if (!ctx || !file_prefix) {
     set_error("mcx_write_vtu: null argument");
@@ -191,4 +192,4 @@ extern "C" int mcx_write_vtu(void* ctx, const char* file_prefix) {
   Ctx& c = *reinterpret_cast<Ctx*>(ctx);
   MCX_HIP(hipSetDevice(c.device));
   return write_vtu(c, file_prefix);
-}
+} MCX_CATCH

@@ -88,3 +88,51 @@ def test_init_without_gpu_fails_loudly():
         pytest.skip("a GPU is visible")
     with pytest.raises(M.MacrocError, match="device"):
         M.Macroc(["-da_grid_x", "4", "-da_grid_y", "4", "-da_grid_z", "2"])
+
+
+def test_no_exception_crosses_the_abi(monkeypatch):
+    """every extern "C" entry is a function-try-block.  MCX_TEST_THROW=<entry>
+    makes that entry throw std::bad_alloc at its start (the failure of an absurd host allocation);
+    the caller gets code 90 and the message instead of std::terminate killing the process."""
+    L = M.lib()
+    o = M.parse_args(["-da_grid_x", 8, "-da_grid_y", 8, "-da_grid_z", 8])
+    inf = M.Info()
+    for fn, call in (("mcx_plan", lambda: L.mcx_plan(M.C.byref(o), 0, 1, M.C.byref(inf))),
+                     ("mcx_parse_args", lambda: L.mcx_parse_args(M.C.byref(o), 0, None)),
+                     ("mcx_init", lambda: L.mcx_init(M.C.byref(o), 0, 1, None, M.C.byref(M.C.c_void_p()))),
+                     ("mcx_local_group_create", lambda: L.mcx_local_group_create(2, 0, M.C.byref(M.C.c_void_p())))):
+        monkeypatch.setenv("MCX_TEST_THROW", fn)
+        assert call() == 90, fn
+        msg = L.mcx_last_error().decode()
+        assert fn in msg and "bad_alloc" in msg, msg
+        monkeypatch.delenv("MCX_TEST_THROW")
+    assert L.mcx_plan(M.C.byref(o), 0, 1, M.C.byref(inf)) == 0 and inf.nx == 8
+
+
+def test_local_group_withheld_member_fails_within_deadline(monkeypatch):
+    """VERDICT r04 item 5 (in-process transport): a member that never reaches the collective makes
+    the others' crossing fail after MCX_COMM_TIMEOUT seconds instead of hanging; the broken group
+    fails every later crossing at once.  The same barrier guards every collective entry point
+    (halo exchange, all-reduce, init, finalize)."""
+    import threading
+    import time
+    monkeypatch.setenv("MCX_COMM_TIMEOUT", "1")
+    g = M.LocalGroup(2)
+    try:
+        ok = []
+        ts = [threading.Thread(target=lambda r=r: (g.barrier(r), ok.append(r))) for r in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(10)
+        assert sorted(ok) == [0, 1]  # both members: the crossing completes
+        t0 = time.time()
+        with pytest.raises(M.MacrocError, match=r"rank 0 waited 1 s in mcx_local_group_barrier: 1 of 2"):
+            g.barrier(0)  # rank 1 withheld
+        assert time.time() - t0 < 5
+        t0 = time.time()
+        with pytest.raises(M.MacrocError, match="in-process group"):
+            g.barrier(1)
+        assert time.time() - t0 < 0.5
+    finally:
+        g.destroy()

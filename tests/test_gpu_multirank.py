@@ -392,3 +392,50 @@ def test_back_to_back_halos():
         for y, yr in zip(o["y"], ys):
             assert np.array_equal(y, yr[o["nat"]])
     assert np.array_equal(b, ref.b())
+
+
+def test_group_member_withheld_or_mismatched_fails(monkeypatch):
+    """VERDICT r04 items 1 and 5 on the device path: (a) a group whose second member never
+    initialises fails rank 0's mcx_init_local after MCX_COMM_TIMEOUT instead of hanging; (b) a
+    member that finalizes while the other exchanges a halo makes both calls fail with the two
+    collectives named, and neither reads the other's freed buffers (the process survives and a
+    fresh group works afterwards)."""
+    import time
+    monkeypatch.setenv("MCX_COMM_TIMEOUT", "2")
+    argv = ["-da_grid_x", 12, "-da_grid_y", 10, "-da_grid_z", 8, "-da_processors_x", 2]
+    g = M.LocalGroup(2)
+    t0 = time.time()
+    with pytest.raises(M.MacrocError, match="waited 2 s in mcx_init_local"):
+        M.Macroc(argv, rank=0, nranks=2, group=g)
+    assert time.time() - t0 < 30
+    g.destroy()
+
+    g = M.LocalGroup(2)
+    errs = [None, None]
+
+    def worker(r):
+        try:
+            m = M.Macroc(argv, rank=r, nranks=2, group=g)
+            try:
+                if r == 0:
+                    m.apply_bc_on_u(m.get_displacement(1))
+                    m.set_strains()  # halo exchange of u: rank 1 is finalizing instead
+            finally:
+                m.finish()
+        except M.MacrocError as e:
+            errs[r] = str(e)
+
+    ts = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(60)
+    assert not any(t.is_alive() for t in ts)
+    g.destroy()
+    assert errs[0] and errs[1], errs
+    assert all("mismatched collectives" in e or "in-process group" in e for e in errs), errs
+    assert any("mcx_finalize" in e and "halo exchange" in e for e in errs), errs
+    monkeypatch.delenv("MCX_COMM_TIMEOUT")
+    out = run_group(argv, 2, lambda m: (m.apply_bc_on_u(m.get_displacement(1)), m.set_strains(), m.homogenize(),
+                                        m.assembly_res())[-1])  # the library still works
+    assert out[0] == out[1] > 0

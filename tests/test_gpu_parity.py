@@ -693,6 +693,7 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
             m.set_option("spmv_zblocks", zblocks)
             # -mat_vi_fma 0: the reference's MatMult order (inode column pairs), bit-exact (scalar-dictionary 16x4 patches, row
             # quarters, every block from LDS); the default fused multiply-adds: within rounding
+            m.set_option("vi_wdesc", 0)  # per-lane index words (the descriptors are the default, below)
             for uni, patch in ((1, 1), (1, 0), (0, 0)):
                 m.set_option("vi_fma", 0)
                 m.set_option("vi_uni", uni)
@@ -752,12 +753,14 @@ def test_round4_options_refused():
 @pytest.mark.parametrize("maxits", [None, 37, 38, 39, 40, 1, 2, 3, 4, 5])
 @pytest.mark.parametrize("storage", ["vi", "vi_staged", "split"])
 def test_cg_pdb_bitwise(maxits, storage):
-    """Option cg_pdb 1 (default): p double-buffered and VecAXPY(x) applied on odd iterations only,
-    both owed terms in PETSc's order, the rest by k_cg_xfinal; cg_pdb 4: four buffers, the four
-    owed terms every fourth iteration (cg_xs 1: eight buffers, the four terms by k_cg_xwin on a side
-    stream beside the next iterations) — bitwise the solve of the single-buffer p update:
-    converged, and stopped by maxits at every residue mod 4 (1 to 5 included); with and without
-    the parity-specialised kernels (cg_par) and the reversed node order (cg_rev)."""
+    """Option cg_pdb 1: p double-buffered and VecAXPY(x) applied on odd iterations only, both
+    owed terms in PETSc's order, the rest by k_cg_xfinal; cg_pdb 4 (the default): four buffers,
+    the four owed terms every fourth iteration (cg_xs 1: eight buffers, the four terms by k_cg_xwin
+    on a side stream beside the next iterations) — bitwise the solve of the single-buffer p
+    update: converged, and stopped by maxits at every residue mod 4 (1 to 5 included); with and
+    without the parity-specialised kernels (cg_par 1), with a deliberately wrong parity hint
+    (cg_par 2: the kernels follow the device's count) and the reversed node order
+    (cg_rev)."""
     NX, NY, NZ = 70, 20, 12
     extra = ["-mat_aij_vi", 0] if storage == "split" else []
     argv = argv_for(NX, NY, NZ, 1e-12, extra) + (["-ksp_max_it", maxits] if maxits else [])
@@ -770,7 +773,8 @@ def test_cg_pdb_bitwise(maxits, storage):
         m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
         for pdb, par, rev, xs, p2d in ((0, 0, 0, 0, 0), (1, 0, 0, 0, 0), (0, 1, 0, 0, 0), (1, 1, 0, 0, 0), (1, 1, 1, 0, 0),
                                        (1, 0, 1, 0, 0), (4, 0, 0, 0, 0), (4, 1, 0, 0, 0), (4, 1, 1, 0, 0), (4, 1, 0, 1, 0),
-                                       (4, 0, 1, 1, 0), (4, 1, 0, 0, 1)):
+                                       (4, 0, 1, 1, 0), (4, 1, 0, 0, 1), (4, 2, 0, 0, 0), (4, 2, 1, 0, 0),
+                                       (1, 2, 0, 0, 0)):
             m.set_option("cg_pdb", pdb)
             m.set_option("cg_par", par)
             m.set_option("cg_rev", rev)
