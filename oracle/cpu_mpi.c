@@ -17,8 +17,8 @@
  *   MatZeroRowsColumns(diag 1) (apply_bc_on_jac, src/bcs.c:341-347),
  *   KSPSolve_CG + PCJacobi with KSP_NORM_PRECONDITIONED and KSPConvergedDefault: MatMult in the
  *   MATAIJ inode kernel's form (the three rows of a node share one column-index stream, each
- *   row adds its column pairs, diagonal block then off-diagonal block: oracle/oracle.c
- *   row_part), VecScatter of the ghost values by MPI_Isend/Irecv with the <= 26 neighbour
+ *   row adds its column pairs over the diagonal block, then the off-diagonal block term by term:
+ *   oracle/oracle.c orc_spmv_order), VecScatter of the ghost values by MPI_Isend/Irecv with the <= 26 neighbour
  *   ranks, MPI_Allreduce for every dot product and norm,
  *   VecAXPY(u, 1, du).
  * Assembly is owner-computes: the rank evaluates every element touching an owned node and adds
@@ -482,9 +482,10 @@ static void assembly_jac(Ctx* c) {
   }
 }
 
-/* MatMult_MPIAIJ with the SeqAIJ inode kernels (oracle/oracle.c row_part): the node's column
-   index stream is read once for its three rows; each row adds its terms in column pairs, the
-   diagonal block from 0, then the off-diagonal block from that sum */
+/* MatMult_MPIAIJ (oracle/oracle.c orc_spmv_order): the diagonal block with the SeqAIJ inode
+   kernel (the node's column index stream read once for its three rows; each row adds its terms
+   in column pairs from 0), then the off-diagonal block from that sum with MatMultAdd_SeqAIJ's
+   plain loop, term by term (MatAssemblyEnd_MPIAIJ turns inodes off for it) */
 static void matmult(Ctx* c, const double* x, double* y) {
   exchange(c, x, c->pg);
   for (int64_t n = 0; n < c->nown; n++) {
@@ -498,6 +499,14 @@ static void matmult(Ctx* c, const double* x, double* y) {
       const double* xx = part ? c->pg : x;
       double s1 = s[0], s2 = s[1], s3 = s[2];
       int q = 0;
+      if (part) {  // off-diagonal block: no inodes, one term at a time
+        for (; q < len; q++) {
+          const double t0 = xx[idx[q]];
+          s1 += v1[q] * t0;
+          s2 += v2[q] * t0;
+          s3 += v3[q] * t0;
+        }
+      }
       for (; q < len - 1; q += 2) {
         const double t0 = xx[idx[q]], t1 = xx[idx[q + 1]];
         s1 += v1[q] * t0 + v1[q + 1] * t1;

@@ -1017,16 +1017,19 @@ static double row_part(const orc_problem* P, int64_t row, int64_t lo, int64_t hi
 }
 
 /* MatMult (KSPSolve's, src/assembly.c:185): one rank = the SeqAIJ kernel above over the row;
-   several ranks = MatMult_MPIAIJ, the diagonal (owned-column) block first, then MatMultAdd of
-   the off-diagonal block (its columns, the compressed ghosts, in ascending global order)
-   starting from that sum [ext]. */
+   several ranks = MatMult_MPIAIJ, the diagonal (owned-column) block A first, then MatMultAdd of
+   the off-diagonal block B (its columns, the compressed ghosts, in ascending global order)
+   starting from that sum [ext].  MatAssemblyEnd_MPIAIJ turns inodes off for B
+   (MatSetOption(aij->B, MAT_USE_INODES, PETSC_FALSE) before B's assembly [ext]), so B's part
+   always runs MatMultAdd_SeqAIJ's plain loop, sum += a * x term by term; A keeps
+   the order asked for. */
 void orc_spmv_order(const orc_problem* P, const double* x, double* y, int order) {
 #pragma omp parallel for schedule(static)
   for (int r = 0; r < P->nranks; r++) {
     int64_t c0 = 3 * P->node_off[r], c1 = 3 * P->node_off[r + 1];
     for (int64_t row = c0; row < c1; row++) {
       double sum = row_part(P, row, c0, c1, 1, 0., x, order);
-      if (P->nranks > 1) sum = row_part(P, row, c0, c1, 0, sum, x, order);
+      if (P->nranks > 1) sum = row_part(P, row, c0, c1, 0, sum, x, ORC_SPMV_SEQAIJ);
       y[row] = sum;
     }
   }

@@ -314,7 +314,8 @@ def _row_sums(indptr, t, sel, s0, inode):
 def spmv(indptr, indices, data, x, dof_off=None, inode=True):
     """MatMult of a CSR matrix in PETSc numbering, restated independently of oracle.c: one rank
     (dof_off None) = the SeqAIJ kernel over each row; several = MatMult_MPIAIJ, the owned-column
-    block then MatMultAdd of the off-diagonal block from that sum."""
+    block then MatMultAdd of the off-diagonal block from that sum — term by term whatever
+    `inode` says: MatAssemblyEnd_MPIAIJ sets MAT_USE_INODES false on the off-diagonal block."""
     t = data * x[indices]
     n = len(indptr) - 1
     if dof_off is None:
@@ -323,7 +324,7 @@ def spmv(indptr, indices, data, x, dof_off=None, inode=True):
     rk = np.searchsorted(dof_off, rows, side="right") - 1
     own = (indices >= dof_off[rk]) & (indices < dof_off[rk + 1])
     s = _row_sums(indptr, t, own, np.zeros(n), inode)
-    return _row_sums(indptr, t, ~own, s, inode)
+    return _row_sums(indptr, t, ~own, s, False)
 
 
 # ----------------------------------------------------------------- fixtures
