@@ -72,7 +72,7 @@ static int free_ctx(Ctx* c) {
   if (c->x_stream) (void)hipStreamSynchronize(c->x_stream);
   void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->wd, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
                   c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2, c->p_pad3, c->p_pad4, c->p_pad58[0], c->p_pad58[1], c->p_pad58[2], c->p_pad58[3], c->xdone, c->esc_node, c->esc_res, c->esc_slot, c->elem_plain, c->cref, c->vi_xslot,
-                  c->vi_xlist, c->vi_exc,
+                  c->vi_xlist, c->vi_xcnt, c->vi_exc,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf, c->halo.d_bnd};
   for (void* p : ptrs)
@@ -176,7 +176,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
       (c.o.mat_type == MCX_MAT_SBAIJ && (rc = dalloc(c, &c.U, c.npgroups * UPAIR * 128))) ||
       (c.o.mat_type == MCX_MAT_AIJ && !c.aij_split && (rc = dalloc(c, &c.V, c.ngroups * NPAIR * 128))) ||
       (rc = dalloc(c, &c.eps, 6 * 8 * E)) || (rc = dalloc(c, &c.sig, 6 * 8 * E)) ||
-      (rc = dalloc(c, &c.partials, c.partials_cap = 4 * std::max(max_spmv_blocks(c), node_blocks(c)) + 64)) ||
+      (rc = dalloc(c, &c.partials, c.partials_cap = 6 * std::max(max_spmv_blocks(c), node_blocks(c)) + 64)) ||
       (rc = dalloc(c, &c.red, 16)) || (rc = dalloc(c, &c.red_loc, 16)) || (rc = dalloc(c, &c.cg, 2)) ||
       (rc = dalloc(c, &c.hist, (int64_t)o->ksp_max_it + 2)) || (rc = dalloc(c, &c.ke_uni, 576)) ||
       (rc = dalloc(c, &c.p_pad2, npad)) || (rc = dalloc(c, &c.xdone, 1)))  // p's second buffer (cg_pdb, cg_fusep)
@@ -1243,8 +1243,8 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) try 
   std::vector<unsigned char> Ih;
   std::vector<double> dict;
   std::vector<double> Xh;  // exception nodes' blocks
-  if (vals && c.fmt == FMT_VI && c.vi_block && c.vi_nexc) {
-    Xh.resize((size_t)c.vi_nexc * 27 * 9);
+  if (vals && c.fmt == FMT_VI && c.vi_block && c.vi_nexc) {  // [243][xld], slot fastest
+    Xh.resize((size_t)c.g.xld * 27 * 9);
     MCX_HIP(hipMemcpyAsync(Xh.data(), c.vi_exc, Xh.size() * sizeof(double), hipMemcpyDeviceToHost, c.stream));
   }
   if (vals && c.fmt == FMT_VI) {
@@ -1343,7 +1343,7 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) try 
             if (c.vi_block) {  // byte nb of 2 chunks of 16 B: the block's dictionary entry
               uint32_t xs = 0;  // exception slot + 1 in bytes 28-31
               std::memcpy(&xs, &Ih[(((n >> 6) * 2 + 1) * 64 + (n & 63)) * 16 + 12], 4);
-              if (xs && !Xh.empty()) v = Xh[((size_t)(xs - 1) * 27 + nb) * 9 + r * 3 + cc];
+              if (xs && !Xh.empty()) v = Xh[(size_t)(nb * 9 + r * 3 + cc) * c.g.xld + (xs - 1)];
               else v = dict[Ih[(((n >> 6) * 2 + (nb >> 4)) * 64 + (n & 63)) * 16 + (nb & 15)] * VIB_STRIDE + r * 3 + cc];
             } else if (c.vi_bits == 8) {
               v = dict[Ih[(((n >> 6) * VI_CHUNKS + (s >> 4)) * 64 + (n & 63)) * 16 + (s & 15)]];
@@ -1604,6 +1604,10 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
   }
   if (!std::strcmp(name, "cg_p2d")) {
     c.cg_p2d = value != 0.;
+    return 0;
+  }
+  if (!std::strcmp(name, "vi_exc_kernel")) {
+    c.vi_exc_kernel = value != 0.;
     return 0;
   }
   if (!std::strcmp(name, "vi_lg_exc")) {

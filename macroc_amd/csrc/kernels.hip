@@ -1063,6 +1063,7 @@ struct ZTiling {
   int dbg = 0;            // timing-only diagnostics (k_spmv_vibm: 1 = every wave takes the scalar path)
   int wmap = 1;           // k_spmv_vibm PATCH: 1 = patches on SIMDs as a Latin square, 0 = row-major (A/B)
   int xlist = VI_EXC_LIST;  // k_spmv_vibm EXC: exception nodes a tile defers (option vi_exc_list; the rest in their plane)
+  int xskip = 0;          // k_spmv_vibm EXC: exception nodes are left to k_spmv_exc (option vi_exc_kernel)
   int ypair = 0;          // k_spmv_vibm UNI: y of lane pairs as 16-B stores (option vi_ypair; needs an even nx)
   const unsigned* wd = nullptr;  // k_spmv_vibm WD: the wave descriptors (build_wdesc), npx x npy 16 x 4 patches per plane
   int npx = 0, npy = 0;
@@ -2230,13 +2231,13 @@ __global__ __launch_bounds__(TPB) void k_elem_plain(Geo g, const double* __restr
   plain[le] = same ? 1 : 0;
 }
 
-// owned node n is an exception when one of its elements is not plain: slot = ctl[2]++,
-// xslot[n] = slot + 1, xlist[slot] = n (slots in arrival order; a row's values do not depend on it)
-__global__ __launch_bounds__(TPB) void k_node_exc(Geo g, const unsigned char* __restrict__ plain,
-                                                  unsigned* __restrict__ xslot, int* __restrict__ xlist,
-                                                  unsigned* __restrict__ ctl) {
-  const int n = blockIdx.x * TPB + threadIdx.x;
-  if (n >= g.nown) return;
+// Exception nodes (an owned node touching an element that is not plain) get their slots by an
+// ordered compaction: slot = the number of exception nodes before n in owned-node order (three
+// passes: per-block counts, one block's scan of the counts, per-node ranks).  Neighbouring
+// exception nodes then hold neighbouring slots, so a wave of consecutive slots reads the
+// slot-fastest exc array in whole lines, and the slots are deterministic (round 4 took them from
+// an atomic counter, in arrival order).
+__device__ __forceinline__ bool node_is_exc(const Geo& g, const unsigned char* __restrict__ plain, int n) {
   int i, j, k;
   node_ijk(g, n, i, j, k);
   const int gi = g.xs + i, gj = g.ys + j, gk = g.zs + k;
@@ -2249,17 +2250,67 @@ __global__ __launch_bounds__(TPB) void k_node_exc(Geo g, const unsigned char* __
         const int64_t le = (ex - g.ex0) + (int64_t)(ey - g.ey0) * g.nex + (int64_t)(ez - g.ez0) * g.nex * g.ney;
         exc = exc || !plain[le];
       }
-  unsigned v = 0u;
-  if (exc) {
-    const unsigned slot = atomicAdd(&ctl[2], 1u);
-    xlist[slot] = n;
-    v = slot + 1u;
-  }
-  xslot[n] = v;
+  return exc;
 }
 
-// the exception nodes' 27 blocks, [slot][nb][9]: thread = (slot, nb); each element block from
-// kref (plain elements) or from Ke (the others: k_element_ke forms only those)
+// pass 1: xslot[n] = 1 for an exception node (0 otherwise), cnt[block] = the block's count
+__global__ __launch_bounds__(TPB) void k_exc_flag(Geo g, const unsigned char* __restrict__ plain,
+                                                  unsigned* __restrict__ xslot, unsigned* __restrict__ cnt) {
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  const bool e = n < g.nown && node_is_exc(g, plain, n);
+  if (n < g.nown) xslot[n] = e ? 1u : 0u;
+  const int c = __syncthreads_count(e);
+  if (threadIdx.x == 0) cnt[blockIdx.x] = (unsigned)c;
+}
+
+// pass 2 (one block): cnt[0..nb) -> exclusive prefix sums, the total to ctl[2] (read back with the
+// block-build's sets)
+__global__ __launch_bounds__(1024) void k_exc_scan(unsigned* __restrict__ cnt, int nb, unsigned* __restrict__ ctl) {
+  __shared__ unsigned s[1024];
+  const int t = threadIdx.x, per = (nb + 1023) / 1024, lo = min(nb, t * per), hi = min(nb, lo + per);
+  unsigned sum = 0u;
+  for (int q = lo; q < hi; q++) sum += cnt[q];
+  s[t] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan of the 1024 chunk sums
+    const unsigned v = t >= o ? s[t - o] : 0u;
+    __syncthreads();
+    s[t] += v;
+    __syncthreads();
+  }
+  unsigned run = s[t] - sum;
+  for (int q = lo; q < hi; q++) {
+    const unsigned c = cnt[q];
+    cnt[q] = run;
+    run += c;
+  }
+  if (t == 1023) ctl[2] = s[1023];
+}
+
+// pass 3: slot = the block's offset + the node's rank among the block's exception nodes;
+// xslot[n] = slot + 1, xlist[slot] = n
+__global__ __launch_bounds__(TPB) void k_exc_assign(Geo g, unsigned* __restrict__ xslot, int* __restrict__ xlist,
+                                                    const unsigned* __restrict__ cnt) {
+  __shared__ unsigned wsum[TPB / 64];
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  const bool e = n < g.nown && xslot[n] != 0u;
+  const unsigned long long m = __ballot(e);
+  const unsigned lane_rank = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) wsum[w] = (unsigned)__popcll(m);
+  __syncthreads();
+  unsigned off = cnt[blockIdx.x];
+  for (int q = 0; q < w; q++) off += wsum[q];
+  if (n < g.nown) {
+    const unsigned slot = off + lane_rank;
+    xslot[n] = e ? slot + 1u : 0u;
+    if (e) xlist[slot] = n;
+  }
+}
+
+// the exception nodes' 27 blocks, value (nb, q) of slot s at exc[(nb * 9 + q) * g.xld + s] (slot
+// fastest): thread = (slot, nb); each element block from kref (plain elements) or from Ke (the
+// others: k_element_ke forms only those)
 __global__ __launch_bounds__(TPB) void k_exc_fill(Geo g, Material mat, const double* __restrict__ Ke,
                                                   const double* __restrict__ kref,
                                                   const unsigned char* __restrict__ plain,
@@ -2275,7 +2326,7 @@ __global__ __launch_bounds__(TPB) void k_exc_fill(Geo g, Material mat, const dou
   matrix_block<true>(g, mat, Ke, g.xs + i, g.ys + j, g.zs + k, nb % 3 - 1, (nb / 3) % 3 - 1, nb / 9 - 1, val,
                      kref, plain);
 #pragma unroll
-  for (int q = 0; q < 9; q++) exc[(t * 27 + nb) * 9 + q] = val[q];
+  for (int q = 0; q < 9; q++) exc[(int64_t)(nb * 9 + q) * g.xld + t] = val[q];
 }
 
 __device__ __forceinline__ double jacobi_inv(double d) {
@@ -2294,9 +2345,9 @@ __global__ void k_jacobi_vib(Geo g, const unsigned char* __restrict__ I, const d
   const unsigned xs =
       exc ? *reinterpret_cast<const unsigned*>(I + (((int64_t)(n >> 6) * 2 + 1) * 64 + (n & 63)) * 16 + 12) : 0u;
   jix[n] = xs ? 255 : (unsigned char)id;  // 255: the CG kernels read dinv (jac_inv)
-  const double* d = xs ? exc + ((int64_t)(xs - 1) * 27 + 13) * 9 : bdict + id * VIB_STRIDE;
 #pragma unroll
-  for (int r = 0; r < 3; r++) dinv[3 * n + r] = jacobi_inv(d[r * 4]);
+  for (int r = 0; r < 3; r++)
+    dinv[3 * n + r] = jacobi_inv(xs ? exc[(int64_t)(13 * 9 + r * 4) * g.xld + (xs - 1)] : bdict[id * VIB_STRIDE + r * 4]);
 }
 
 // the dictionary's inverse diagonals [VI_MAX][3] (same values as k_jacobi_vib's dinv)
@@ -2346,9 +2397,8 @@ __global__ __launch_bounds__(TPB) void k_spmv_vib(Geo g, const u32x4* __restrict
       const unsigned id = (word >> (8 * (nb & 3))) & 255u;
       double a[9];
       if (EXC && w1[3]) {
-        const double* e = exc + ((int64_t)(w1[3] - 1) * 27 + nb) * 9;
 #pragma unroll
-        for (int q = 0; q < 9; q++) a[q] = e[q];
+        for (int q = 0; q < 9; q++) a[q] = exc[(int64_t)(nb * 9 + q) * g.xld + (w1[3] - 1)];
       } else {
         const double2* e = tab + id * (VIB_STRIDE / 2);
         const double2 a01 = e[0], a23 = e[1], a45 = e[2], a67 = e[3], a8 = e[4];
@@ -2651,7 +2701,8 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
     bool deferred = false;
     if constexpr (EXC) {
       const bool xh = !(UNI && uni) && inxy && full && c1[3] != 0u;
-      const unsigned long long xm = __ballot(xh);
+      const unsigned long long xm = zt.xskip ? 0ull : __ballot(xh);
+      deferred = zt.xskip && xh;  // (xskip: k_spmv_exc computes the row)
       if (xm) {  // uniform
         const int pos = wn + (int)__builtin_amdgcn_mbcnt_hi((unsigned)(xm >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((unsigned)xm, 0u));
@@ -2767,12 +2818,12 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       // round trip per group instead of per block.
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
       InodeRows<true> acc;  // !FMA: all 27 neighbours present (full)
-      const double* eb = exc + (int64_t)(c1[3] - 1) * 243;
+      const double* eb = exc + (c1[3] - 1);  // value v at eb[v * g.xld]
 #pragma unroll 1
       for (int nb0 = 0; nb0 < 27; nb0 += 3) {
         double av[27];
 #pragma unroll
-        for (int q = 0; q < 27; q++) av[q] = eb[nb0 * 9 + q];
+        for (int q = 0; q < 27; q++) av[q] = eb[(int64_t)(nb0 * 9 + q) * g.xld];
         const int dy = (nb0 / 3) % 3 - 1, dz = nb0 / 9 - 1;
         const int xo = ((k + dz - k0 + 1) % R) * PLANE + (ly + 1 + dy) * RL + 3 * lx;
 #pragma unroll
@@ -2882,7 +2933,7 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       __syncthreads();
     }
   }
-  if constexpr (EXC) {
+  if (EXC && !zt.xskip) {
     // the exception pass: one listed node per thread, x gathered from the padded vector (the
     // values the ring held), rows in the indexed path's order and products: y bit-identical.
     // Only the block's dot partial adds these nodes' terms in another order.
@@ -2901,14 +2952,14 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       const int ei = i0 + ex, ej = j0 + ey;
       const int64_t n = ei + g.nx * (ej + (int64_t)g.ny * kk);
       const unsigned slot = I[(int64_t)(n >> 6) * (2 * 64) + (n & 63) + 64][3];
-      const double* eb = exc + (int64_t)(slot - 1) * 243;
+      const double* eb = exc + (slot - 1);  // value v at eb[v * g.xld]
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
       InodeRows<true> acc;  // !FMA: listed nodes are full (boundary nodes go to k_spmv_vib_faces)
 #pragma unroll 1
       for (int nb0 = 0; nb0 < 27; nb0 += 3) {
         double av[27];
 #pragma unroll
-        for (int q = 0; q < 27; q++) av[q] = eb[nb0 * 9 + q];
+        for (int q = 0; q < 27; q++) av[q] = eb[(int64_t)(nb0 * 9 + q) * g.xld];
         const int dy = (nb0 / 3) % 3 - 1, dz = nb0 / 9 - 1;
         const double* xr = x + 3 * ((int64_t)ei + (ej + 1 + dy) * (int64_t)PX + (kk + 1 + dz) * (int64_t)PXY);
         double xw[9];
@@ -3035,19 +3086,89 @@ __global__ __launch_bounds__(TPB) void k_spmv_vib_faces(Geo g, const u32x4* __re
         xc2 = xv[2];
       }
       const double* e;
+      int64_t es = 1;  // stride of the block's values: the dictionary's 1, the exception array's xld
       if (EXC && slot) {
-        e = exc + ((int64_t)(slot - 1) * 27 + nb) * 9;
+        e = exc + (int64_t)(nb * 9) * g.xld + (slot - 1);
+        es = g.xld;
       } else {
         const unsigned word = nb < 16 ? w0[nb >> 2] : w1[(nb - 16) >> 2];
         e = bdict + ((word >> (8 * (nb & 3))) & 255u) * VIB_STRIDE;
       }
 #pragma unroll
-      for (int q = 0; q < 9; q++) acc.term(nb, q / 3, q % 3, e[q] * xv[q % 3]);
+      for (int q = 0; q < 9; q++) acc.term(nb, q / 3, q % 3, e[q * es] * xv[q % 3]);
     }
     const double y0 = acc.row(0), y1 = acc.row(1), y2 = acc.row(2);
     y[3 * n + 0] = y0;
     y[3 * n + 1] = y1;
     y[3 * n + 2] = y2;
+    if (DOT) dot = xc0 * y0 + xc1 * y1 + xc2 * y2;
+  }
+  if (DOT) {
+    const double sm = block_sum<TPB>(dot, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = sm;
+  }
+}
+
+// The exception rows of the block-indexed storage: after the z-march (which
+// leaves them out, vi_exc_kernel), one thread per exception slot over the whole device instead of a
+// block-wide pass in the tail of the tile that owns them.  Slots are in owned-node order (ordered
+// compaction) and exc is slot fastest, so the 243 value loads of a wave are whole lines; x is
+// gathered from the padded vector.  Each row adds its 27 blocks' terms in the order and with the
+// products of the z-march's rows (FMA: one fused multiply-add per term in (nb, c) order; exact:
+// the inode pairs of a node with all 27 neighbours — exact rows of boundary nodes are the faces
+// kernel's), so y is bitwise what the in-tile pass computed.  The block's p.w partial goes after
+// the z-march's and the faces kernel's partials.
+template <bool DOT, bool GATED, bool FMA>
+__global__ __launch_bounds__(TPB) void k_spmv_exc(Geo g, const int* __restrict__ xlist, int64_t nexc,
+                                                  const double* __restrict__ exc, const double* __restrict__ x,
+                                                  double* __restrict__ y, double* __restrict__ part,
+                                                  const CgState* __restrict__ cg) {
+  __shared__ double sh[TPB / 64];
+  if (GATED && cg->reason) return;
+  const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  double dot = 0.;
+  int n = -1, i = 0, j = 0, k = 0;
+  if (t < nexc) {
+    n = xlist[t];
+    node_ijk(g, n, i, j, k);
+    if (!FMA && present_mask(g, i, j, k) != PRES_ALL) n = -1;  // k_spmv_vib_faces' row
+  }
+  if (n >= 0) {
+    const int PX = g.PX, PXY = g.PX * g.PY;
+    const double* eb = exc + t;  // value v at eb[v * g.xld]
+    double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+    InodeRows<true> acc;
+#pragma unroll 1
+    for (int nb0 = 0; nb0 < 27; nb0 += 3) {  // one dy row of the stencil: 27 values, 9 x
+      double av[27];
+#pragma unroll
+      for (int q = 0; q < 27; q++) av[q] = eb[(int64_t)(nb0 * 9 + q) * g.xld];
+      const int dy = (nb0 / 3) % 3 - 1, dz = nb0 / 9 - 1;
+      const double* xr = x + 3 * ((int64_t)i + (j + 1 + dy) * (int64_t)PX + (k + 1 + dz) * (int64_t)PXY);
+      double xw[9];
+#pragma unroll
+      for (int q = 0; q < 9; q++) xw[q] = xr[q];  // nodes i-1, i, i+1 of the row (padded i = node i + 1)
+#pragma unroll
+      for (int t3 = 0; t3 < 3; t3++) {
+        const double xv[3] = {xw[3 * t3], xw[3 * t3 + 1], xw[3 * t3 + 2]};
+        if (nb0 + t3 == 13) {
+          xc0 = xv[0];
+          xc1 = xv[1];
+          xc2 = xv[2];
+        }
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+          const int r = q / 3, cc = q % 3;
+          double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
+          if constexpr (FMA) yr = __builtin_fma(av[t3 * 9 + q], xv[cc], yr);
+          else acc.term(nb0 + t3, r, cc, av[t3 * 9 + q] * xv[cc]);
+        }
+      }
+    }
+    if constexpr (!FMA) y0 = acc.row(0), y1 = acc.row(1), y2 = acc.row(2);
+    __builtin_nontemporal_store(y0, &y[3 * (int64_t)n + 0]);
+    __builtin_nontemporal_store(y1, &y[3 * (int64_t)n + 1]);
+    __builtin_nontemporal_store(y2, &y[3 * (int64_t)n + 2]);
     if (DOT) dot = xc0 * y0 + xc1 * y1 + xc2 * y2;
   }
   if (DOT) {
@@ -4152,9 +4273,15 @@ static int64_t faces_blocks(const Ctx& c) {
   return (face_enum(c.g).n + TPB - 1) / TPB;
 }
 
+// the exception rows' kernel (staged block-indexed storage with exception nodes, vi_exc_kernel)
+static int64_t exc_blocks(const Ctx& c) {
+  if (!(c.fmt == FMT_VI && c.vi_block && c.vi_nexc && vi_staged(c) && c.vi_exc_kernel)) return 0;
+  return (c.vi_nexc + TPB - 1) / TPB;
+}
+
 int64_t spmv_nparts(const Ctx& c) {
   if (c.fmt == FMT_SPLIT && c.dsl.dense) return node_blocks(c);
-  return spmv_grid_blocks(c) + faces_blocks(c);
+  return spmv_grid_blocks(c) + faces_blocks(c) + exc_blocks(c);
 }
 
 int upload_constants(Ctx& c) {
@@ -4209,7 +4336,8 @@ int launch_plain_ke(Ctx& c) {
     MCX_HIP(hipMalloc(&c.cref, (36 + 36 * 8 + 576) * sizeof(double)));  // cref, cref8, kref
     MCX_HIP(hipMalloc(&c.vi_xslot, c.g.nown * sizeof(unsigned)));
     MCX_HIP(hipMalloc(&c.vi_xlist, c.g.nown * sizeof(int)));
-    c.device_bytes += c.g.nelem + (36 + 288 + 576) * 8 + c.g.nown * 8;
+    MCX_HIP(hipMalloc(&c.vi_xcnt, (node_blocks(c) + 1) * sizeof(unsigned)));
+    c.device_bytes += c.g.nelem + (36 + 288 + 576) * 8 + c.g.nown * 8 + (node_blocks(c) + 1) * 4;
   }
   double* kref = c.cref + 36 + 288;
   hipLaunchKernelGGL(k_cref, dim3(1), dim3(64), 0, c.stream, c.mat, c.ctan, (int64_t)8 * c.g.nelem, c.cref);
@@ -4395,9 +4523,11 @@ static int build_vib(Ctx& c, bool* ok) {
   // exceptions; every other node's blocks are sums of kref blocks
   const bool exc = table_law(c) && c.plain_ke;
   c.vi_nexc = 0;
-  if (exc) {
-    hipLaunchKernelGGL(k_node_exc, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.elem_plain, c.vi_xslot,
-                       c.vi_xlist, c.vib_ctl);
+  if (exc) {  // ordered compaction: slots in owned-node order
+    const unsigned nbn = nblk(c.g.nown);
+    hipLaunchKernelGGL(k_exc_flag, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.elem_plain, c.vi_xslot, c.vi_xcnt);
+    hipLaunchKernelGGL(k_exc_scan, dim3(1), dim3(1024), 0, c.stream, c.vi_xcnt, (int)nbn, c.vib_ctl);
+    hipLaunchKernelGGL(k_exc_assign, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.vi_xslot, c.vi_xlist, c.vi_xcnt);
   }
   const unsigned* xslot = exc ? c.vi_xslot : nullptr;
   const double* kref = exc ? c.cref + 36 + 288 : nullptr;
@@ -4419,14 +4549,16 @@ static int build_vib(Ctx& c, bool* ok) {
   if (hctl[1] || hctl[0] > (unsigned)VI_MAX) return 0;
   const int64_t nexc = exc ? (int64_t)hctl[2] : 0;
   if (nexc * 1000 > (int64_t)c.vi_exc_max * c.g.nown) return 0;  // too many: AIJ-split
-  if (nexc * 27 * 9 * (int64_t)sizeof(double) > c.vi_exc_bytes) {
+  if (nexc > c.g.xld) {
     if (c.vi_exc) {
       MCX_HIP(hipFree(c.vi_exc));
       c.device_bytes -= c.vi_exc_bytes;
       c.vi_exc = nullptr;
     }
-    // grown with headroom: the plastic zone spreads over the time steps
-    c.vi_exc_bytes = std::min<int64_t>(2 * nexc + 1024, c.g.nown) * 27 * 9 * (int64_t)sizeof(double);
+    // [243][xld], slot fastest; grown with headroom (the plastic zone spreads over the time steps),
+    // the leading dimension a multiple of 64 slots (whole 512-B lines per wave)
+    c.g.xld = (std::min<int64_t>(2 * nexc + 1024, c.g.nown) + 63) / 64 * 64;
+    c.vi_exc_bytes = c.g.xld * 27 * 9 * (int64_t)sizeof(double);
     MCX_HIP(hipMalloc(&c.vi_exc, c.vi_exc_bytes));
     c.device_bytes += c.vi_exc_bytes;
   }
@@ -4829,6 +4961,7 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
       zt.dbg = c.split_dbg;
       zt.wmap = c.vi_wmap;
       zt.xlist = c.vi_exc_list;
+      zt.xskip = exc_blocks(c) > 0;
       zt.ypair = c.vi_ypair && (c.g.nx % 2) == 0;
       int tx, ty;
       vis_shape(c, tx, ty);
@@ -4939,6 +5072,23 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
         else
           hipLaunchKernelGGL((k_spmv_vib_faces<false, false, false>), dim3(nbf), dim3(TPB), 0, c.stream, c.g, I,
                              c.vi_bdict, xpad, y, pf, c.cg, fe, c.vi_exc);
+      }
+      const int64_t nbx = exc_blocks(c);
+      if (nbx) {  // the exception rows the z-march left out
+        double* px = c.partials + nb + nbf;
+#define MCX_EXCK(DV, GV, FV)                                                                                       \
+  hipLaunchKernelGGL((k_spmv_exc<DV, GV, FV>), dim3((unsigned)nbx), dim3(TPB), 0, c.stream, c.g, c.vi_xlist,        \
+                     c.vi_nexc, c.vi_exc, xpad, y, px, c.cg)
+        if (c.vi_fma) {
+          if (dot && gated) MCX_EXCK(true, true, true);
+          else if (dot) MCX_EXCK(true, false, true);
+          else MCX_EXCK(false, false, true);
+        } else {
+          if (dot && gated) MCX_EXCK(true, true, false);
+          else if (dot) MCX_EXCK(true, false, false);
+          else MCX_EXCK(false, false, false);
+        }
+#undef MCX_EXCK
       }
       return;
     }

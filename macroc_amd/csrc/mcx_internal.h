@@ -33,6 +33,7 @@ struct Geo {
   int ex0, ey0, ez0;       // first element evaluated on this device (global)
   int nex, ney, nez;       // extended element counts (owned + upper ghost layer)
   int64_t nelem;           // nex*ney*nez
+  int64_t xld;             // value-indexed exception blocks: leading dimension (slot capacity) of exc [243][xld]
   int bc_type;
   double lx, lz, dx, dz, rad, wg;
 };
@@ -222,7 +223,8 @@ struct Ctx {
   double* cref = nullptr;               // [36] the reference tangent (plastic: the elastic branch's C)
   unsigned* vi_xslot = nullptr;         // [nown] exception slot + 1, 0 = indexed node
   int* vi_xlist = nullptr;              // [nown] exception slot -> owned node
-  double* vi_exc = nullptr;             // [exceptions][27][9] block values
+  unsigned* vi_xcnt = nullptr;          // [node blocks + 1] exception nodes per block, then their exclusive scan
+  double* vi_exc = nullptr;             // [27 x 9][xld] block values, slot fastest (a wave's consecutive slots: coalesced)
   int64_t vi_exc_bytes = 0;             // allocated bytes of vi_exc
   int64_t vi_nexc = 0;                  // exception nodes of the current matrix
   bool plain_ke = false;                // this assembly formed kref + the non-plain elements' Ke only
@@ -243,6 +245,8 @@ struct Ctx {
   int vi_lg = 2;             // staged block-indexed SpMV, LDS-dictionary waves: blocks whose reads are issued together (option vi_lg: 1, 2, 3)
   int cg_p2d = 0;            // quad-buffered p update on a (rows, x chunks) grid: no per-node divisions (option cg_p2d; A/B)
   int vi_lg_exc = 1;         // vi_lg 2 also in the exception-node kernel (option vi_lg_exc; 0: per-block waits)
+  int vi_exc_kernel = 1;     // staged SpMV: exception rows in their own kernel after the march (k_spmv_exc, option
+                             // vi_exc_kernel; 0: round 4's block-wide pass in each tile's tail)
   int vi_wdesc = 1;          // staged block-indexed SpMV: wave descriptors (option vi_wdesc): 1 = uniform waves (default since round 5: -2.1 % per CG iteration), 2 = also two-set waves (FMA rows), 0 = per-lane index words
   unsigned* wd = nullptr;    // wave descriptors [plane][npy][npx][8] + 2 counters (build_wdesc)
   int64_t wd_bytes = 0;

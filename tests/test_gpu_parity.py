@@ -254,14 +254,20 @@ def test_aij_vi_exception_nodes(grid, stage, vi_tx, tile):
         assert np.array_equal(m.dump_csr()[2], v1)
         m.set_option("vi_fma", 0)
         assert np.array_equal(m.spmv(x), y1)
-        # staged tiles: exception nodes computed after the march by the whole block (default), in
-        # their plane (list size 0), or both (a list of 3 that overflows): the same rows
-        for xl in (0, 3, 2048):
+        # staged tiles: exception rows in their own kernel after the march (k_spmv_exc, default),
+        # or round 4's forms: after the march by the whole tile block, in their plane (list size
+        # 0), or both (a list of 3 that overflows): the same rows
+        for xk, xl in ((0, 0), (0, 3), (0, 2048), (1, 2048)):
+            m.set_option("vi_exc_kernel", xk)
             m.set_option("vi_exc_list", xl)
-            assert np.array_equal(m.spmv(x), y1), xl
+            assert np.array_equal(m.spmv(x), y1), (xk, xl)
         m.set_option("vi_fma", 1)
         y = m.spmv(x)
         assert np.all(np.abs(y - y1) <= 1e-14 * absrow + 1e-300)
+        for xk, xl in ((0, 0), (0, 3), (0, 2048), (1, 2048)):
+            m.set_option("vi_exc_kernel", xk)
+            m.set_option("vi_exc_list", xl)
+            assert np.array_equal(m.spmv(x), y), (xk, xl)
         m.set_option("vi_lg_exc", 0)  # per-block waits on the LDS path of the exception kernel: the same rows
         assert np.array_equal(m.spmv(x), y)
         m.set_option("vi_lg_exc", 1)
@@ -328,11 +334,13 @@ def _exc_waves_per_plane(P, NX, NY, NZ, TX=64, TY=16):
 
 
 def test_aij_vi_exception_pass_deterministic():
-    """The staged SpMV's block-wide exception pass is deterministic by construction: each wave
-    fills its own segment of the tile's list in (plane, lane) order (ballot), so the list, the
-    pass's thread -> node map and the block's p.w partial do not depend on wave scheduling.
-    Precondition asserted: some tile plane holds exception nodes in two or more waves.  Repeated
-    solves (default FMA rows, and -mat_vi_fma 0) are bitwise equal, with equal iteration counts."""
+    """The exception rows are deterministic by construction: slots come from an ordered
+    compaction (owned-node order, not an atomic counter), the exception kernel's thread -> slot map
+    and block partials are fixed (default), and round 4's block-wide pass (vi_exc_kernel 0) fills
+    one list segment per wave in (plane, lane) order (ballot).  Precondition asserted: some tile
+    plane holds exception nodes in two or more waves.  Repeated solves (default FMA rows, and
+    -mat_vi_fma 0; both exception forms) are bitwise equal, with equal iteration counts; the slot
+    order is the owned-node order (the matrix dump's exception blocks are read through it)."""
     NX, NY, NZ = 130, 9, 12
     rtol = 1e-10
     P, u = plastic_state(NX, NY, NZ, rtol=rtol)
@@ -346,15 +354,22 @@ def test_aij_vi_exception_pass_deterministic():
         m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
         info = m.get_info()
         assert info["storage"] == 3 and info["vi_exc_nodes"] > 0 and (info["spmv_tx"], info["spmv_ty"]) == (64, 16)
-        for fma in (1, 0):
-            m.set_option("vi_fma", fma)
-            runs = []
-            for _ in range(3):
-                its, rn, reason = m.solve_Ax()
-                runs.append((its, rn, m.du().copy()))
-            assert reason > 0
-            for its, rn, du in runs[1:]:
-                assert its == runs[0][0] and rn == runs[0][1] and np.array_equal(du, runs[0][2]), fma
+        assert np.array_equal(m.dump_csr()[2], P.A_values())
+        for xk in (1, 0):
+            m.set_option("vi_exc_kernel", xk)
+            for fma in (1, 0):
+                m.set_option("vi_fma", fma)
+                runs = []
+                for _ in range(3):
+                    its, rn, reason = m.solve_Ax()
+                    runs.append((its, rn, m.du().copy()))
+                assert reason > 0
+                for its, rn, du in runs[1:]:
+                    assert its == runs[0][0] and rn == runs[0][1] and np.array_equal(du, runs[0][2]), (xk, fma)
+        # assembled again: the same slots, the same solve
+        m.assembly_jac()
+        its, rn, reason = m.solve_Ax()
+        assert its == runs[0][0] and np.array_equal(m.du(), runs[0][2])
 
 
 @pytest.mark.parametrize("name", SINGLE)

@@ -28,7 +28,8 @@ ap.add_argument("--its", type=int, default=200, help="CG iterations timed per st
 ap.add_argument("--gamma", type=float, default=1e-2, help="shear strain of the plastic slab (yield ~1e-3)")
 a = ap.parse_args()
 G = a.grid
-ARGS = {"aij-vi": ["-dm_mat_type", "aij"], "aij-split": ["-dm_mat_type", "aij"], "sbaij": ["-dm_mat_type", "sbaij"]}
+ARGS = {"aij-vi": ["-dm_mat_type", "aij"], "aij-vi-pass": ["-dm_mat_type", "aij"], "aij-split": ["-dm_mat_type", "aij"],
+        "sbaij": ["-dm_mat_type", "sbaij"]}  # aij-vi-pass: round 4's in-tile exception pass (vi_exc_kernel 0)
 lx = 50.0
 dx = lx / (G - 1)
 i = np.arange(G)
@@ -49,8 +50,9 @@ for frac in [float(f) for f in a.fracs.split(",")]:
         m = M.Macroc(["-da_grid_x", G, "-da_grid_y", G, "-da_grid_z", G, "-mat_law", "plastic", "-ksp_rtol", "1e-300",
                       "-ksp_max_it", a.its] + ARGS[st])
         try:
-            if st == "aij-vi":
+            if st.startswith("aij-vi"):
                 m.set_option("vi_exc_max", 1000)
+                m.set_option("vi_exc_kernel", 0 if st == "aij-vi-pass" else 1)
             elif st == "aij-split":
                 m.set_option("vi_exc_max", 0)
             m.set_u(u)

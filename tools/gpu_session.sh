@@ -11,8 +11,8 @@
 #   bench-default  python bench.py
 #   rocprof        the headline under rocprofv3 --kernel-trace --stats (no variants / legs / CPU baseline)
 #   pmc            PMC HBM-traffic passes of the headline SpMV (tools/pmc_spmv.sh) + SQ passes (tools/pmc_vibm.sh)
-#   py:<script>    python tools/<script> (an A/B script; its arguments after a second colon, space separated
-#                  with commas: py:spmv_ab.py:--grid,256)
+#   py:<script>    python tools/<script> (an A/B script; its arguments after a second colon, separated
+#                  by @: py:spmv_ab.py:--grid@256)
 # Every step has its own timeout and its own log, named with the step and the box's clock, so a
 # failing attempt is never overwritten by a later one (gpurun merges gpurun_out/ back by name).
 # The session stops at the first failing step: nothing more runs on the GPU after a fault, an abort
@@ -39,7 +39,8 @@ run() {  # run NAME TIMEOUT OUTFILE CMD...  (stdout to OUTFILE, stderr to the .l
 }
 
 for step in "$@"; do
-  base="gpurun_out/${TAG}_${STAMP}_${step//[:,\/ ]/_}"
+  name=${step%%@*}
+  base="gpurun_out/${TAG}_${STAMP}_${name//[:,\/ ]/_}"
   case "$step" in
     suite)
       AMD_LOG_LEVEL=1 run suite 1100 "$base.log" python -u -m pytest tests -m gpu -x -v -s -p no:cacheprovider \
@@ -66,7 +67,7 @@ for step in "$@"; do
       script=${spec%%:*}
       args=""
       [ "$spec" != "$script" ] && args=${spec#*:}
-      run "$script" 900 "$base.log" python -u "tools/$script" ${args//,/ } ;;
+      run "$script" 900 "$base.log" python -u "tools/$script" ${args//@/ } ;;
     *)
       echo "unknown step $step" >&2
       exit 2 ;;
