@@ -30,6 +30,19 @@ void test_inject(const char* fn) {
   if (e && !std::strcmp(e, fn)) throw std::bad_alloc();
 }
 
+// padded node vectors (u, p and its buffers): the allocation is shifted by pad_off bytes so that
+// with a 16-node row pitch (pad_align) every interior row's first owned node starts a 128-B line
+// (DESIGN §3); the base pointers are kept for hipFree
+static int dalloc_pad(Ctx& c, double** p, int64_t n) {
+  char* base = nullptr;
+  MCX_HIP(hipMalloc((void**)&base, sizeof(double) * n + 256));
+  MCX_HIP(hipMemsetAsync(base, 0, sizeof(double) * n + 256, c.stream));
+  c.pad_bases.push_back(base);
+  c.device_bytes += (int64_t)sizeof(double) * n + 256;
+  *p = reinterpret_cast<double*>(base + c.pad_off);
+  return 0;
+}
+
 template <class T>
 static int dalloc(Ctx& c, T** p, int64_t n) {
   if (n <= 0) n = 1;
@@ -70,13 +83,14 @@ static int free_ctx(Ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
   if (c->x_stream) (void)hipStreamSynchronize(c->x_stream);
-  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->u_pad, c->p_pad, c->b, c->du, c->r, c->z, c->w, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->wd, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
-                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->p_pad2, c->p_pad3, c->p_pad4, c->p_pad58[0], c->p_pad58[1], c->p_pad58[2], c->p_pad58[3], c->xdone, c->esc_node, c->esc_res, c->esc_slot, c->elem_plain, c->cref, c->vi_xslot,
+  void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->b, c->du, c->r, c->z, c->w, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->wd, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
+                  c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->xdone, c->esc_node, c->esc_res, c->esc_slot, c->elem_plain, c->cref, c->vi_xslot,
                   c->vi_xlist, c->vi_xcnt, c->vi_exc,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf, c->halo.d_bnd};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
+  for (void* p : c->pad_bases) (void)hipFree(p);  // u and the p buffers (dalloc_pad)
   if (c->h_cg) (void)hipHostFree(c->h_cg);
   for (void* h : {(void*)c->h_vib_keys, (void*)c->h_vib_map, (void*)c->h_vib_dict})
     if (h) (void)hipHostFree(h);
@@ -124,6 +138,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   c.rank = rank;
   c.nranks = nranks;
   c.comm_timeout = comm_timeout_default();
+  if (const char* e = std::getenv("MCX_PAD_ALIGN")) c.pad_align = std::atoi(e);  // A/B of the padded layout
   int ndev = 0;
   MCX_HIP(hipGetDeviceCount(&ndev));
   if (ndev <= 0) {
@@ -169,7 +184,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   // AIJ-split corrections D are sized by build_split to the active slots
   // jdd [VI_MAX][3] and the Jacobi vector dinv behind it in one buffer: the block-indexed CG
   // kernels read an exception node's (jix 255) inverse diagonal at jdd + 3 VI_MAX + 3n
-  if ((rc = dalloc(c, &c.u_pad, npad)) || (rc = dalloc(c, &c.p_pad, npad)) || (rc = dalloc(c, &c.b, nown3)) ||
+  if ((rc = dalloc_pad(c, &c.u_pad, npad)) || (rc = dalloc_pad(c, &c.p_pad, npad)) || (rc = dalloc(c, &c.b, nown3)) ||
       (rc = dalloc(c, &c.du, nown3)) || (rc = dalloc(c, &c.r, nown3)) || (rc = dalloc(c, &c.z, nown3)) ||
       (rc = dalloc(c, &c.w, nown3)) || (rc = dalloc(c, &c.jdd, 3 * VI_MAX + nown3)) ||
       (rc = dalloc(c, &c.jix, (int64_t)g.nown)) || (rc = dalloc(c, &c.tmp, nown3)) ||
@@ -179,7 +194,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
       (rc = dalloc(c, &c.partials, c.partials_cap = 6 * std::max(max_spmv_blocks(c), node_blocks(c)) + 64)) ||
       (rc = dalloc(c, &c.red, 16)) || (rc = dalloc(c, &c.red_loc, 16)) || (rc = dalloc(c, &c.cg, 2)) ||
       (rc = dalloc(c, &c.hist, (int64_t)o->ksp_max_it + 2)) || (rc = dalloc(c, &c.ke_uni, 576)) ||
-      (rc = dalloc(c, &c.p_pad2, npad)) || (rc = dalloc(c, &c.xdone, 1)))  // p's second buffer (cg_pdb, cg_fusep)
+      (rc = dalloc_pad(c, &c.p_pad2, npad)) || (rc = dalloc(c, &c.xdone, 1)))  // p's second buffer (cg_pdb, cg_fusep)
     return rc;
   c.dinv = c.jdd + 3 * VI_MAX;
   // per-GP tangent: only laws that hand one over (the isotropic elastic C is a kernel argument)
@@ -231,13 +246,13 @@ static int cg_solve(Ctx& c, int* its, double* rnorm, int* reason) {
   if (c.pqb_used && !c.p_pad3) {  // the quad-buffered p update's third and fourth buffers
     const int64_t npad = (int64_t)c.g.PX * c.g.PY * c.g.PZ * 3;
     int rc = 0;
-    if ((rc = dalloc(c, &c.p_pad3, npad)) || (rc = dalloc(c, &c.p_pad4, npad))) return rc;
+    if ((rc = dalloc_pad(c, &c.p_pad3, npad)) || (rc = dalloc_pad(c, &c.p_pad4, npad))) return rc;
   }
   if (c.xs_used && !c.p_pad58[0]) {  // cg_xs: buffers 5-8, the side stream and its events
     const int64_t npad = (int64_t)c.g.PX * c.g.PY * c.g.PZ * 3;
     int rc = 0;
     for (int q = 0; q < 4; q++)
-      if ((rc = dalloc(c, &c.p_pad58[q], npad))) return rc;
+      if ((rc = dalloc_pad(c, &c.p_pad58[q], npad))) return rc;
     MCX_HIP(hipStreamCreateWithFlags(&c.x_stream, hipStreamNonBlocking));
     MCX_HIP(hipEventCreateWithFlags(&c.ev_xp, hipEventDisableTiming));
     MCX_HIP(hipEventCreateWithFlags(&c.ev_xd[0], hipEventDisableTiming));

@@ -111,7 +111,10 @@ int setup_decomposition(Ctx& c) {
   g.nx = (int)c.wx[c.pi];
   g.ny = (int)c.wy[c.pj];
   g.nz = (int)c.wz[c.pk];
-  g.PX = g.nx + 2;
+  // padded row pitch: nx + 2 nodes, rounded to 16 (384 B = 3 lines) with pad_align, so the rows
+  // of a padded vector keep one alignment
+  g.PX = c.pad_align ? (g.nx + 2 + 15) / 16 * 16 : g.nx + 2;
+  c.pad_off = c.pad_align == 1 ? 104 : 0;  // 104 + 24 = 128: node (0, j, k) starts a line
   g.PY = g.ny + 2;
   g.PZ = g.nz + 2;
   g.nown = g.nx * g.ny * g.nz;

@@ -151,6 +151,11 @@ struct Ctx {
 
   // device arrays
   double* u_pad = nullptr;   // displacement, padded ghosted box [PX*PY*PZ][3]
+  int pad_align = 1;         // padded box: 1 = row pitch PX a multiple of 16 nodes and node (0, j, k) of
+                             // every row at a 128-B line (pad_off 104), 2 = the same pitch with the
+                             // ghost column (-1, j, k) at a line (pad_off 0), 0 = PX = nx + 2 (round 4)
+  int pad_off = 104;         // bytes from an allocation's base to padded node 0
+  std::vector<void*> pad_bases;  // allocations of the padded vectors (freed by base)
   double* p_pad = nullptr;   // CG search direction, padded
   double* p_pad2 = nullptr;  // its second buffer (single rank: the p update fused into the SpMV, cg_fusep)
   double* p_pad3 = nullptr;  // third and fourth buffers (cg_pdb 4), allocated at the first solve that uses them
