@@ -225,6 +225,9 @@ def measure(argv, rank, world, comm_id, args, steps, warmup):
     per phase and per SpMV launch of the first 256 CG iterations of each solve."""
     t_setup = time.perf_counter()
     m = M.Macroc(argv, rank=rank, nranks=world, comm_id=comm_id)
+    # a peer that stopped or a mismatched collective fails the waiting rank with its rank and the
+    # operation named (communicator aborted) instead of hanging the job until the driver's timeout
+    m.set_option("comm_timeout", args.comm_timeout)
     m.set_timing(True)
     info = m.info
     log(f"[rank {rank}] {' '.join(map(str, argv))}: setup {time.perf_counter() - t_setup:.1f}s, device GB "
@@ -368,6 +371,9 @@ def main():
     ap.add_argument("--wall", type=float, default=570.0,
                     help="wall seconds the invocation must fit: warmup steps after the first are skipped when the "
                          "timed steps would not fit (reported as warmup_run); the timed steps are never cut")
+    ap.add_argument("--comm-timeout", type=float, default=120.0,
+                    help="seconds a rank's host wait on collective work may take before the communicator is aborted "
+                         "and the run fails with the rank and the operation named")
     ap.add_argument("--tail", type=float, default=30.0, help="seconds reserved after the timed steps (check, CPU "
                                                              "baseline)")
     args = ap.parse_args()

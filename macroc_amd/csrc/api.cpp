@@ -1144,8 +1144,8 @@ int mcx_time_step(void* ctx, int time_s, int* newton_its, double* res, int* ksp_
   }
   if (newton_its) *newton_its = it;
   if ((rc = mcx_update_vars(ctx))) return rc;  // src/main.c:83
-  MCX_HIP(hipStreamSynchronize(c.stream));
-  return 0;
+  MCX_HIP(hipEventRecord(c.ev_chunk[0], c.stream));
+  return comm_wait(c, c.ev_chunk[0], "time step end");
 } MCX_CATCH
 
 // ---------------------------------------------------------------- data access
@@ -1778,8 +1778,8 @@ int mcx_synchronize(void* ctx) try {
   MCX_ENTRY();
   GUARD(ctx);
   CTX(ctx);
-  MCX_HIP(hipStreamSynchronize(c.stream));
-  return 0;
+  MCX_HIP(hipEventRecord(c.ev_chunk[0], c.stream));  // the stream may hold collectives: bounded wait
+  return comm_wait(c, c.ev_chunk[0], "mcx_synchronize");
 } MCX_CATCH
 
 }  // extern "C"

@@ -1472,6 +1472,43 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
         // the slots held in wpre (24 bf16 / 12 f32) at unrolled positions: one 8-B x load per slot,
         // all issued before the first use (one round trip, not one per block)
         const int nfast = min(dl.L, 3 * per);
+#ifndef MCX_SPLIT_WALK_GROUPED
+#define MCX_SPLIT_WALK_GROUPED 1  // AIJ-split walk in quad groups (round 5: 44 -> 12 B of spills per lane at 256x4)
+#endif
+#if MCX_SPLIT_WALK_GROUPED
+        // the first 24 corrections in three groups of one quad each: the quad and its x gathers
+        // issued together, then its products (16 live VGPRs per group instead of 60 for all 24)
+#pragma unroll
+        for (int t = 0; t < 3; t++) {
+          if (t * per >= nfast) break;  // (uniform)
+          const u32x4 w = __builtin_nontemporal_load(Dn + t * 64);
+          double xv[8];
+#pragma unroll
+          for (int e = 0; e < 8; e++) {
+            const int p = t * per + e;
+            xv[e] = 0.;
+            if (e < per && p < nfast) xv[e] = x[3 * (int64_t)pc + (dl.xc[p] >> 2)];
+          }
+#pragma unroll
+          for (int e = 0; e < 8; e++) {
+            const int p = t * per + e;
+            if (e >= per || p >= nfast) continue;
+            const int r = dl.xc[p] & 3;
+            double v;
+            if (dl.wide) {
+              v = (double)__uint_as_float(w[e & 3]);
+            } else {
+              const unsigned hw = w[e >> 1];
+              v = (double)__uint_as_float((e & 1) ? (hw & 0xffff0000u) : (hw << 16));
+            }
+            const double tv = v * xv[e];
+            if (r == 0) d0 += tv;
+            else if (r == 1) d1 += tv;
+            else d2 += tv;
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#else
         // the first 24 corrections of this node (3 quads), loaded with the x gathers below
         u32x4 wpre[3] = {{0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}, {0u, 0u, 0u, 0u}};
 #pragma unroll
@@ -1499,6 +1536,7 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
           else if (r == 1) d1 += tv;
           else d2 += tv;
         }
+#endif
         for (int p = nfast; p < dl.L; p++) {  // beyond wpre (dense corrections): one slot at a time
           const u32x4 w = __builtin_nontemporal_load(Dn + (p / per) * 64);
           const int s = dl.s[p], nb = s / 9, rc = s - 9 * nb, r = rc / 3, cc = rc - 3 * r, e = p % per;
