@@ -248,15 +248,15 @@ static int cg_solve(Ctx& c, int* its, double* rnorm, int* reason) {
     int rc = 0;
     if ((rc = dalloc_pad(c, &c.p_pad3, npad)) || (rc = dalloc_pad(c, &c.p_pad4, npad))) return rc;
   }
-  if (c.xs_used && !c.p_pad58[0]) {  // cg_xs: buffers 5-8, the side stream and its events
+  if (c.xs_used) {  // cg_xs: buffers 5-8, the side stream and its events (each made once; a setup
+                    // that failed part-way completes at the next solve instead of running without them)
     const int64_t npad = (int64_t)c.g.PX * c.g.PY * c.g.PZ * 3;
     int rc = 0;
     for (int q = 0; q < 4; q++)
-      if ((rc = dalloc_pad(c, &c.p_pad58[q], npad))) return rc;
-    MCX_HIP(hipStreamCreateWithFlags(&c.x_stream, hipStreamNonBlocking));
-    MCX_HIP(hipEventCreateWithFlags(&c.ev_xp, hipEventDisableTiming));
-    MCX_HIP(hipEventCreateWithFlags(&c.ev_xd[0], hipEventDisableTiming));
-    MCX_HIP(hipEventCreateWithFlags(&c.ev_xd[1], hipEventDisableTiming));
+      if (!c.p_pad58[q] && (rc = dalloc_pad(c, &c.p_pad58[q], npad))) return rc;
+    if (!c.x_stream) MCX_HIP(hipStreamCreateWithFlags(&c.x_stream, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&c.ev_xp, &c.ev_xd[0], &c.ev_xd[1]})
+      if (!*e) MCX_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
   if (c.pdb_used) MCX_HIP(hipMemsetAsync(c.xdone, 0, sizeof(int), c.stream));
   CgState s{};

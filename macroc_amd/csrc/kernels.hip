@@ -801,8 +801,8 @@ __global__ __launch_bounds__(TPB) void k_split_esc(Geo g, Material mat, const do
     m += __builtin_popcount(esc);
   }
   const unsigned base = atomicAdd(cnt, m);
-  if (base + m > cap || m > 126u) {  // more escapes than the host sized for: the host falls back
-    eflag[n] = 0xffffffffu;
+  if (base + m > cap || m > 126u) {  // more escapes than the host sized for: build_split reads the
+    eflag[n] = 0xffffffffu;          // counter back and falls back to AIJ blocks (never dereferenced)
     return;
   }
   unsigned t = base;
@@ -4510,6 +4510,16 @@ int build_split(Ctx& c, bool* exact) {
     else
       hipLaunchKernelGGL(k_split_esc<false>, dim3(nblk(c.g.nown)), dim3(TPB), 0, c.stream, c.g, c.mat, ke_src(c), c.U,
                          c.esc_node, c.d_mask + 15, (unsigned)c.esc_cap, c.esc_res, c.esc_slot);
+    // the escape pass must have placed exactly the escapes the mask pass counted (an
+    // overflow leaves a sentinel k_split_dense would misread); otherwise this matrix goes to AIJ
+    // blocks (*exact = false)
+    unsigned placed = 0;
+    MCX_HIP(hipMemcpyAsync(&placed, c.d_mask + 15, sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
+    MCX_HIP(hipStreamSynchronize(c.stream));
+    if ((int64_t)placed != dl.nesc) {
+      c.dsl.nesc = 0;
+      *exact = false;
+    }
   }
   return 0;
 }
