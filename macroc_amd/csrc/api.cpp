@@ -85,7 +85,7 @@ static int free_ctx(Ctx* c) {
   if (c->x_stream) (void)hipStreamSynchronize(c->x_stream);
   void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->b, c->du, c->r, c->z, c->w, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->wd, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
                   c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->xdone, c->esc_node, c->esc_res, c->esc_slot, c->elem_plain, c->cref, c->vi_xslot,
-                  c->vi_xlist, c->vi_xcnt, c->vi_exc,
+                  c->vi_xlist, c->vi_xcnt, c->vi_exc, c->st_coef, c->st_ids, c->st_slot, c->st_list, c->st_cnt, c->st_mask,
                   c->partials, c->red, c->red_loc, c->cg, c->hist, c->tmp, c->halo.d_send_idx,
                   c->halo.d_recv_idx, c->halo.d_sendbuf, c->halo.d_recvbuf, c->halo.d_bnd};
   for (void* p : ptrs)
@@ -905,7 +905,7 @@ int mcx_assembly_jac(void* ctx) try {
     if ((rc = ensure_VI(c)) || (rc = build_vi(c, &ok))) return rc;
     if (ok) {
       c.fmt = FMT_VI;
-      if ((rc = build_wdesc(c))) return rc;
+      if ((rc = build_wdesc(c)) || (rc = build_st(c))) return rc;
       c.assembled = true;
       MCX_HIP(hipGetLastError());
       return 0;
@@ -1258,7 +1258,7 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) try 
   std::vector<unsigned char> Ih;
   std::vector<double> dict;
   std::vector<double> Xh;  // exception nodes' blocks
-  if (vals && c.fmt == FMT_VI && c.vi_block && c.vi_nexc) {  // [243][xld], slot fastest
+  if (vals && c.fmt == FMT_VI && c.vi_block && c.vi_nexc) {  // AoSoA (exc_base)
     Xh.resize((size_t)c.g.xld * 27 * 9);
     MCX_HIP(hipMemcpyAsync(Xh.data(), c.vi_exc, Xh.size() * sizeof(double), hipMemcpyDeviceToHost, c.stream));
   }
@@ -1358,7 +1358,7 @@ int mcx_dump_csr(void* ctx, int64_t* rowptr, int64_t* colidx, double* vals) try 
             if (c.vi_block) {  // byte nb of 2 chunks of 16 B: the block's dictionary entry
               uint32_t xs = 0;  // exception slot + 1 in bytes 28-31
               std::memcpy(&xs, &Ih[(((n >> 6) * 2 + 1) * 64 + (n & 63)) * 16 + 12], 4);
-              if (xs && !Xh.empty()) v = Xh[(size_t)(nb * 9 + r * 3 + cc) * c.g.xld + (xs - 1)];
+              if (xs && !Xh.empty()) v = Xh[exc_base(xs - 1) + (nb * 9 + r * 3 + cc) * 64];
               else v = dict[Ih[(((n >> 6) * 2 + (nb >> 4)) * 64 + (n & 63)) * 16 + (nb & 15)] * VIB_STRIDE + r * 3 + cc];
             } else if (c.vi_bits == 8) {
               v = dict[Ih[(((n >> 6) * VI_CHUNKS + (s >> 4)) * 64 + (n & 63)) * 16 + (s & 15)]];
@@ -1472,7 +1472,9 @@ int mcx_get_timing(void* ctx, mcx_timing* t) try {
       2 * 3 * (int64_t)c.g.nown * 8;
   if (c.fmt == FMT_SPLIT) t->spmv_bytes_per_launch += (int64_t)c.g.nown * c.dsl.Lq * 16;
   if (c.fmt == FMT_VI && c.vi_block) t->spmv_bytes_per_launch += c.vi_nexc * 27 * 9 * 8;  // exception blocks
-  if (wd_used(c)) {  // wave descriptors: 128 B per wave and plane, index bytes for the waves that still read per-lane words
+  if (st_used(c)) {  // default stencil: no index bytes but the listed nodes'; the patch masks
+    t->spmv_bytes_per_launch += c.st_n * 32 - c.nnz_local / 9 + (int64_t)c.st_npx * c.st_npy * c.g.nz * 8;
+  } else if (wd_used(c)) {  // wave descriptors: 128 B per wave and plane, index bytes for the waves that still read per-lane words
     const int64_t nwp = (int64_t)c.wd_npx * c.wd_npy * c.g.nz;
     t->spmv_bytes_per_launch += nwp * 128 - c.nnz_local / 9 +
                                 (!c.vi_fma ? c.wd_blocks_exact : c.vi_wdesc == 2 ? c.wd_blocks_two : c.wd_blocks_fma);
@@ -1619,6 +1621,10 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
   }
   if (!std::strcmp(name, "cg_p2d")) {
     c.cg_p2d = value != 0.;
+    return 0;
+  }
+  if (!std::strcmp(name, "vi_st")) {  // takes effect at once if the structures were built (they are by default)
+    c.vi_st = value != 0.;
     return 0;
   }
   if (!std::strcmp(name, "vi_exc_kernel")) {

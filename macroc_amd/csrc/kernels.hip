@@ -2301,9 +2301,9 @@ __global__ __launch_bounds__(TPB) void k_exc_flag(Geo g, const unsigned char* __
   if (threadIdx.x == 0) cnt[blockIdx.x] = (unsigned)c;
 }
 
-// pass 2 (one block): cnt[0..nb) -> exclusive prefix sums, the total to ctl[2] (read back with the
-// block-build's sets)
-__global__ __launch_bounds__(1024) void k_exc_scan(unsigned* __restrict__ cnt, int nb, unsigned* __restrict__ ctl) {
+// pass 2 (one block): cnt[0..nb) -> exclusive prefix sums, the total to *total (exceptions: the
+// block build's ctl[2], read back with its sets)
+__global__ __launch_bounds__(1024) void k_exc_scan(unsigned* __restrict__ cnt, int nb, unsigned* __restrict__ total) {
   __shared__ unsigned s[1024];
   const int t = threadIdx.x, per = (nb + 1023) / 1024, lo = min(nb, t * per), hi = min(nb, lo + per);
   unsigned sum = 0u;
@@ -2322,7 +2322,7 @@ __global__ __launch_bounds__(1024) void k_exc_scan(unsigned* __restrict__ cnt, i
     cnt[q] = run;
     run += c;
   }
-  if (t == 1023) ctl[2] = s[1023];
+  if (t == 1023) *total = s[1023];
 }
 
 // pass 3: slot = the block's offset + the node's rank among the block's exception nodes;
@@ -2346,8 +2346,8 @@ __global__ __launch_bounds__(TPB) void k_exc_assign(Geo g, unsigned* __restrict_
   }
 }
 
-// the exception nodes' 27 blocks, value (nb, q) of slot s at exc[(nb * 9 + q) * g.xld + s] (slot
-// fastest): thread = (slot, nb); each element block from kref (plain elements) or from Ke (the
+// the exception nodes' 27 blocks, value (nb, q) of slot s at exc[exc_base(s) + (nb * 9 + q) * 64]
+// (AoSoA): thread = (slot, nb); each element block from kref (plain elements) or from Ke (the
 // others: k_element_ke forms only those)
 __global__ __launch_bounds__(TPB) void k_exc_fill(Geo g, Material mat, const double* __restrict__ Ke,
                                                   const double* __restrict__ kref,
@@ -2364,7 +2364,7 @@ __global__ __launch_bounds__(TPB) void k_exc_fill(Geo g, Material mat, const dou
   matrix_block<true>(g, mat, Ke, g.xs + i, g.ys + j, g.zs + k, nb % 3 - 1, (nb / 3) % 3 - 1, nb / 9 - 1, val,
                      kref, plain);
 #pragma unroll
-  for (int q = 0; q < 9; q++) exc[(int64_t)(nb * 9 + q) * g.xld + t] = val[q];
+  for (int q = 0; q < 9; q++) exc[exc_base(t) + (nb * 9 + q) * 64] = val[q];
 }
 
 __device__ __forceinline__ double jacobi_inv(double d) {
@@ -2385,7 +2385,7 @@ __global__ void k_jacobi_vib(Geo g, const unsigned char* __restrict__ I, const d
   jix[n] = xs ? 255 : (unsigned char)id;  // 255: the CG kernels read dinv (jac_inv)
 #pragma unroll
   for (int r = 0; r < 3; r++)
-    dinv[3 * n + r] = jacobi_inv(xs ? exc[(int64_t)(13 * 9 + r * 4) * g.xld + (xs - 1)] : bdict[id * VIB_STRIDE + r * 4]);
+    dinv[3 * n + r] = jacobi_inv(xs ? exc[exc_base(xs - 1) + (13 * 9 + r * 4) * 64] : bdict[id * VIB_STRIDE + r * 4]);
 }
 
 // the dictionary's inverse diagonals [VI_MAX][3] (same values as k_jacobi_vib's dinv)
@@ -2436,7 +2436,7 @@ __global__ __launch_bounds__(TPB) void k_spmv_vib(Geo g, const u32x4* __restrict
       double a[9];
       if (EXC && w1[3]) {
 #pragma unroll
-        for (int q = 0; q < 9; q++) a[q] = exc[(int64_t)(nb * 9 + q) * g.xld + (w1[3] - 1)];
+        for (int q = 0; q < 9; q++) a[q] = exc[exc_base(w1[3] - 1) + (nb * 9 + q) * 64];
       } else {
         const double2* e = tab + id * (VIB_STRIDE / 2);
         const double2 a01 = e[0], a23 = e[1], a45 = e[2], a67 = e[3], a8 = e[4];
@@ -2856,12 +2856,12 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       // round trip per group instead of per block.
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
       InodeRows<true> acc;  // !FMA: all 27 neighbours present (full)
-      const double* eb = exc + (c1[3] - 1);  // value v at eb[v * g.xld]
+      const double* eb = exc + exc_base(c1[3] - 1);  // value v at eb[v * 64]
 #pragma unroll 1
       for (int nb0 = 0; nb0 < 27; nb0 += 3) {
         double av[27];
 #pragma unroll
-        for (int q = 0; q < 27; q++) av[q] = eb[(int64_t)(nb0 * 9 + q) * g.xld];
+        for (int q = 0; q < 27; q++) av[q] = eb[(nb0 * 9 + q) * 64];
         const int dy = (nb0 / 3) % 3 - 1, dz = nb0 / 9 - 1;
         const int xo = ((k + dz - k0 + 1) % R) * PLANE + (ly + 1 + dy) * RL + 3 * lx;
 #pragma unroll
@@ -2990,14 +2990,14 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
       const int ei = i0 + ex, ej = j0 + ey;
       const int64_t n = ei + g.nx * (ej + (int64_t)g.ny * kk);
       const unsigned slot = I[(int64_t)(n >> 6) * (2 * 64) + (n & 63) + 64][3];
-      const double* eb = exc + (slot - 1);  // value v at eb[v * g.xld]
+      const double* eb = exc + exc_base(slot - 1);  // value v at eb[v * 64]
       double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
       InodeRows<true> acc;  // !FMA: listed nodes are full (boundary nodes go to k_spmv_vib_faces)
 #pragma unroll 1
       for (int nb0 = 0; nb0 < 27; nb0 += 3) {
         double av[27];
 #pragma unroll
-        for (int q = 0; q < 27; q++) av[q] = eb[(int64_t)(nb0 * 9 + q) * g.xld];
+        for (int q = 0; q < 27; q++) av[q] = eb[(nb0 * 9 + q) * 64];
         const int dy = (nb0 / 3) % 3 - 1, dz = nb0 / 9 - 1;
         const double* xr = x + 3 * ((int64_t)ei + (ej + 1 + dy) * (int64_t)PX + (kk + 1 + dz) * (int64_t)PXY);
         double xw[9];
@@ -3031,6 +3031,275 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
     double s = block_sum<T>(dot, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = s;
   }
+}
+
+// ---------------------------------------------------------------------------- default-stencil SpMV
+// Round 5 (vi_st).  On the block-indexed storage almost every node carries the same 27 block
+// indices: the interior stencil of the uniform grid (at 256^3 all but the ~3 % of nodes on the
+// domain faces, next to Dirichlet nodes, or exception nodes).  The matrix is then held as
+//   * the default stencil: the 27 blocks of one interior node (st_coef, 243 doubles, read by every
+//     wave with scalar loads),
+//   * a 64-bit mask per 16 x 4 node patch and plane: the lanes whose node is not default (its
+//     index bytes differ, or it is an exception node, or it is outside the domain),
+//   * the list of the non-default nodes (ordered compaction, owned-node order), whose rows come
+//     from their own index bytes / exception blocks exactly as before.
+// k_spmv_st marches a 64 x 16 tile up its z-chunk two planes per step (nodes k and k+1 per lane):
+// each group of 3 blocks (one (dy, dz) stencil row) is loaded once for two nodes, so the scalar
+// loads and their waits per node halve; the x ring in LDS holds planes k-1 .. k+2, and planes k+3,
+// k+4 are loaded into registers during the step and stored after a barrier.  The default path
+// reads no index bytes.  Rows are the FMA rows of k_spmv_vibm (one fused multiply-add per term in
+// (nb, c) order), so y is bitwise what k_spmv_vibm computes; a non-default lane's row is left to
+// k_spmv_fix, which computes it from its index bytes (dictionary in global memory) or exception
+// blocks, x gathered, in the same order.  p.w partials: the march's blocks, then k_spmv_fix's.
+template <bool DOT, bool GATED>
+__global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restrict__ coef,
+                                                  const unsigned long long* __restrict__ mask, int npx, int npy,
+                                                  const double* __restrict__ x, double* __restrict__ y,
+                                                  double* __restrict__ part, const CgState* __restrict__ cg,
+                                                  ZTiling zt) {
+  constexpr int TX = 64, TY = 16, T = TX * TY, RL = vibm_rl<TX, true>(), PR = TY + 2, PLANE = PR * RL;
+  constexpr int NL = (PLANE + T - 1) / T, R = 4;
+  __shared__ double xs[R][PLANE];
+  __shared__ double sh[T / 64];
+  if (GATED && cg->reason) return;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, t8 = b >> 3;
+  const int slab = (zt.nty + 7) >> 3;
+  const int ty0 = xcd * slab;
+  const int nty_here = min(slab, zt.nty - ty0);
+  const int per = max(nty_here, 0) * zt.ntx * zt.nzc;
+  if (t8 >= per) {  // whole block idle (uniform): still write the partial
+    if (DOT && threadIdx.x == 0) part[blockIdx.x] = 0.;
+    return;
+  }
+  const int txi = t8 % zt.ntx, r8 = t8 / zt.ntx;
+  const int tyi = ty0 + r8 % nty_here, zc = r8 / nty_here;
+  const int i0 = txi * TX, j0 = tyi * TY;
+  const int k0 = zc * zt.kc, k1 = min(g.nz, k0 + zt.kc);
+  const int me = threadIdx.x, wv = me >> 6, ln = me & 63;
+  const int px = wv & 3, py = wv >> 2;  // 16 x 4 patch of the tile (every wave does the same work)
+  const int lx = px * 16 + (ln & 15), ly = py * 4 + (ln >> 4);
+  const int i = i0 + lx, j = j0 + ly;
+  const bool inxy = i < g.nx && j < g.ny;
+  const int PX = g.PX, PXY = g.PX * g.PY;
+  const int gpx = __builtin_amdgcn_readfirstlane((i0 >> 4) + px), gpy = __builtin_amdgcn_readfirstlane((j0 >> 2) + py);
+  const bool wvin = gpx < npx && gpy < npy;  // (uniform) the patch has a mask
+  const int len = 3 * min(TX + 2, g.nx + 2 - i0);
+  const int rows = min(TY + 2, g.ny + 2 - j0);
+  auto xload = [&](int p, int m) -> double {  // x of padded plane p + 1 (p = -1 .. nz), staged element me + m T
+    const int e = me + m * T;
+    const int rr = e / RL, o = e - rr * RL;
+    if (e >= PLANE || o >= len || rr >= rows || p > g.nz) return 0.;
+    return x[3 * (int64_t)(i0 + (j0 + rr) * PX + (p + 1) * PXY) + o];
+  };
+#pragma unroll
+  for (int s = 0; s < 4; s++)  // prologue: planes k0-1 .. k0+2 in ring slots 0 .. 3
+#pragma unroll
+    for (int m = 0; m < NL; m++) {
+      const int e = me + m * T;
+      if (e < PLANE) xs[s][e] = xload(k0 - 1 + s, m);
+    }
+  __syncthreads();
+  typedef const volatile __attribute__((address_space(3))) double lds_vdouble;
+  lds_vdouble* xsv = (lds_vdouble*)&xs[0][0];
+  double dot = 0.;
+  for (int k = k0; k < k1; k += 2) {
+    const bool two = k + 1 < k1, more = k + 2 < k1;
+    double xr[2][NL];
+    if (more) {  // planes k+3 and k+4, in flight during the step
+#pragma unroll
+      for (int m = 0; m < NL; m++) {
+        xr[0][m] = xload(k + 3, m);
+        xr[1][m] = xload(k + 4, m);
+      }
+    }
+    unsigned long long m0 = ~0ull, m1 = ~0ull;  // lanes to leave to k_spmv_fix
+    if (wvin) {
+      m0 = mask[((int64_t)k * npy + gpy) * npx + gpx];
+      if (two) m1 = mask[((int64_t)(k + 1) * npy + gpy) * npx + gpx];
+    }
+    double ya0 = 0., ya1 = 0., ya2 = 0., yb0 = 0., yb1 = 0., yb2 = 0.;
+    double ca0 = 0., ca1 = 0., ca2 = 0., cb0 = 0., cb1 = 0., cb2 = 0.;
+#pragma unroll
+    for (int g9 = 0; g9 < 9; g9++) {  // stencil row (dy, dz): blocks nb = 3 g9 .. 3 g9 + 2 (dx = -1, 0, 1)
+      const int dy = g9 % 3 - 1, dz = g9 / 3 - 1;
+      double av[27], xa[9], xb[9];
+#pragma unroll
+      for (int q = 0; q < 27; q++) av[q] = coef[g9 * 27 + q];
+      const int ra = ((k + dz - k0 + 1) & 3) * PLANE + (ly + 1 + dy) * RL + 3 * lx;
+      const int rb = ((k + 1 + dz - k0 + 1) & 3) * PLANE + (ly + 1 + dy) * RL + 3 * lx;
+#pragma unroll
+      for (int q = 0; q < 9; q++) {
+        xa[q] = xsv[ra + q];
+        xb[q] = xsv[rb + q];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int t = 0; t < 3; t++) {
+        if (g9 * 3 + t == 13) {
+          ca0 = xa[3], ca1 = xa[4], ca2 = xa[5];
+          cb0 = xb[3], cb1 = xb[4], cb2 = xb[5];
+        }
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+          const int r = q / 3, cc = q % 3;
+          const double a = av[t * 9 + q];
+          double& ya = r == 0 ? ya0 : (r == 1 ? ya1 : ya2);
+          double& yb = r == 0 ? yb0 : (r == 1 ? yb1 : yb2);
+          ya = __builtin_fma(a, xa[3 * t + cc], ya);
+          yb = __builtin_fma(a, xb[3 * t + cc], yb);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (inxy && !((m0 >> ln) & 1ull)) {
+      const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
+      __builtin_nontemporal_store(ya0, &y[3 * n + 0]);
+      __builtin_nontemporal_store(ya1, &y[3 * n + 1]);
+      __builtin_nontemporal_store(ya2, &y[3 * n + 2]);
+      if (DOT) dot += ca0 * ya0 + ca1 * ya1 + ca2 * ya2;
+    }
+    if (two && inxy && !((m1 >> ln) & 1ull)) {
+      const int64_t n = i + g.nx * (j + (int64_t)g.ny * (k + 1));
+      __builtin_nontemporal_store(yb0, &y[3 * n + 0]);
+      __builtin_nontemporal_store(yb1, &y[3 * n + 1]);
+      __builtin_nontemporal_store(yb2, &y[3 * n + 2]);
+      if (DOT) dot += cb0 * yb0 + cb1 * yb1 + cb2 * yb2;
+    }
+    if (more) {  // (uniform) planes k+3, k+4 replace k-1, k (no longer read)
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < NL; m++) {
+        const int e = me + m * T;
+        if (e < PLANE) {
+          xs[(k + 3 - k0 + 1) & 3][e] = xr[0][m];
+          xs[(k + 4 - k0 + 1) & 3][e] = xr[1][m];
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (DOT) {
+    const double s = block_sum<T>(dot, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+  }
+}
+
+// The non-default rows of the default-stencil SpMV (k_spmv_st): one thread per listed node, its
+// 27 blocks from its index bytes (dictionary in global memory, 20 KB, cache resident) or, for an
+// exception node, from exc; x gathered from the padded vector; the FMA rows of k_spmv_vibm.
+template <bool DOT, bool GATED>
+__global__ __launch_bounds__(TPB) void k_spmv_fix(Geo g, const int* __restrict__ list, int64_t cnt,
+                                                  const u32x4* __restrict__ I, const double* __restrict__ bdict,
+                                                  const double* __restrict__ exc, const double* __restrict__ x,
+                                                  double* __restrict__ y, double* __restrict__ part,
+                                                  const CgState* __restrict__ cg) {
+  __shared__ double sh[TPB / 64];
+  if (GATED && cg->reason) return;
+  const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
+  double dot = 0.;
+  if (t < cnt) {
+    const int n = list[t];
+    int i, j, k;
+    node_ijk(g, n, i, j, k);
+    const int PX = g.PX, PXY = g.PX * g.PY;
+    const u32x4* ip = I + (int64_t)(n >> 6) * (2 * 64) + (n & 63);
+    const u32x4 w0 = ip[0], w1 = ip[64];
+    const unsigned slot = w1[3];  // exception slot + 1
+    double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+#pragma unroll 1
+    for (int nb0 = 0; nb0 < 27; nb0 += 3) {
+      double av[27];
+#pragma unroll
+      for (int t3 = 0; t3 < 3; t3++) {
+        const int nb = nb0 + t3;
+        const unsigned word = nb < 16 ? w0[nb >> 2] : w1[(nb - 16) >> 2];
+        const double* e = slot ? exc + exc_base(slot - 1) + nb * 9 * 64 : bdict + ((word >> (8 * (nb & 3))) & 255u) * VIB_STRIDE;
+        const int es = slot ? 64 : 1;
+#pragma unroll
+        for (int q = 0; q < 9; q++) av[t3 * 9 + q] = e[q * es];
+      }
+      const int dy = (nb0 / 3) % 3 - 1, dz = nb0 / 9 - 1;
+      const double* xr = x + 3 * ((int64_t)i + (j + 1 + dy) * (int64_t)PX + (k + 1 + dz) * (int64_t)PXY);
+      double xw[9];
+#pragma unroll
+      for (int q = 0; q < 9; q++) xw[q] = xr[q];
+#pragma unroll
+      for (int t3 = 0; t3 < 3; t3++) {
+        if (nb0 + t3 == 13) {
+          xc0 = xw[3], xc1 = xw[4], xc2 = xw[5];
+        }
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+          const int r = q / 3, cc = q % 3;
+          double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
+          yr = __builtin_fma(av[t3 * 9 + q], xw[3 * t3 + cc], yr);
+        }
+      }
+    }
+    __builtin_nontemporal_store(y0, &y[3 * (int64_t)n + 0]);
+    __builtin_nontemporal_store(y1, &y[3 * (int64_t)n + 1]);
+    __builtin_nontemporal_store(y2, &y[3 * (int64_t)n + 2]);
+    if (DOT) dot = xc0 * y0 + xc1 * y1 + xc2 * y2;
+  }
+  if (DOT) {
+    const double sm = block_sum<TPB>(dot, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = sm;
+  }
+}
+
+// default-stencil build, pass 0 (one block): the 27 blocks of node `center` (its index bytes into
+// the dictionary) as coef[243] and its 7 index words as ids[0..6]; ids[7] = 1 when the node is an
+// exception node (no default stencil then)
+__global__ void k_st_setup(const u32x4* __restrict__ I, const double* __restrict__ bdict, int center,
+                           double* __restrict__ coef, unsigned* __restrict__ ids) {
+  const int t = threadIdx.x;
+  const u32x4* ip = I + (int64_t)(center >> 6) * (2 * 64) + (center & 63);
+  const u32x4 w0 = ip[0], w1 = ip[64];
+  if (t < 243) {
+    const int nb = t / 9, q = t % 9;
+    const unsigned word = nb < 16 ? w0[nb >> 2] : w1[(nb - 16) >> 2];
+    coef[t] = bdict[((word >> (8 * (nb & 3))) & 255u) * VIB_STRIDE + q];
+  }
+  if (t < 7) ids[t] = t < 4 ? w0[t] : w1[t - 4];
+  if (t == 7) ids[7] = w1[3] != 0u ? 1u : 0u;
+}
+
+// pass 1: flag[n] = 1 for a node whose index words differ from the default's or that is an
+// exception node; cnt[block] = the block's count (then k_exc_scan / k_exc_assign: list in
+// owned-node order, flag -> slot + 1)
+__global__ __launch_bounds__(TPB) void k_st_flag(Geo g, const u32x4* __restrict__ I, const unsigned* __restrict__ ids,
+                                                 unsigned* __restrict__ flag, unsigned* __restrict__ cnt) {
+  const int n = blockIdx.x * TPB + threadIdx.x;
+  bool nd = false;
+  if (n < g.nown) {
+    const u32x4* ip = I + (int64_t)(n >> 6) * (2 * 64) + (n & 63);
+    const u32x4 w0 = ip[0], w1 = ip[64];
+    unsigned diff = w1[3];
+#pragma unroll
+    for (int q = 0; q < 7; q++) diff |= (q < 4 ? w0[q] : w1[q - 4]) ^ ids[q];
+    nd = diff != 0u;
+    flag[n] = nd ? 1u : 0u;
+  }
+  const int c = __syncthreads_count(nd);
+  if (threadIdx.x == 0) cnt[blockIdx.x] = (unsigned)c;
+}
+
+// pass 2: one 64-bit mask per 16 x 4 patch and plane (k_spmv_st's wave layout): bit = the lane's
+// node is listed (slot != 0) or outside the domain
+__global__ __launch_bounds__(TPB) void k_st_mask(Geo g, const unsigned* __restrict__ slot,
+                                                 unsigned long long* __restrict__ mask, int npx, int npy) {
+  const int64_t w = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
+  const int ln = threadIdx.x & 63;
+  if (w >= (int64_t)npx * npy * g.nz) return;  // (whole wave)
+  const int px = (int)(w % npx);
+  const int64_t r = w / npx;
+  const int py = (int)(r % npy), k = (int)(r / npy);
+  const int i = px * 16 + (ln & 15), j = py * 4 + (ln >> 4);
+  bool skip = true;
+  if (i < g.nx && j < g.ny) skip = slot[i + g.nx * (j + (int64_t)g.ny * k)] != 0u;
+  const unsigned long long m = __ballot(skip);
+  if (ln == 0) mask[w] = m;
 }
 
 // Owned nodes on the global domain boundary (faces whose stencil the DMDA clips), enumerated
@@ -3124,10 +3393,10 @@ __global__ __launch_bounds__(TPB) void k_spmv_vib_faces(Geo g, const u32x4* __re
         xc2 = xv[2];
       }
       const double* e;
-      int64_t es = 1;  // stride of the block's values: the dictionary's 1, the exception array's xld
+      int es = 1;  // stride of the block's values: the dictionary's 1, the exception array's 64
       if (EXC && slot) {
-        e = exc + (int64_t)(nb * 9) * g.xld + (slot - 1);
-        es = g.xld;
+        e = exc + exc_base(slot - 1) + nb * 9 * 64;
+        es = 64;
       } else {
         const unsigned word = nb < 16 ? w0[nb >> 2] : w1[(nb - 16) >> 2];
         e = bdict + ((word >> (8 * (nb & 3))) & 255u) * VIB_STRIDE;
@@ -3173,14 +3442,14 @@ __global__ __launch_bounds__(TPB) void k_spmv_exc(Geo g, const int* __restrict__
   }
   if (n >= 0) {
     const int PX = g.PX, PXY = g.PX * g.PY;
-    const double* eb = exc + t;  // value v at eb[v * g.xld]
+    const double* eb = exc + exc_base(t);  // value v at eb[v * 64]
     double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
     InodeRows<true> acc;
 #pragma unroll 1
     for (int nb0 = 0; nb0 < 27; nb0 += 3) {  // one dy row of the stencil: 27 values, 9 x
       double av[27];
 #pragma unroll
-      for (int q = 0; q < 27; q++) av[q] = eb[(int64_t)(nb0 * 9 + q) * g.xld];
+      for (int q = 0; q < 27; q++) av[q] = eb[(nb0 * 9 + q) * 64];
       const int dy = (nb0 / 3) % 3 - 1, dz = nb0 / 9 - 1;
       const double* xr = x + 3 * ((int64_t)i + (j + 1 + dy) * (int64_t)PX + (k + 1 + dz) * (int64_t)PXY);
       double xw[9];
@@ -4311,15 +4580,28 @@ static int64_t faces_blocks(const Ctx& c) {
   return (face_enum(c.g).n + TPB - 1) / TPB;
 }
 
+bool fusep(const Ctx& c);
+
+// the default-stencil SpMV (k_spmv_st + k_spmv_fix): FMA rows on the 64 x 16 staged tiles with the
+// scalar-dictionary patches, not the fused p update
+bool st_used(const Ctx& c) {
+  int tx, ty;
+  vis_shape(c, tx, ty);
+  return c.vi_st && c.st_ok && c.fmt == FMT_VI && c.vi_block && vi_staged(c) && c.vi_fma && c.vi_uni && c.vi_patch &&
+         tx == 64 && !fusep(c);
+}
+
+static int64_t fix_blocks(const Ctx& c) { return st_used(c) ? (c.st_n + TPB - 1) / TPB : 0; }
+
 // the exception rows' kernel (staged block-indexed storage with exception nodes, vi_exc_kernel)
 static int64_t exc_blocks(const Ctx& c) {
-  if (!(c.fmt == FMT_VI && c.vi_block && c.vi_nexc && vi_staged(c) && c.vi_exc_kernel)) return 0;
+  if (!(c.fmt == FMT_VI && c.vi_block && c.vi_nexc && vi_staged(c) && c.vi_exc_kernel) || st_used(c)) return 0;
   return (c.vi_nexc + TPB - 1) / TPB;
 }
 
 int64_t spmv_nparts(const Ctx& c) {
   if (c.fmt == FMT_SPLIT && c.dsl.dense) return node_blocks(c);
-  return spmv_grid_blocks(c) + faces_blocks(c) + exc_blocks(c);
+  return spmv_grid_blocks(c) + faces_blocks(c) + exc_blocks(c) + fix_blocks(c);
 }
 
 int upload_constants(Ctx& c) {
@@ -4574,7 +4856,7 @@ static int build_vib(Ctx& c, bool* ok) {
   if (exc) {  // ordered compaction: slots in owned-node order
     const unsigned nbn = nblk(c.g.nown);
     hipLaunchKernelGGL(k_exc_flag, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.elem_plain, c.vi_xslot, c.vi_xcnt);
-    hipLaunchKernelGGL(k_exc_scan, dim3(1), dim3(1024), 0, c.stream, c.vi_xcnt, (int)nbn, c.vib_ctl);
+    hipLaunchKernelGGL(k_exc_scan, dim3(1), dim3(1024), 0, c.stream, c.vi_xcnt, (int)nbn, c.vib_ctl + 2);
     hipLaunchKernelGGL(k_exc_assign, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.vi_xslot, c.vi_xlist, c.vi_xcnt);
   }
   const unsigned* xslot = exc ? c.vi_xslot : nullptr;
@@ -4603,8 +4885,8 @@ static int build_vib(Ctx& c, bool* ok) {
       c.device_bytes -= c.vi_exc_bytes;
       c.vi_exc = nullptr;
     }
-    // [243][xld], slot fastest; grown with headroom (the plastic zone spreads over the time steps),
-    // the leading dimension a multiple of 64 slots (whole 512-B lines per wave)
+    // AoSoA groups of 64 slots (exc_base); grown with headroom (the plastic zone spreads over the
+    // time steps)
     c.g.xld = (std::min<int64_t>(2 * nexc + 1024, c.g.nown) + 63) / 64 * 64;
     c.vi_exc_bytes = c.g.xld * 27 * 9 * (int64_t)sizeof(double);
     MCX_HIP(hipMalloc(&c.vi_exc, c.vi_exc_bytes));
@@ -4777,6 +5059,50 @@ int build_wdesc(Ctx& c) {
   c.wd_blocks_exact = (int64_t)h[1];
   c.wd_blocks_two = (int64_t)h[2];
   c.wd_ok = true;
+  return 0;
+}
+
+// default-stencil structures (k_spmv_st): the stencil of the middle node, the list of the other
+// nodes (ordered compaction), the patch masks; one host round trip for the list's length
+int build_st(Ctx& c) {
+  c.st_ok = false;
+  if (!(c.fmt == FMT_VI && c.vi_block && vi_staged(c) && c.g.nown > 0)) return 0;
+  const int npx = (c.g.nx + 15) / 16, npy = (c.g.ny + 3) / 4;
+  const int64_t nwp = (int64_t)npx * npy * c.g.nz;
+  if (!c.st_coef) {
+    MCX_HIP(hipMalloc(&c.st_coef, 256 * sizeof(double)));
+    MCX_HIP(hipMalloc(&c.st_ids, 8 * sizeof(unsigned)));
+    MCX_HIP(hipMalloc(&c.st_slot, c.g.nown * sizeof(unsigned)));
+    MCX_HIP(hipMalloc(&c.st_list, c.g.nown * sizeof(int)));
+    MCX_HIP(hipMalloc(&c.st_cnt, (node_blocks(c) + 1) * sizeof(unsigned)));
+    c.device_bytes += 256 * 8 + 32 + c.g.nown * 8 + (node_blocks(c) + 1) * 4;
+  }
+  if (nwp * 8 > c.st_mask_bytes) {
+    if (c.st_mask) {
+      MCX_HIP(hipFree(c.st_mask));
+      c.device_bytes -= c.st_mask_bytes;
+    }
+    MCX_HIP(hipMalloc(&c.st_mask, nwp * 8));
+    c.st_mask_bytes = nwp * 8;
+    c.device_bytes += c.st_mask_bytes;
+  }
+  const u32x4* I = reinterpret_cast<const u32x4*>(c.vi_idx);
+  const int center = c.g.nx / 2 + c.g.nx * (c.g.ny / 2 + c.g.ny * (c.g.nz / 2));
+  const unsigned nbn = nblk(c.g.nown);
+  hipLaunchKernelGGL(k_st_setup, dim3(1), dim3(256), 0, c.stream, I, c.vi_bdict, center, c.st_coef, c.st_ids);
+  hipLaunchKernelGGL(k_st_flag, dim3(nbn), dim3(TPB), 0, c.stream, c.g, I, c.st_ids, c.st_slot, c.st_cnt);
+  hipLaunchKernelGGL(k_exc_scan, dim3(1), dim3(1024), 0, c.stream, c.st_cnt, (int)nbn, c.st_cnt + nbn);
+  hipLaunchKernelGGL(k_exc_assign, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.st_slot, c.st_list, c.st_cnt);
+  hipLaunchKernelGGL(k_st_mask, dim3((unsigned)((nwp + TPB / 64 - 1) / (TPB / 64))), dim3(TPB), 0, c.stream, c.g,
+                     c.st_slot, c.st_mask, npx, npy);
+  unsigned h[2] = {0u, 0u};
+  MCX_HIP(hipMemcpyAsync(&h[0], c.st_cnt + nbn, sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipMemcpyAsync(&h[1], c.st_ids + 7, sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipStreamSynchronize(c.stream));
+  c.st_n = h[0];
+  c.st_npx = npx;
+  c.st_npy = npy;
+  c.st_ok = h[1] == 0u;  // the middle node is an exception node: no default stencil
   return 0;
 }
 
@@ -5013,6 +5339,23 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
       zt.ypair = c.vi_ypair && (c.g.nx % 2) == 0;
       int tx, ty;
       vis_shape(c, tx, ty);
+      if (st_used(c)) {  // default stencil: two planes per step, the listed rows after the march
+        const int64_t nbf = fix_blocks(c);
+        double* pf = c.partials + nb;
+#define MCX_ST(DV, GV)                                                                                             \
+  do {                                                                                                            \
+    hipLaunchKernelGGL((k_spmv_st<DV, GV>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask, c.st_npx, \
+                       c.st_npy, xpad, y, c.partials, c.cg, zt);                                                  \
+    if (nbf)                                                                                                      \
+      hipLaunchKernelGGL((k_spmv_fix<DV, GV>), dim3((unsigned)nbf), dim3(TPB), 0, c.stream, c.g, c.st_list, c.st_n, \
+                         I, c.vi_bdict, c.vi_exc, xpad, y, pf, c.cg);                                             \
+  } while (0)
+        if (dot && gated) MCX_ST(true, true);
+        else if (dot) MCX_ST(true, false);
+        else MCX_ST(false, false);
+#undef MCX_ST
+        return;
+      }
 #define MCX_VIBM(TXV, TYV, XVV, UV, PV, ...)                                                                          \
   do {                                                                                                             \
     if (dot && gated)                                                                                              \

@@ -33,7 +33,7 @@ struct Geo {
   int ex0, ey0, ez0;       // first element evaluated on this device (global)
   int nex, ney, nez;       // extended element counts (owned + upper ghost layer)
   int64_t nelem;           // nex*ney*nez
-  int64_t xld;             // value-indexed exception blocks: leading dimension (slot capacity) of exc [243][xld]
+  int64_t xld;             // value-indexed exception blocks: slot capacity of exc (a multiple of 64, exc_base)
   int bc_type;
   double lx, lz, dx, dz, rad, wg;
 };
@@ -68,6 +68,11 @@ struct HaloPlan {
 };
 
 struct Ctx;
+
+// value-indexed exception blocks, AoSoA: groups of 64 slots, each group value-major (243 runs of 64
+// doubles, one per value (nb, r, c)), so a wave of 64 consecutive slots reads one 512-B run per value
+// and a group's values are contiguous (124 KB); value v of slot s at exc[exc_base(s) + v * 64]
+__host__ __device__ inline int64_t exc_base(int64_t s) { return (s >> 6) * (243 * 64) + (s & 63); }
 
 // Matrix storage of a context.  FMT_V: AIJ stencil blocks (all 27 blocks per node, every row
 // summed in the reference's MatMult order (inode column pairs)).  FMT_U: MATSBAIJ (upper blocks, lower mirrored).  FMT_SPLIT:
@@ -229,7 +234,7 @@ struct Ctx {
   unsigned* vi_xslot = nullptr;         // [nown] exception slot + 1, 0 = indexed node
   int* vi_xlist = nullptr;              // [nown] exception slot -> owned node
   unsigned* vi_xcnt = nullptr;          // [node blocks + 1] exception nodes per block, then their exclusive scan
-  double* vi_exc = nullptr;             // [27 x 9][xld] block values, slot fastest (a wave's consecutive slots: coalesced)
+  double* vi_exc = nullptr;             // block values [slot/64][27 x 9][slot%64] (exc_base)
   int64_t vi_exc_bytes = 0;             // allocated bytes of vi_exc
   int64_t vi_nexc = 0;                  // exception nodes of the current matrix
   bool plain_ke = false;                // this assembly formed kref + the non-plain elements' Ke only
@@ -250,6 +255,16 @@ struct Ctx {
   int vi_lg = 2;             // staged block-indexed SpMV, LDS-dictionary waves: blocks whose reads are issued together (option vi_lg: 1, 2, 3)
   int cg_p2d = 0;            // quad-buffered p update on a (rows, x chunks) grid: no per-node divisions (option cg_p2d; A/B)
   int vi_lg_exc = 1;         // vi_lg 2 also in the exception-node kernel (option vi_lg_exc; 0: per-block waits)
+  int vi_st = 1;             // default-stencil SpMV (k_spmv_st + k_spmv_fix, option vi_st; FMA rows, 64 x 16 tiles)
+  double* st_coef = nullptr;            // [243] the default stencil's blocks
+  unsigned* st_ids = nullptr;           // [8] its 7 index words, [7] = center is an exception node
+  unsigned* st_slot = nullptr;          // [nown] list position + 1 of a non-default node, 0 = default
+  int* st_list = nullptr;               // [nown] non-default nodes in owned-node order
+  unsigned* st_cnt = nullptr;           // [node blocks + 1] scan scratch
+  unsigned long long* st_mask = nullptr;  // [nz][npy][npx] 16 x 4 patch masks (bit = leave the lane to k_spmv_fix)
+  int64_t st_mask_bytes = 0, st_n = 0;
+  int st_npx = 0, st_npy = 0;
+  bool st_ok = false;                   // built for the current block indices
   int vi_exc_kernel = 1;     // staged SpMV: exception rows in their own kernel after the march (k_spmv_exc, option
                              // vi_exc_kernel; 0: round 4's block-wide pass in each tile's tail)
   int vi_wdesc = 1;          // staged block-indexed SpMV: wave descriptors (option vi_wdesc): 1 = uniform waves (default since round 5: -2.1 % per CG iteration), 2 = also two-set waves (FMA rows), 0 = per-lane index words
@@ -384,6 +399,8 @@ int64_t node_blocks(const Ctx& c);
 bool vi_staged(const Ctx& c);
 int build_wdesc(Ctx& c);    // wave descriptors of the block-indexed storage (after build_vi)
 bool wd_used(const Ctx& c);  // the staged SpMV reads them
+int build_st(Ctx& c);       // default-stencil SpMV structures (after build_vi)
+bool st_used(const Ctx& c);  // the SpMV runs k_spmv_st + k_spmv_fix
 bool fusep(const Ctx& c);  // the CG's p update runs inside the value-indexed SpMV
 bool cg_pdb(const Ctx& c);  // the CG's p update double-buffered (x every second iteration)
 int64_t cg_vec_bytes_per_node(const Ctx& c);  // the last solve's CG vector kernels, bytes per owned node and iteration

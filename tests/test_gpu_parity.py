@@ -264,6 +264,7 @@ def test_aij_vi_exception_nodes(grid, stage, vi_tx, tile):
         m.set_option("vi_fma", 1)
         y = m.spmv(x)
         assert np.all(np.abs(y - y1) <= 1e-14 * absrow + 1e-300)
+        m.set_option("vi_st", 0)  # the exception rows through k_spmv_exc / the in-tile pass below
         for xk, xl in ((0, 0), (0, 3), (0, 2048), (1, 2048)):
             m.set_option("vi_exc_kernel", xk)
             m.set_option("vi_exc_list", xl)
@@ -271,6 +272,8 @@ def test_aij_vi_exception_nodes(grid, stage, vi_tx, tile):
         m.set_option("vi_lg_exc", 0)  # per-block waits on the LDS path of the exception kernel: the same rows
         assert np.array_equal(m.spmv(x), y)
         m.set_option("vi_lg_exc", 1)
+        m.set_option("vi_st", 1)  # default-stencil kernel: exception nodes among the listed rows
+        assert np.array_equal(m.spmv(x), y)
         its, rn, reason = m.solve_Ax()
         assert reason > 0 and abs(its - ref_its) <= 1
         assert np.linalg.norm(m.du() - P.du()) <= 50 * rtol * np.linalg.norm(P.du())
@@ -726,6 +729,11 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
             yf = m.spmv(x)
             assert np.all(np.abs(yf - y_ref) <= 1e-14 * absrow + 1e-300), zblocks
             assert np.array_equal(m.spmv(x), yf)
+            # the default-stencil kernel (64 x 16 tiles, the default there) and the per-node index
+            # path compute the same FMA rows: bitwise
+            m.set_option("vi_st", 0)
+            assert np.array_equal(m.spmv(x), yf), (zblocks, "vi_st 0")
+            m.set_option("vi_st", 1)
             m.set_option("vi_ypair", 1)
             assert np.array_equal(m.spmv(x), yf), (zblocks, "ypair")
             m.set_option("vi_ypair", 0)

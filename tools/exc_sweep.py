@@ -28,8 +28,10 @@ ap.add_argument("--its", type=int, default=200, help="CG iterations timed per st
 ap.add_argument("--gamma", type=float, default=1e-2, help="shear strain of the plastic slab (yield ~1e-3)")
 a = ap.parse_args()
 G = a.grid
-ARGS = {"aij-vi": ["-dm_mat_type", "aij"], "aij-vi-pass": ["-dm_mat_type", "aij"], "aij-split": ["-dm_mat_type", "aij"],
-        "sbaij": ["-dm_mat_type", "sbaij"]}  # aij-vi-pass: round 4's in-tile exception pass (vi_exc_kernel 0)
+ARGS = {"aij-vi": ["-dm_mat_type", "aij"], "aij-vi-exck": ["-dm_mat_type", "aij"], "aij-vi-pass": ["-dm_mat_type", "aij"],
+        "aij-split": ["-dm_mat_type", "aij"], "sbaij": ["-dm_mat_type", "sbaij"]}
+# aij-vi: the default (default-stencil kernel, exception rows among its listed rows); aij-vi-exck: vi_st 0 with
+# the exception kernel; aij-vi-pass: vi_st 0 with round 4's in-tile exception pass (vi_exc_kernel 0)
 lx = 50.0
 dx = lx / (G - 1)
 i = np.arange(G)
@@ -53,6 +55,7 @@ for frac in [float(f) for f in a.fracs.split(",")]:
             if st.startswith("aij-vi"):
                 m.set_option("vi_exc_max", 1000)
                 m.set_option("vi_exc_kernel", 0 if st == "aij-vi-pass" else 1)
+                m.set_option("vi_st", 1 if st == "aij-vi" else 0)
             elif st == "aij-split":
                 m.set_option("vi_exc_max", 0)
             m.set_u(u)
