@@ -3037,8 +3037,8 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
 // Round 5 (vi_st).  On the block-indexed storage almost every node carries the same 27 block
 // indices: the interior stencil of the uniform grid (at 256^3 all but the ~3 % of nodes on the
 // domain faces, next to Dirichlet nodes, or exception nodes).  The matrix is then held as
-//   * the default stencil: the 27 blocks of one interior node (st_coef, 243 doubles, read by every
-//     wave with scalar loads),
+//   * the default stencil: the 27 blocks of one interior node (st_coef, rows of VIB_STRIDE doubles,
+//     read by every wave with scalar loads),
 //   * a 64-bit mask per 16 x 4 node patch and plane: the lanes whose node is not default (its
 //     index bytes differ, or it is an exception node, or it is outside the domain),
 //   * the list of the non-default nodes (ordered compaction, owned-node order), whose rows come
@@ -3061,6 +3061,7 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
   constexpr int NL = (PLANE + T - 1) / T, R = 4;
   __shared__ double xs[R][PLANE];
   __shared__ double sh[T / 64];
+  __shared__ double s9[27];  // value 8 of the default stencil's blocks
   if (GATED && cg->reason) return;
   const int b = blockIdx.x;
   const int xcd = b & 7, t8 = b >> 3;
@@ -3077,6 +3078,7 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
   const int i0 = txi * TX, j0 = tyi * TY;
   const int k0 = zc * zt.kc, k1 = min(g.nz, k0 + zt.kc);
   const int me = threadIdx.x, wv = me >> 6, ln = me & 63;
+  if (me < 27) s9[me] = coef[me * VIB_STRIDE + 8];
   const int px = wv & 3, py = wv >> 2;  // 16 x 4 patch of the tile (every wave does the same work)
   const int lx = px * 16 + (ln & 15), ly = py * 4 + (ln >> 4);
   const int i = i0 + lx, j = j0 + ly;
@@ -3120,12 +3122,25 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
     }
     double ya0 = 0., ya1 = 0., ya2 = 0., yb0 = 0., yb1 = 0., yb2 = 0.;
     double ca0 = 0., ca1 = 0., ca2 = 0., cb0 = 0., cb1 = 0., cb2 = 0.;
-#pragma unroll
+    // a rolled loop over the 9 stencil rows: unrolled, the compiler hoisted every group's scalar
+    // loads to the top of the step (or out of the plane loop: 486 SGPRs) and spilled
+#pragma unroll 1
     for (int g9 = 0; g9 < 9; g9++) {  // stencil row (dy, dz): blocks nb = 3 g9 .. 3 g9 + 2 (dx = -1, 0, 1)
       const int dy = g9 % 3 - 1, dz = g9 / 3 - 1;
       double av[27], xa[9], xb[9];
+      // the group's 27 values from the scalar cache at every step: an opaque (uniform) zero in the
+      // offset keeps the compiler from hoisting all 243 loop-invariant loads out of the plane loop
+      // (486 SGPRs, spilled to VGPRs and scratch); an opaque pointer instead turned them into flat
+      // vector loads
+      // values 0-7 of each block by one s_load_dwordx16 (coef rows of VIB_STRIDE doubles: 16-B
+      // aligned), value 8 from the LDS copy s9 (a broadcast ds_read_b64): 48 SGPRs per group, as
+      // k_spmv_vibm's scalar path
 #pragma unroll
-      for (int q = 0; q < 27; q++) av[q] = coef[g9 * 27 + q];
+      for (int t = 0; t < 3; t++) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) av[t * 9 + q] = coef[(g9 * 3 + t) * VIB_STRIDE + q];
+        av[t * 9 + 8] = s9[g9 * 3 + t];
+      }
       const int ra = ((k + dz - k0 + 1) & 3) * PLANE + (ly + 1 + dy) * RL + 3 * lx;
       const int rb = ((k + 1 + dz - k0 + 1) & 3) * PLANE + (ly + 1 + dy) * RL + 3 * lx;
 #pragma unroll
@@ -3134,12 +3149,12 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
         xb[q] = xsv[rb + q];
       }
       __builtin_amdgcn_sched_barrier(0);
+      if (g9 == 4) {  // (uniform) block 13: the node's own x
+        ca0 = xa[3], ca1 = xa[4], ca2 = xa[5];
+        cb0 = xb[3], cb1 = xb[4], cb2 = xb[5];
+      }
 #pragma unroll
       for (int t = 0; t < 3; t++) {
-        if (g9 * 3 + t == 13) {
-          ca0 = xa[3], ca1 = xa[4], ca2 = xa[5];
-          cb0 = xb[3], cb1 = xb[4], cb2 = xb[5];
-        }
 #pragma unroll
         for (int q = 0; q < 9; q++) {
           const int r = q / 3, cc = q % 3;
@@ -3249,17 +3264,17 @@ __global__ __launch_bounds__(TPB) void k_spmv_fix(Geo g, const int* __restrict__
 }
 
 // default-stencil build, pass 0 (one block): the 27 blocks of node `center` (its index bytes into
-// the dictionary) as coef[243] and its 7 index words as ids[0..6]; ids[7] = 1 when the node is an
+// the dictionary) as coef[27][VIB_STRIDE] and its 7 index words as ids[0..6]; ids[7] = 1 when the node is an
 // exception node (no default stencil then)
 __global__ void k_st_setup(const u32x4* __restrict__ I, const double* __restrict__ bdict, int center,
                            double* __restrict__ coef, unsigned* __restrict__ ids) {
   const int t = threadIdx.x;
   const u32x4* ip = I + (int64_t)(center >> 6) * (2 * 64) + (center & 63);
   const u32x4 w0 = ip[0], w1 = ip[64];
-  if (t < 243) {
-    const int nb = t / 9, q = t % 9;
+  if (t < 27 * VIB_STRIDE) {  // rows of VIB_STRIDE doubles like the dictionary's
+    const int nb = t / VIB_STRIDE, q = t % VIB_STRIDE;
     const unsigned word = nb < 16 ? w0[nb >> 2] : w1[(nb - 16) >> 2];
-    coef[t] = bdict[((word >> (8 * (nb & 3))) & 255u) * VIB_STRIDE + q];
+    coef[t] = q < 9 ? bdict[((word >> (8 * (nb & 3))) & 255u) * VIB_STRIDE + q] : 0.;
   }
   if (t < 7) ids[t] = t < 4 ? w0[t] : w1[t - 4];
   if (t == 7) ids[7] = w1[3] != 0u ? 1u : 0u;
@@ -5070,12 +5085,12 @@ int build_st(Ctx& c) {
   const int npx = (c.g.nx + 15) / 16, npy = (c.g.ny + 3) / 4;
   const int64_t nwp = (int64_t)npx * npy * c.g.nz;
   if (!c.st_coef) {
-    MCX_HIP(hipMalloc(&c.st_coef, 256 * sizeof(double)));
+    MCX_HIP(hipMalloc(&c.st_coef, 27 * VIB_STRIDE * sizeof(double)));
     MCX_HIP(hipMalloc(&c.st_ids, 8 * sizeof(unsigned)));
     MCX_HIP(hipMalloc(&c.st_slot, c.g.nown * sizeof(unsigned)));
     MCX_HIP(hipMalloc(&c.st_list, c.g.nown * sizeof(int)));
     MCX_HIP(hipMalloc(&c.st_cnt, (node_blocks(c) + 1) * sizeof(unsigned)));
-    c.device_bytes += 256 * 8 + 32 + c.g.nown * 8 + (node_blocks(c) + 1) * 4;
+    c.device_bytes += 27 * VIB_STRIDE * 8 + 32 + c.g.nown * 8 + (node_blocks(c) + 1) * 4;
   }
   if (nwp * 8 > c.st_mask_bytes) {
     if (c.st_mask) {
@@ -5089,7 +5104,7 @@ int build_st(Ctx& c) {
   const u32x4* I = reinterpret_cast<const u32x4*>(c.vi_idx);
   const int center = c.g.nx / 2 + c.g.nx * (c.g.ny / 2 + c.g.ny * (c.g.nz / 2));
   const unsigned nbn = nblk(c.g.nown);
-  hipLaunchKernelGGL(k_st_setup, dim3(1), dim3(256), 0, c.stream, I, c.vi_bdict, center, c.st_coef, c.st_ids);
+  hipLaunchKernelGGL(k_st_setup, dim3(1), dim3(27 * VIB_STRIDE), 0, c.stream, I, c.vi_bdict, center, c.st_coef, c.st_ids);
   hipLaunchKernelGGL(k_st_flag, dim3(nbn), dim3(TPB), 0, c.stream, c.g, I, c.st_ids, c.st_slot, c.st_cnt);
   hipLaunchKernelGGL(k_exc_scan, dim3(1), dim3(1024), 0, c.stream, c.st_cnt, (int)nbn, c.st_cnt + nbn);
   hipLaunchKernelGGL(k_exc_assign, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.st_slot, c.st_list, c.st_cnt);

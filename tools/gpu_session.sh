@@ -38,9 +38,11 @@ run() {  # run NAME TIMEOUT OUTFILE CMD...  (stdout to OUTFILE, stderr to the .l
   fi
 }
 
+idx=0
 for step in "$@"; do
+  idx=$((idx + 1))
   name=${step%%@*}
-  base="gpurun_out/${TAG}_${STAMP}_${name//[:,\/ ]/_}"
+  base="gpurun_out/${TAG}_${STAMP}_${idx}_${name//[:,\/ ]/_}"
   case "$step" in
     suite)
       AMD_LOG_LEVEL=1 run suite 1100 "$base.log" python -u -m pytest tests -m gpu -x -v -s -p no:cacheprovider \
