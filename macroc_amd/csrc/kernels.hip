@@ -1473,7 +1473,8 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
         // all issued before the first use (one round trip, not one per block)
         const int nfast = min(dl.L, 3 * per);
 #ifndef MCX_SPLIT_WALK_GROUPED
-#define MCX_SPLIT_WALK_GROUPED 1  // AIJ-split walk in quad groups (round 5: 44 -> 12 B of spills per lane at 256x4)
+#define MCX_SPLIT_WALK_GROUPED 0  // 1: the AIJ-split walk in quad groups (44 -> 12 B of spills per lane at 256x4, but 3.65 vs
+                                   // 3.58 ms per SpMV at 256^3: profiles/r05d_split_walk_ab.log)
 #endif
 #if MCX_SPLIT_WALK_GROUPED
         // the first 24 corrections in three groups of one quad each: the quad and its x gathers

@@ -13,6 +13,8 @@
 #   pmc            PMC HBM-traffic passes of the headline SpMV (tools/pmc_spmv.sh) + SQ passes (tools/pmc_vibm.sh)
 #   py:<script>    python tools/<script> (an A/B script; its arguments after a second colon, separated
 #                  by @: py:spmv_ab.py:--grid@256)
+#   kprof:<script> the same under rocprofv3 --kernel-trace --stats (per-kernel averages in
+#                  gpurun_out/<TAG>_kprof<step>/)
 # Every step has its own timeout and its own log, named with the step and the box's clock, so a
 # failing attempt is never overwritten by a later one (gpurun merges gpurun_out/ back by name).
 # The session stops at the first failing step: nothing more runs on the GPU after a fault, an abort
@@ -61,6 +63,13 @@ for step in "$@"; do
     rocprof)
       run rocprof 600 "$base.json" rocprofv3 --kernel-trace --stats -d "gpurun_out/${TAG}_prof" -o run \
         --output-format csv -- python3 bench.py --variants '' --config5 0 --bending 0 --cpu-grid 0 ;;
+    kprof:*)  # kprof:<script>:<args @-separated>: the script under rocprofv3 --kernel-trace --stats
+      spec=${step#kprof:}
+      script=${spec%%:*}
+      args=""
+      [ "$spec" != "$script" ] && args=${spec#*:}
+      run "kprof-$script" 600 "$base.log" rocprofv3 --kernel-trace --stats -d "gpurun_out/${TAG}_kprof${idx}" -o run \
+        --output-format csv -- python3 "tools/$script" ${args//@/ } ;;
     pmc)
       run pmc-hbm 600 "$base.log" bash tools/pmc_spmv.sh aij-vi 256
       run pmc-sq 600 "${base}_sq.log" bash tools/pmc_vibm.sh ;;
