@@ -3201,62 +3201,80 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
   }
 }
 
-// The non-default rows of the default-stencil SpMV (k_spmv_st): one thread per listed node, its
-// 27 blocks from its index bytes (dictionary in global memory, 20 KB, cache resident) or, for an
-// exception node, from exc; x gathered from the padded vector; the FMA rows of k_spmv_vibm.
+// The non-default rows of the default-stencil SpMV (k_spmv_st): one thread per listed node (the
+// domain faces, the neighbours of Dirichlet nodes, exception nodes: ~2.3 % of the nodes at 256^3).
+// A first form walked the 9 stencil rows with a global round trip each (dictionary values and x):
+// 92 us at 256^3, latency-bound, next to the march's 232 us (profiles/r05e_kprof*).  Here the
+// dictionary is staged in LDS (20 KB per block), all 81 x values of the node are loaded in one
+// round (162 VGPRs: up to 256 per thread, 2 waves per SIMD), and the 27 blocks are then read from
+// LDS (an exception node: from exc) in the FMA rows' order — y bitwise k_spmv_vibm's.
 template <bool DOT, bool GATED>
-__global__ __launch_bounds__(TPB) void k_spmv_fix(Geo g, const int* __restrict__ list, int64_t cnt,
-                                                  const u32x4* __restrict__ I, const double* __restrict__ bdict,
-                                                  const double* __restrict__ exc, const double* __restrict__ x,
-                                                  double* __restrict__ y, double* __restrict__ part,
-                                                  const CgState* __restrict__ cg) {
+__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 2)))
+void k_spmv_fix(Geo g, const int* __restrict__ list, int64_t cnt, const u32x4* __restrict__ I,
+                const double* __restrict__ bdict, const double* __restrict__ exc, const double* __restrict__ x,
+                double* __restrict__ y, double* __restrict__ part, const CgState* __restrict__ cg) {
+  __shared__ double2 tab[VI_MAX * VIB_STRIDE / 2];
   __shared__ double sh[TPB / 64];
   if (GATED && cg->reason) return;
   const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
-  double dot = 0.;
-  if (t < cnt) {
-    const int n = list[t];
-    int i, j, k;
+  const bool live = t < cnt;
+  int n = 0, i = 0, j = 0, k = 0;
+  u32x4 w0 = {0u, 0u, 0u, 0u}, w1 = w0;
+  if (live) {  // the node's index words first: their latency overlaps the dictionary staging
+    n = list[t];
     node_ijk(g, n, i, j, k);
-    const int PX = g.PX, PXY = g.PX * g.PY;
     const u32x4* ip = I + (int64_t)(n >> 6) * (2 * 64) + (n & 63);
-    const u32x4 w0 = ip[0], w1 = ip[64];
-    const unsigned slot = w1[3];  // exception slot + 1
-    double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
-#pragma unroll 1
-    for (int nb0 = 0; nb0 < 27; nb0 += 3) {
-      double av[27];
+    w0 = ip[0];
+    w1 = ip[64];
+  }
+  for (int q = threadIdx.x; q < VI_MAX * VIB_STRIDE / 2; q += TPB) tab[q] = reinterpret_cast<const double2*>(bdict)[q];
+  double xw[81];  // x of the 27 neighbours: 9 stencil rows of 3 nodes, 9 contiguous doubles each
+  if (live) {
+    const int PX = g.PX, PXY = g.PX * g.PY;
 #pragma unroll
-      for (int t3 = 0; t3 < 3; t3++) {
-        const int nb = nb0 + t3;
-        const unsigned word = nb < 16 ? w0[nb >> 2] : w1[(nb - 16) >> 2];
-        const double* e = slot ? exc + exc_base(slot - 1) + nb * 9 * 64 : bdict + ((word >> (8 * (nb & 3))) & 255u) * VIB_STRIDE;
-        const int es = slot ? 64 : 1;
-#pragma unroll
-        for (int q = 0; q < 9; q++) av[t3 * 9 + q] = e[q * es];
-      }
-      const int dy = (nb0 / 3) % 3 - 1, dz = nb0 / 9 - 1;
+    for (int g9 = 0; g9 < 9; g9++) {
+      const int dy = g9 % 3 - 1, dz = g9 / 3 - 1;
       const double* xr = x + 3 * ((int64_t)i + (j + 1 + dy) * (int64_t)PX + (k + 1 + dz) * (int64_t)PXY);
-      double xw[9];
 #pragma unroll
-      for (int q = 0; q < 9; q++) xw[q] = xr[q];
+      for (int q = 0; q < 9; q++) xw[g9 * 9 + q] = xr[q];
+    }
+  }
+  __syncthreads();
+  double dot = 0.;
+  if (live) {
+    const unsigned slot = w1[3];  // exception slot + 1
+    double y0 = 0., y1 = 0., y2 = 0.;
+    if (slot) {  // rare (a per-GP-tangent law): the node's plain blocks
+      const double* eb = exc + exc_base(slot - 1);
 #pragma unroll
-      for (int t3 = 0; t3 < 3; t3++) {
-        if (nb0 + t3 == 13) {
-          xc0 = xw[3], xc1 = xw[4], xc2 = xw[5];
-        }
+      for (int nb = 0; nb < 27; nb++) {
 #pragma unroll
         for (int q = 0; q < 9; q++) {
           const int r = q / 3, cc = q % 3;
           double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
-          yr = __builtin_fma(av[t3 * 9 + q], xw[3 * t3 + cc], yr);
+          yr = __builtin_fma(eb[(nb * 9 + q) * 64], xw[(nb / 3) * 9 + 3 * (nb % 3) + cc], yr);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int nb = 0; nb < 27; nb++) {
+        const unsigned word = nb < 16 ? w0[nb >> 2] : w1[(nb - 16) >> 2];
+        const double2* e = tab + ((word >> (8 * (nb & 3))) & 255u) * (VIB_STRIDE / 2);
+        const double2 a01 = e[0], a23 = e[1], a45 = e[2], a67 = e[3];
+        const double a[9] = {a01.x, a01.y, a23.x, a23.y, a45.x, a45.y, a67.x, a67.y,
+                             reinterpret_cast<const double*>(e)[8]};
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+          const int r = q / 3, cc = q % 3;
+          double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
+          yr = __builtin_fma(a[q], xw[(nb / 3) * 9 + 3 * (nb % 3) + cc], yr);
         }
       }
     }
     __builtin_nontemporal_store(y0, &y[3 * (int64_t)n + 0]);
     __builtin_nontemporal_store(y1, &y[3 * (int64_t)n + 1]);
     __builtin_nontemporal_store(y2, &y[3 * (int64_t)n + 2]);
-    if (DOT) dot = xc0 * y0 + xc1 * y1 + xc2 * y2;
+    if (DOT) dot = xw[39] * y0 + xw[40] * y1 + xw[41] * y2;  // block 13 (g9 4, dx 0): the node's own x
   }
   if (DOT) {
     const double sm = block_sum<TPB>(dot, sh);
