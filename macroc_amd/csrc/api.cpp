@@ -1623,6 +1623,10 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
     c.cg_p2d = value != 0.;
     return 0;
   }
+  if (!std::strcmp(name, "vi_st_tail")) {
+    c.vi_st_tail = value != 0.;
+    return 0;
+  }
   if (!std::strcmp(name, "vi_st")) {  // takes effect at once if the structures were built (they are by default)
     c.vi_st = value != 0.;
     return 0;

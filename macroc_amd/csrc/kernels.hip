@@ -3052,12 +3052,87 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
 // (nb, c) order), so y is bitwise what k_spmv_vibm computes; a non-default lane's row is left to
 // k_spmv_fix, which computes it from its index bytes (dictionary in global memory) or exception
 // blocks, x gathered, in the same order.  p.w partials: the march's blocks, then k_spmv_fix's.
-template <bool DOT, bool GATED>
+// k_spmv_st TAIL: this block's share of the listed (non-default) rows, in list order, the
+// dictionary staged in tab (the freed ring); x gathered, one stencil row (9 x, 3 blocks) per
+// round; the FMA rows of k_spmv_vibm (an exception node's blocks from exc)
+__device__ __forceinline__ void st_tail(const Geo& g, const int* __restrict__ list, int64_t cnt,
+                                        const u32x4* __restrict__ I, const double* __restrict__ bdict,
+                                        const double* __restrict__ exc, const double* __restrict__ x,
+                                        double* __restrict__ y, double2* tabg, double& dot) {
+  constexpr int T = 1024;
+  if (cnt <= 0) return;  // (uniform)
+  typedef __attribute__((address_space(3))) double2 lds_double2;
+  lds_double2* tab = (lds_double2*)tabg;  // (the ring's LDS: ds_read, not flat loads)
+  const int me = threadIdx.x;
+  for (int q = me; q < VI_MAX * VIB_STRIDE / 2; q += T) tab[q] = reinterpret_cast<const double2*>(bdict)[q];
+  __syncthreads();
+  const int64_t lo = (int64_t)blockIdx.x * cnt / gridDim.x, hi = (int64_t)(blockIdx.x + 1) * cnt / gridDim.x;
+  const int PX = g.PX, PXY = g.PX * g.PY;
+  for (int64_t t = lo + me; t < hi; t += T) {
+    const int n = list[t];
+    int i, j, k;
+    node_ijk(g, n, i, j, k);
+    const u32x4* ip = I + (int64_t)(n >> 6) * (2 * 64) + (n & 63);
+    const u32x4 w0 = ip[0], w1 = ip[64];
+    const unsigned slot = w1[3];  // exception slot + 1
+    const double* eb = exc + exc_base(slot ? slot - 1 : 0);
+    double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+    // a rolled loop over the stencil rows (unrolled, the compiler hoisted the rows' loads and spilled)
+#pragma unroll 1
+    for (int g9 = 0; g9 < 9; g9++) {
+      const int dy = g9 % 3 - 1, dz = g9 / 3 - 1;
+      const double* xr = x + 3 * ((int64_t)i + (j + 1 + dy) * (int64_t)PX + (k + 1 + dz) * (int64_t)PXY);
+      double xw[9], av[27];
+#pragma unroll
+      for (int q = 0; q < 9; q++) xw[q] = xr[q];
+#pragma unroll
+      for (int t3 = 0; t3 < 3; t3++) {
+        const int nb = g9 * 3 + t3;
+        if (slot) {
+#pragma unroll
+          for (int q = 0; q < 9; q++) av[t3 * 9 + q] = eb[(nb * 9 + q) * 64];
+        } else {
+          const int wi = nb >> 2;  // (run-time, uniform): a select chain, not a private array
+          const unsigned word = wi == 0 ? w0[0] : wi == 1 ? w0[1] : wi == 2 ? w0[2] : wi == 3 ? w0[3]
+                              : wi == 4 ? w1[0] : wi == 5 ? w1[1] : w1[2];
+          const lds_double2* e = tab + ((word >> (8 * (nb & 3))) & 255u) * (VIB_STRIDE / 2);
+          const double2 a01 = e[0], a23 = e[1], a45 = e[2], a67 = e[3], a89 = e[4];
+          av[t3 * 9 + 0] = a01.x, av[t3 * 9 + 1] = a01.y, av[t3 * 9 + 2] = a23.x, av[t3 * 9 + 3] = a23.y;
+          av[t3 * 9 + 4] = a45.x, av[t3 * 9 + 5] = a45.y, av[t3 * 9 + 6] = a67.x, av[t3 * 9 + 7] = a67.y;
+          av[t3 * 9 + 8] = a89.x;
+        }
+      }
+      if (g9 == 4) xc0 = xw[3], xc1 = xw[4], xc2 = xw[5];
+#pragma unroll
+      for (int t3 = 0; t3 < 3; t3++)
+#pragma unroll
+        for (int q = 0; q < 9; q++) {
+          const int r = q / 3, cc = q % 3;
+          double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
+          yr = __builtin_fma(av[t3 * 9 + q], xw[3 * t3 + cc], yr);
+        }
+    }
+    __builtin_nontemporal_store(y0, &y[3 * (int64_t)n + 0]);
+    __builtin_nontemporal_store(y1, &y[3 * (int64_t)n + 1]);
+    __builtin_nontemporal_store(y2, &y[3 * (int64_t)n + 2]);
+    dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
+  }
+}
+
+// TAIL (option vi_st_tail, default): the listed rows are computed by the same blocks after their
+// march, each block a fixed share of the list (idle blocks too), with the dictionary staged in the
+// freed x ring: 16 waves per CU hide the gathers' latency that a separate kernel at 2 waves per SIMD
+// exposed (k_spmv_fix: 52 us at 256^3).  Same rows; the listed nodes' p.w terms go to the block's
+// partial.
+template <bool DOT, bool GATED, bool TAIL = false>
 __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restrict__ coef,
                                                   const unsigned long long* __restrict__ mask, int npx, int npy,
                                                   const double* __restrict__ x, double* __restrict__ y,
                                                   double* __restrict__ part, const CgState* __restrict__ cg,
-                                                  ZTiling zt) {
+                                                  ZTiling zt, const int* __restrict__ list = nullptr, int64_t cnt = 0,
+                                                  const u32x4* __restrict__ I = nullptr,
+                                                  const double* __restrict__ bdict = nullptr,
+                                                  const double* __restrict__ exc = nullptr) {
   constexpr int TX = 64, TY = 16, T = TX * TY, RL = vibm_rl<TX, true>(), PR = TY + 2, PLANE = PR * RL;
   constexpr int NL = (PLANE + T - 1) / T, R = 4;
   __shared__ double xs[R][PLANE];
@@ -3070,15 +3145,21 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
   const int ty0 = xcd * slab;
   const int nty_here = min(slab, zt.nty - ty0);
   const int per = max(nty_here, 0) * zt.ntx * zt.nzc;
-  if (t8 >= per) {  // whole block idle (uniform): still write the partial
-    if (DOT && threadIdx.x == 0) part[blockIdx.x] = 0.;
+  const int me = threadIdx.x;
+  double dot = 0.;
+  if (t8 >= per) {  // whole block idle (uniform): the listed rows' share only (TAIL), the partial
+    if (TAIL) st_tail(g, list, cnt, I, bdict, exc, x, y, reinterpret_cast<double2*>(&xs[0][0]), dot);
+    if (DOT) {
+      const double s = block_sum<T>(dot, sh);
+      if (threadIdx.x == 0) part[blockIdx.x] = s;
+    }
     return;
   }
   const int txi = t8 % zt.ntx, r8 = t8 / zt.ntx;
   const int tyi = ty0 + r8 % nty_here, zc = r8 / nty_here;
   const int i0 = txi * TX, j0 = tyi * TY;
   const int k0 = zc * zt.kc, k1 = min(g.nz, k0 + zt.kc);
-  const int me = threadIdx.x, wv = me >> 6, ln = me & 63;
+  const int wv = me >> 6, ln = me & 63;
   if (me < 27) s9[me] = coef[me * VIB_STRIDE + 8];
   const int px = wv & 3, py = wv >> 2;  // 16 x 4 patch of the tile (every wave does the same work)
   const int lx = px * 16 + (ln & 15), ly = py * 4 + (ln >> 4);
@@ -3105,7 +3186,6 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
   __syncthreads();
   typedef const volatile __attribute__((address_space(3))) double lds_vdouble;
   lds_vdouble* xsv = (lds_vdouble*)&xs[0][0];
-  double dot = 0.;
   for (int k = k0; k < k1; k += 2) {
     const bool two = k + 1 < k1, more = k + 2 < k1;
     double xr[2][NL];
@@ -3194,6 +3274,10 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
       }
       __syncthreads();
     }
+  }
+  if (TAIL) {
+    __syncthreads();  // every wave is done with the ring: it holds the dictionary now
+    st_tail(g, list, cnt, I, bdict, exc, x, y, reinterpret_cast<double2*>(&xs[0][0]), dot);
   }
   if (DOT) {
     const double s = block_sum<T>(dot, sh);
@@ -4625,7 +4709,7 @@ bool st_used(const Ctx& c) {
          tx == 64 && !fusep(c);
 }
 
-static int64_t fix_blocks(const Ctx& c) { return st_used(c) ? (c.st_n + TPB - 1) / TPB : 0; }
+static int64_t fix_blocks(const Ctx& c) { return st_used(c) && !c.vi_st_tail ? (c.st_n + TPB - 1) / TPB : 0; }
 
 // the exception rows' kernel (staged block-indexed storage with exception nodes, vi_exc_kernel)
 static int64_t exc_blocks(const Ctx& c) {
@@ -5378,8 +5462,13 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
         double* pf = c.partials + nb;
 #define MCX_ST(DV, GV)                                                                                             \
   do {                                                                                                            \
-    hipLaunchKernelGGL((k_spmv_st<DV, GV>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask, c.st_npx, \
-                       c.st_npy, xpad, y, c.partials, c.cg, zt);                                                  \
+    if (c.vi_st_tail)                                                                                             \
+      hipLaunchKernelGGL((k_spmv_st<DV, GV, true>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,   \
+                         c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt, c.st_list, c.st_n, I, c.vi_bdict,     \
+                         c.vi_exc);                                                                               \
+    else                                                                                                          \
+      hipLaunchKernelGGL((k_spmv_st<DV, GV>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,         \
+                         c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);                                      \
     if (nbf)                                                                                                      \
       hipLaunchKernelGGL((k_spmv_fix<DV, GV>), dim3((unsigned)nbf), dim3(TPB), 0, c.stream, c.g, c.st_list, c.st_n, \
                          I, c.vi_bdict, c.vi_exc, xpad, y, pf, c.cg);                                             \

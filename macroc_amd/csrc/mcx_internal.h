@@ -256,6 +256,7 @@ struct Ctx {
   int cg_p2d = 0;            // quad-buffered p update on a (rows, x chunks) grid: no per-node divisions (option cg_p2d; A/B)
   int vi_lg_exc = 1;         // vi_lg 2 also in the exception-node kernel (option vi_lg_exc; 0: per-block waits)
   int vi_st = 1;             // default-stencil SpMV (k_spmv_st + k_spmv_fix, option vi_st; FMA rows, 64 x 16 tiles)
+  int vi_st_tail = 1;        // its listed rows in the same blocks after the march (option vi_st_tail; 0: k_spmv_fix)
   double* st_coef = nullptr;            // [27][VIB_STRIDE] the default stencil's blocks
   unsigned* st_ids = nullptr;           // [8] its 7 index words, [7] = center is an exception node
   unsigned* st_slot = nullptr;          // [nown] list position + 1 of a non-default node, 0 = default

@@ -734,6 +734,9 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
             m.set_option("vi_st", 0)
             assert np.array_equal(m.spmv(x), yf), (zblocks, "vi_st 0")
             m.set_option("vi_st", 1)
+            m.set_option("vi_st_tail", 0)  # the listed rows by k_spmv_fix instead of the march blocks' tail
+            assert np.array_equal(m.spmv(x), yf), (zblocks, "vi_st_tail 0")
+            m.set_option("vi_st_tail", 1)
             m.set_option("vi_ypair", 1)
             assert np.array_equal(m.spmv(x), yf), (zblocks, "ypair")
             m.set_option("vi_ypair", 0)

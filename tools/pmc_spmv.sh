@@ -7,7 +7,7 @@ set -euo pipefail
 MAT=${1:-aij-split}
 G=${2:-256}
 case $MAT in
-  aij-vi) RE='k_spmv_vib'; BM=aij ;;
+  aij-vi) RE='k_spmv_vib|k_spmv_st'; BM=aij ;;  # value-indexed: k_spmv_vibm, or the default-stencil k_spmv_st (vi_st)
   aij-split) RE='k_spmv_symp'; BM=aij-split ;;
   aij-blocks) RE='k_spmv<'; BM=aij-blocks ;;
   sbaij) RE='k_spmv_sym'; BM=sbaij ;;
