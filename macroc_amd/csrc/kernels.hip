@@ -3061,10 +3061,10 @@ __device__ __forceinline__ void st_tail(const Geo& g, const int* __restrict__ li
                                         double* __restrict__ y, double2* tabg, double& dot) {
   constexpr int T = 1024;
   if (cnt <= 0) return;  // (uniform)
-  typedef __attribute__((address_space(3))) double2 lds_double2;
-  lds_double2* tab = (lds_double2*)tabg;  // (the ring's LDS: ds_read, not flat loads)
+  typedef __attribute__((address_space(3))) double lds_double;
+  lds_double* tab = (lds_double*)tabg;  // (the ring's LDS: ds_read, not flat loads)
   const int me = threadIdx.x;
-  for (int q = me; q < VI_MAX * VIB_STRIDE / 2; q += T) tab[q] = reinterpret_cast<const double2*>(bdict)[q];
+  for (int q = me; q < VI_MAX * VIB_STRIDE; q += T) tab[q] = bdict[q];
   __syncthreads();
   const int64_t lo = (int64_t)blockIdx.x * cnt / gridDim.x, hi = (int64_t)(blockIdx.x + 1) * cnt / gridDim.x;
   const int PX = g.PX, PXY = g.PX * g.PY;
@@ -3095,11 +3095,9 @@ __device__ __forceinline__ void st_tail(const Geo& g, const int* __restrict__ li
           const int wi = nb >> 2;  // (run-time, uniform): a select chain, not a private array
           const unsigned word = wi == 0 ? w0[0] : wi == 1 ? w0[1] : wi == 2 ? w0[2] : wi == 3 ? w0[3]
                               : wi == 4 ? w1[0] : wi == 5 ? w1[1] : w1[2];
-          const lds_double2* e = tab + ((word >> (8 * (nb & 3))) & 255u) * (VIB_STRIDE / 2);
-          const double2 a01 = e[0], a23 = e[1], a45 = e[2], a67 = e[3], a89 = e[4];
-          av[t3 * 9 + 0] = a01.x, av[t3 * 9 + 1] = a01.y, av[t3 * 9 + 2] = a23.x, av[t3 * 9 + 3] = a23.y;
-          av[t3 * 9 + 4] = a45.x, av[t3 * 9 + 5] = a45.y, av[t3 * 9 + 6] = a67.x, av[t3 * 9 + 7] = a67.y;
-          av[t3 * 9 + 8] = a89.x;
+          const lds_double* e = tab + ((word >> (8 * (nb & 3))) & 255u) * VIB_STRIDE;
+#pragma unroll
+          for (int q = 0; q < 9; q++) av[t3 * 9 + q] = e[q];
         }
       }
       if (g9 == 4) xc0 = xw[3], xc1 = xw[4], xc2 = xw[5];
