@@ -61,11 +61,16 @@ KERNEL_NAME = {0: "k_spmv (AIJ stencil blocks, CPU AIJ row order)",
                      "from scalar loads, others from the dictionary in LDS; 16x4-node waves; rows summed with fused "
                      "multiply-adds)",
                "3be": "k_spmv_vibm (block-indexed AIJ as above, -mat_vi_fma 0: multiply then add in the CPU AIJ "
-                      "row order, bit-exact)"}
+                      "row order, bit-exact)",
+               "3bs": "k_spmv_st (block-indexed AIJ, default-stencil path: the interior stencil's blocks from scalar "
+                      "loads, two z-planes per step, x ring in LDS, no index bytes; the listed non-default rows from "
+                      "their index bytes in the same blocks after the march; rows summed with fused multiply-adds)"}
 
 
 def kernel_name(r):
     if r["storage_id"] == 3 and r["vi_blocks"]:
+        if r.get("st_listed", -1) >= 0:
+            return KERNEL_NAME["3bs"]
         return KERNEL_NAME["3be" if r.get("exact") else "3b"]
     return KERNEL_NAME[r["storage_id"]]
 
@@ -299,6 +304,7 @@ def measure(argv, rank, world, comm_id, args, steps, warmup):
             "csr_bytes": csr_bytes, "storage": STORAGE_NAME[storage["storage"]], "storage_id": storage["storage"],
             "split_slots": storage["split_slots"], "split_bits": storage["split_bits"],
             "vi_values": storage["vi_values"], "vi_bits": storage["vi_bits"], "vi_blocks": storage["vi_blocks"],
+            "st_listed": storage["st_listed"],
             "achieved": spmv_bytes / (spmv_avg_ms * 1e-3) / 1e9, "ms_step": dt / max(steps, 1) * 1e3,
             "warmup_s": t_warm}
 
@@ -473,6 +479,7 @@ def main():
                        "mat_type": "aij" if args.mat_type.startswith("aij") else "sbaij", "storage": r["storage"],
                        "split_slots": r["split_slots"], "split_bits": r["split_bits"],
                        "vi_values": r["vi_values"], "vi_bits": r["vi_bits"], "vi_blocks": r["vi_blocks"],
+                       "st_listed": r["st_listed"],
                        "spmv_rows": "fused multiply-add (-mat_vi_fma 1)" if r["storage_id"] == 3 and not r["exact"]
                        else "multiply, add (MatMult inode order)"},
             "cg_its": its,

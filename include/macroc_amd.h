@@ -151,6 +151,9 @@ typedef struct {
                                    tangent differs from the law's reference tangent) */
   int64_t split_escapes;        /* AIJ-split with dense bf16 corrections: corrections not exact in bf16, kept as
                                    their bf16 hi plus an exact double residual (0 otherwise) */
+  int64_t st_listed;            /* value-indexed AIJ through the default-stencil SpMV: owned nodes whose 27 blocks
+                                   differ from the default (interior) stencil's, computed from their own index
+                                   bytes or exception blocks; -1 when the SpMV does not take that path */
 } mcx_info;
 
 typedef struct {

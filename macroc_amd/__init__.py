@@ -77,7 +77,7 @@ class Info(C.Structure):
         ("nez", C.c_int64),
         ("vi_values", C.c_int), ("vi_bits", C.c_int), ("vi_blocks", C.c_int),
         ("spmv_tx", C.c_int), ("spmv_ty", C.c_int), ("spmv_kc", C.c_int),
-        ("vi_exc_nodes", C.c_int64), ("split_escapes", C.c_int64),
+        ("vi_exc_nodes", C.c_int64), ("split_escapes", C.c_int64), ("st_listed", C.c_int64),
     ]
 
     def as_dict(self):

@@ -576,6 +576,7 @@ static void fill_info(const Ctx& c, mcx_info* in) {
   in->vi_blocks = c.fmt == FMT_VI && c.vi_block ? c.vi_nblocks : 0;
   in->vi_exc_nodes = c.fmt == FMT_VI && c.vi_block ? c.vi_nexc : 0;
   in->split_escapes = c.fmt == FMT_SPLIT && c.dsl.esc ? c.dsl.nesc : 0;
+  in->st_listed = c.device >= 0 && st_used(c) ? c.st_n : -1;
   if (c.device >= 0) spmv_tile(c, &in->spmv_tx, &in->spmv_ty, &in->spmv_kc);
   in->ex0 = g.ex0;
   in->ey0 = g.ey0;
