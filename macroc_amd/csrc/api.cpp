@@ -1624,12 +1624,21 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
     c.cg_p2d = value != 0.;
     return 0;
   }
+  if (!std::strcmp(name, "vi_st_faces")) {  // rebuilds the default-stencil structures if built
+    c.vi_st_faces = (int)value & 0x7f;  // 1: all 6 faces; else bit c = face class c (1..6)
+    if (c.st_ok && build_st(c)) return 1;
+    return 0;
+  }
   if (!std::strcmp(name, "vi_st_tail")) {
     c.vi_st_tail = value != 0.;
     return 0;
   }
   if (!std::strcmp(name, "vi_st")) {  // takes effect at once if the structures were built (they are by default)
-    c.vi_st = value != 0.;
+    if (!(value == -1. || value == 0. || value == 1.)) {
+      set_error("vi_st: -1 (by size), 0 or 1");
+      return 1;
+    }
+    c.vi_st = (int)value;
     return 0;
   }
   if (!std::strcmp(name, "vi_exc_kernel")) {

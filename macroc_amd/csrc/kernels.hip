@@ -3055,18 +3055,17 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
 // k_spmv_st TAIL: this block's share of the listed (non-default) rows, in list order, the
 // dictionary staged in tab (the freed ring); x gathered, one stencil row (9 x, 3 blocks) per
 // round; the FMA rows of k_spmv_vibm (an exception node's blocks from exc)
-__device__ __forceinline__ void st_tail(const Geo& g, const int* __restrict__ list, int64_t cnt,
+template <int T>
+__device__ __forceinline__ void st_tail(const Geo& g, const int* __restrict__ list, int64_t lo, int64_t hi,
                                         const u32x4* __restrict__ I, const double* __restrict__ bdict,
                                         const double* __restrict__ exc, const double* __restrict__ x,
                                         double* __restrict__ y, double2* tabg, double& dot) {
-  constexpr int T = 1024;
-  if (cnt <= 0) return;  // (uniform)
   typedef __attribute__((address_space(3))) double lds_double;
   lds_double* tab = (lds_double*)tabg;  // (the ring's LDS: ds_read, not flat loads)
   const int me = threadIdx.x;
+  if (lo >= hi) return;  // (uniform) no share: no dictionary staging
   for (int q = me; q < VI_MAX * VIB_STRIDE; q += T) tab[q] = bdict[q];
   __syncthreads();
-  const int64_t lo = (int64_t)blockIdx.x * cnt / gridDim.x, hi = (int64_t)(blockIdx.x + 1) * cnt / gridDim.x;
   const int PX = g.PX, PXY = g.PX * g.PY;
   for (int64_t t = lo + me; t < hi; t += T) {
     const int n = list[t];
@@ -3117,6 +3116,139 @@ __device__ __forceinline__ void st_tail(const Geo& g, const int* __restrict__ li
   }
 }
 
+// The face phase: the domain faces' nodes of a usable stencil class (k_st_setup) in patches of 64
+// nodes along the face's fast axis (x-faces: j; y- and z-faces: i) x 4 along its slow axis, 256
+// threads each.  The patch's x is staged in LDS first (SFP_N doubles: 9-double chunks (i-1 .. i+1)
+// of the 66 x 6 neighbour grid for an x-face, 198-double row segments (66 nodes) for y- and
+// z-faces, loaded in address order -- an x-face node's rows are PX apart, so gathered per lane
+// they cost a cache line each), then a thread's node takes the class's 27 blocks from the scalar
+// cache (the patch's class is uniform) and its x from LDS in the FMA rows' order of k_spmv_vibm, so
+// y is bitwise the same.  A face node that is listed (slot != 0: an edge node, next to a Dirichlet
+// node, an exception node, or not its class's stencil) is left to the listed rows.
+constexpr int SFP_N = 66 * 6 * 9;  // staged doubles per patch (= 6 * 3 * 198 = 3 * 6 * 198)
+
+struct SfPatch {  // patch p's class, axis, side and origin
+  int c, ax, f0, s0;
+  bool hi;
+};
+
+__device__ __forceinline__ SfPatch sf_patch(const Geo& g, const StFaces& sf, int64_t p) {
+  SfPatch q;
+  q.c = 1;
+  while (q.c < 6 && p >= sf.u[q.c]) q.c++;
+  q.ax = (q.c - 1) >> 1;
+  q.hi = !(q.c & 1);
+  const int fb = ((q.ax == 0 ? g.ny : g.nx) + 63) >> 6;
+  const int64_t lp = p - sf.u[q.c - 1];
+  q.s0 = (int)(lp / fb) * 4;
+  q.f0 = (int)(lp - (int64_t)(q.s0 / 4) * fb) * 64;
+  return q;
+}
+
+// stage patch q's x into S (t = 0 .. 255: the patch's threads)
+__device__ __forceinline__ void sf_stage(const Geo& g, const SfPatch& q, const double* __restrict__ x, double* S,
+                                         int t) {
+  const int PX = g.PX, PXY = g.PX * g.PY;
+  const int iface = q.hi ? g.nx - 1 : 0, jface = q.hi ? g.ny - 1 : 0, kface = q.hi ? g.nz - 1 : 0;
+  constexpr int NE = (SFP_N + 255) / 256;
+  double v[NE];  // all loads in flight before the LDS stores (a load-store round trip each: 14 HBM latencies)
+#pragma unroll
+  for (int m = 0; m < NE; m++) {
+    const int e = t + m * 256;
+    int pi, jp, kp, o;  // padded column of the chunk / segment start, local j', k', offset
+    bool ok;
+    if (q.ax == 0) {  // 9-double chunks, (kk, jj) of 6 x 66
+      const int ch = e / 9, jj = ch % 66;
+      o = e - ch * 9;
+      pi = iface;
+      jp = q.f0 - 1 + jj;
+      kp = q.s0 - 1 + ch / 66;
+      ok = e < SFP_N && jp <= g.ny && kp <= g.nz;
+    } else {  // 198-double segments: y-face (kk, dy) of 6 x 3, z-face (dz, jj) of 3 x 6
+      const int r = e / 198;
+      o = e - r * 198;
+      pi = q.f0;
+      if (q.ax == 1) jp = jface - 1 + r % 3, kp = q.s0 - 1 + r / 3;
+      else jp = q.s0 - 1 + r % 6, kp = kface - 1 + r / 6;
+      ok = e < SFP_N && o < 3 * (g.nx + 2 - q.f0) && jp <= g.ny && kp <= g.nz;
+    }
+    v[m] = ok ? x[3 * ((int64_t)pi + (jp + 1) * (int64_t)PX + (kp + 1) * (int64_t)PXY) + o] : 0.;
+  }
+#pragma unroll
+  for (int m = 0; m < NE; m++)
+    if (t + m * 256 < SFP_N) S[t + m * 256] = v[m];
+}
+
+// the rows of patch q's nodes from S (after a barrier)
+__device__ __forceinline__ void sf_rows(const Geo& g, const SfPatch& q, const double* __restrict__ coef,
+                                        const unsigned* __restrict__ slot, const double* S, double* __restrict__ y,
+                                        double& dot, int t) {
+  typedef const __attribute__((address_space(3))) double lds_double;
+  lds_double* Sl = (lds_double*)S;
+  const int w = t >> 6, ln = t & 63;
+  const int nfast = q.ax == 0 ? g.ny : g.nx, nslow = q.ax == 2 ? g.ny : g.nz;
+  const int f = q.f0 + ln, sl = q.s0 + w;
+  const int i = q.ax == 0 ? (q.hi ? g.nx - 1 : 0) : f;
+  const int j = q.ax == 0 ? f : (q.ax == 1 ? (q.hi ? g.ny - 1 : 0) : sl);
+  const int k = q.ax == 2 ? (q.hi ? g.nz - 1 : 0) : sl;
+  const bool in = f < nfast && sl < nslow;
+  const int64_t n = in ? i + g.nx * (j + (int64_t)g.ny * k) : 0;
+  const bool live = in && slot[n] == 0u;
+  const double* cf = coef + q.c * 27 * VIB_STRIDE;  // (uniform) the class's stencil
+  double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+  // a rolled loop over the stencil rows (unrolled, the compiler hoists the rows' scalar loads and spills)
+#pragma unroll 1
+  for (int g9 = 0; g9 < 9; g9++) {
+    const int dy = g9 % 3 - 1, dz = g9 / 3 - 1;
+    const int base = q.ax == 0 ? ((w + 1 + dz) * 66 + (ln + 1 + dy)) * 9
+                   : q.ax == 1 ? ((w + 1 + dz) * 3 + (dy + 1)) * 198 + 3 * ln
+                               : ((dz + 1) * 6 + (w + 1 + dy)) * 198 + 3 * ln;
+    double xw[9], av[27];
+#pragma unroll
+    for (int qq = 0; qq < 9; qq++) xw[qq] = Sl[base + qq];
+#pragma unroll
+    for (int t3 = 0; t3 < 3; t3++)
+#pragma unroll
+      for (int qq = 0; qq < 9; qq++) av[t3 * 9 + qq] = cf[(g9 * 3 + t3) * VIB_STRIDE + qq];
+    if (g9 == 4) xc0 = xw[3], xc1 = xw[4], xc2 = xw[5];
+#pragma unroll
+    for (int t3 = 0; t3 < 3; t3++)
+#pragma unroll
+      for (int qq = 0; qq < 9; qq++) {
+        const int r = qq / 3, cc = qq % 3;
+        double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
+        yr = __builtin_fma(av[t3 * 9 + qq], xw[3 * t3 + cc], yr);
+      }
+  }
+  if (live) {
+    __builtin_nontemporal_store(y0, &y[3 * n + 0]);
+    __builtin_nontemporal_store(y1, &y[3 * n + 1]);
+    __builtin_nontemporal_store(y2, &y[3 * n + 2]);
+    dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
+  }
+}
+
+// a 1024-thread block's share of the patches [b P / nb, (b+1) P / nb), 4 at a time (a quarter
+// block each, S: 4 SFP_N doubles); every thread takes part in every barrier
+__device__ __forceinline__ void st_faces(const Geo& g, const StFaces& sf, const double* __restrict__ coef,
+                                         const unsigned* __restrict__ slot, const double* __restrict__ x,
+                                         double* __restrict__ y, double& dot, double* S) {
+  const int64_t P = sf.u[6], lo = (int64_t)blockIdx.x * P / gridDim.x, hi = (int64_t)(blockIdx.x + 1) * P / gridDim.x;
+  const int q4 = threadIdx.x >> 8, t = threadIdx.x & 255;
+  for (int64_t p0 = lo; p0 < hi; p0 += 4) {  // (uniform)
+    const int64_t p = p0 + q4;
+    const bool has = p < hi;
+    SfPatch q{};
+    if (has) {
+      q = sf_patch(g, sf, p);
+      sf_stage(g, q, x, S + q4 * SFP_N, t);
+    }
+    __syncthreads();
+    if (has) sf_rows(g, q, coef, slot, S + q4 * SFP_N, y, dot, t);
+    __syncthreads();
+  }
+}
+
 // TAIL (option vi_st_tail, default): the listed rows are computed by the same blocks after their
 // march, each block a fixed share of the list (idle blocks too), with the dictionary staged in the
 // freed x ring: 16 waves per CU hide the gathers' latency that a separate kernel at 2 waves per SIMD
@@ -3130,7 +3262,8 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
                                                   ZTiling zt, const int* __restrict__ list = nullptr, int64_t cnt = 0,
                                                   const u32x4* __restrict__ I = nullptr,
                                                   const double* __restrict__ bdict = nullptr,
-                                                  const double* __restrict__ exc = nullptr) {
+                                                  const double* __restrict__ exc = nullptr,
+                                                  const unsigned* __restrict__ slot = nullptr, StFaces sf = {}) {
   constexpr int TX = 64, TY = 16, T = TX * TY, RL = vibm_rl<TX, true>(), PR = TY + 2, PLANE = PR * RL;
   constexpr int NL = (PLANE + T - 1) / T, R = 4;
   __shared__ double xs[R][PLANE];
@@ -3146,7 +3279,11 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
   const int me = threadIdx.x;
   double dot = 0.;
   if (t8 >= per) {  // whole block idle (uniform): the listed rows' share only (TAIL), the partial
-    if (TAIL) st_tail(g, list, cnt, I, bdict, exc, x, y, reinterpret_cast<double2*>(&xs[0][0]), dot);
+    if (TAIL) {
+      st_faces(g, sf, coef, slot, x, y, dot, &xs[0][0]);
+      st_tail<T>(g, list, (int64_t)b * cnt / gridDim.x, (int64_t)(b + 1) * cnt / gridDim.x, I, bdict, exc, x, y,
+                 reinterpret_cast<double2*>(&xs[0][0]), dot);
+    }
     if (DOT) {
       const double s = block_sum<T>(dot, sh);
       if (threadIdx.x == 0) part[blockIdx.x] = s;
@@ -3274,8 +3411,10 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
     }
   }
   if (TAIL) {
-    __syncthreads();  // every wave is done with the ring: it holds the dictionary now
-    st_tail(g, list, cnt, I, bdict, exc, x, y, reinterpret_cast<double2*>(&xs[0][0]), dot);
+    __syncthreads();  // every wave is done with the ring: it holds the face patches' x, then the dictionary
+    st_faces(g, sf, coef, slot, x, y, dot, &xs[0][0]);
+    st_tail<T>(g, list, (int64_t)b * cnt / gridDim.x, (int64_t)(b + 1) * cnt / gridDim.x, I, bdict, exc, x, y,
+               reinterpret_cast<double2*>(&xs[0][0]), dot);
   }
   if (DOT) {
     const double s = block_sum<T>(dot, sh);
@@ -3283,117 +3422,137 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
   }
 }
 
-// The non-default rows of the default-stencil SpMV (k_spmv_st): one thread per listed node (the
-// domain faces, the neighbours of Dirichlet nodes, exception nodes: ~2.3 % of the nodes at 256^3).
-// A first form walked the 9 stencil rows with a global round trip each (dictionary values and x):
-// 92 us at 256^3, latency-bound, next to the march's 232 us (profiles/r05e_kprof*).  Here the
-// dictionary is staged in LDS (20 KB per block), all 81 x values of the node are loaded in one
-// round (162 VGPRs: up to 256 per thread, 2 waves per SIMD), and the 27 blocks are then read from
-// LDS (an exception node: from exc) in the FMA rows' order — y bitwise k_spmv_vibm's.
+// the face phase and the listed rows as a kernel of their own (vi_st_tail 0): blocks [0, P) one face
+// patch each, then 256 listed rows per block (the dictionary staged in the patch's LDS)
 template <bool DOT, bool GATED>
-__global__ __launch_bounds__(TPB) __attribute__((amdgpu_waves_per_eu(1, 2)))
-void k_spmv_fix(Geo g, const int* __restrict__ list, int64_t cnt, const u32x4* __restrict__ I,
-                const double* __restrict__ bdict, const double* __restrict__ exc, const double* __restrict__ x,
-                double* __restrict__ y, double* __restrict__ part, const CgState* __restrict__ cg) {
-  __shared__ double2 tab[VI_MAX * VIB_STRIDE / 2];
-  __shared__ double sh[TPB / 64];
+__global__ __launch_bounds__(256) void k_spmv_face(Geo g, StFaces sf, const double* __restrict__ coef,
+                                                   const unsigned* __restrict__ slot, const double* __restrict__ x,
+                                                   double* __restrict__ y, double* __restrict__ part,
+                                                   const CgState* __restrict__ cg, const int* __restrict__ list,
+                                                   int64_t cnt, const u32x4* __restrict__ I,
+                                                   const double* __restrict__ bdict, const double* __restrict__ exc) {
+  static_assert(SFP_N >= VI_MAX * VIB_STRIDE, "the dictionary fits the patch's LDS");
+  __shared__ __attribute__((aligned(16))) double S[SFP_N];
+  __shared__ double sh[4];
   if (GATED && cg->reason) return;
-  const int64_t t = (int64_t)blockIdx.x * TPB + threadIdx.x;
-  const bool live = t < cnt;
-  int n = 0, i = 0, j = 0, k = 0;
-  u32x4 w0 = {0u, 0u, 0u, 0u}, w1 = w0;
-  if (live) {  // the node's index words first: their latency overlaps the dictionary staging
-    n = list[t];
-    node_ijk(g, n, i, j, k);
-    const u32x4* ip = I + (int64_t)(n >> 6) * (2 * 64) + (n & 63);
-    w0 = ip[0];
-    w1 = ip[64];
-  }
-  for (int q = threadIdx.x; q < VI_MAX * VIB_STRIDE / 2; q += TPB) tab[q] = reinterpret_cast<const double2*>(bdict)[q];
-  double xw[81];  // x of the 27 neighbours: 9 stencil rows of 3 nodes, 9 contiguous doubles each
-  if (live) {
-    const int PX = g.PX, PXY = g.PX * g.PY;
-#pragma unroll
-    for (int g9 = 0; g9 < 9; g9++) {
-      const int dy = g9 % 3 - 1, dz = g9 / 3 - 1;
-      const double* xr = x + 3 * ((int64_t)i + (j + 1 + dy) * (int64_t)PX + (k + 1 + dz) * (int64_t)PXY);
-#pragma unroll
-      for (int q = 0; q < 9; q++) xw[g9 * 9 + q] = xr[q];
-    }
-  }
-  __syncthreads();
   double dot = 0.;
-  if (live) {
-    const unsigned slot = w1[3];  // exception slot + 1
-    double y0 = 0., y1 = 0., y2 = 0.;
-    if (slot) {  // rare (a per-GP-tangent law): the node's plain blocks
-      const double* eb = exc + exc_base(slot - 1);
-#pragma unroll
-      for (int nb = 0; nb < 27; nb++) {
-#pragma unroll
-        for (int q = 0; q < 9; q++) {
-          const int r = q / 3, cc = q % 3;
-          double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
-          yr = __builtin_fma(eb[(nb * 9 + q) * 64], xw[(nb / 3) * 9 + 3 * (nb % 3) + cc], yr);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int nb = 0; nb < 27; nb++) {
-        const unsigned word = nb < 16 ? w0[nb >> 2] : w1[(nb - 16) >> 2];
-        const double2* e = tab + ((word >> (8 * (nb & 3))) & 255u) * (VIB_STRIDE / 2);
-        const double2 a01 = e[0], a23 = e[1], a45 = e[2], a67 = e[3];
-        const double a[9] = {a01.x, a01.y, a23.x, a23.y, a45.x, a45.y, a67.x, a67.y,
-                             reinterpret_cast<const double*>(e)[8]};
-#pragma unroll
-        for (int q = 0; q < 9; q++) {
-          const int r = q / 3, cc = q % 3;
-          double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
-          yr = __builtin_fma(a[q], xw[(nb / 3) * 9 + 3 * (nb % 3) + cc], yr);
-        }
-      }
-    }
-    __builtin_nontemporal_store(y0, &y[3 * (int64_t)n + 0]);
-    __builtin_nontemporal_store(y1, &y[3 * (int64_t)n + 1]);
-    __builtin_nontemporal_store(y2, &y[3 * (int64_t)n + 2]);
-    if (DOT) dot = xw[39] * y0 + xw[40] * y1 + xw[41] * y2;  // block 13 (g9 4, dx 0): the node's own x
+  const int64_t P = sf.u[6];
+  if ((int64_t)blockIdx.x < P) {
+    const SfPatch q = sf_patch(g, sf, blockIdx.x);
+    sf_stage(g, q, x, S, threadIdx.x);
+    __syncthreads();
+    sf_rows(g, q, coef, slot, S, y, dot, threadIdx.x);
+  } else {
+    const int64_t lo = ((int64_t)blockIdx.x - P) * 256;
+    st_tail<256>(g, list, lo, min(cnt, lo + 256), I, bdict, exc, x, y, reinterpret_cast<double2*>(S), dot);
   }
   if (DOT) {
-    const double sm = block_sum<TPB>(dot, sh);
+    const double sm = block_sum<256>(dot, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = sm;
   }
 }
 
-// default-stencil build, pass 0 (one block): the 27 blocks of node `center` (its index bytes into
-// the dictionary) as coef[27][VIB_STRIDE] and its 7 index words as ids[0..6]; ids[7] = 1 when the node is an
-// exception node (no default stencil then)
-__global__ void k_st_setup(const u32x4* __restrict__ I, const double* __restrict__ bdict, int center,
-                           double* __restrict__ coef, unsigned* __restrict__ ids) {
-  const int t = threadIdx.x;
-  const u32x4* ip = I + (int64_t)(center >> 6) * (2 * 64) + (center & 63);
-  const u32x4 w0 = ip[0], w1 = ip[64];
-  if (t < 27 * VIB_STRIDE) {  // rows of VIB_STRIDE doubles like the dictionary's
-    const int nb = t / VIB_STRIDE, q = t % VIB_STRIDE;
-    const unsigned word = nb < 16 ? w0[nb >> 2] : w1[(nb - 16) >> 2];
-    coef[t] = q < 9 ? bdict[((word >> (8 * (nb & 3))) & 255u) * VIB_STRIDE + q] : 0.;
-  }
-  if (t < 7) ids[t] = t < 4 ? w0[t] : w1[t - 4];
-  if (t == 7) ids[7] = w1[3] != 0u ? 1u : 0u;
+// Stencil classes of the default-stencil SpMV: 0 the interior (marched), 1/2 the x-lo/x-hi domain
+// face, 3/4 y-lo/y-hi, 5/6 z-lo/z-hi (an owned node on exactly one face of the GLOBAL domain: the
+// face phase st_faces; a node on two or three is an edge / corner node and always listed).  On the
+// uniform grid almost every node of a face has the same 27 block indices (its far-side blocks the
+// zero block the DMDA's clipping leaves).
+__device__ __forceinline__ int st_class(const Geo& g, int i, int j, int k, int& nf) {
+  const bool xl = g.xs == 0 && i == 0, xh = g.xs + g.nx == g.NX && i == g.nx - 1;
+  const bool yl = g.ys == 0 && j == 0, yh = g.ys + g.ny == g.NY && j == g.ny - 1;
+  const bool zl = g.zs == 0 && k == 0, zh = g.zs + g.nz == g.NZ && k == g.nz - 1;
+  nf = (int)(xl || xh) + (int)(yl || yh) + (int)(zl || zh) + (int)(xl && xh) + (int)(yl && yh) + (int)(zl && zh);
+  return xl ? 1 : xh ? 2 : yl ? 3 : yh ? 4 : zl ? 5 : zh ? 6 : 0;
 }
 
-// pass 1: flag[n] = 1 for a node whose index words differ from the default's or that is an
-// exception node; cnt[block] = the block's count (then k_exc_scan / k_exc_assign: list in
-// owned-node order, flag -> slot + 1)
+// block nb's index byte in the node's index words
+__device__ __forceinline__ unsigned st_byte(const unsigned* w, int nb) { return (w[nb >> 2] >> (8 * (nb & 3))) & 255u; }
+
+// default-stencil build, pass 0 (one block per class c): the class's representative node -- of up to
+// 5 candidates spread over the class's nodes (not exception nodes, on exactly the class's face), the
+// one whose index words the most candidates share (the interior: the middle node first; a face: its
+// middle and 2 nodes in from its corners, away from Dirichlet edges and load patches) -- its 27 blocks
+// as coef[c][27][VIB_STRIDE], its 7 index words as ids[8 c + 0..6] and ids[8 c + 7] = 1 when the
+// class is usable: it has a representative (a face: and option vi_st_faces is on).  ids[7] = 0: no
+// default stencil at all.
+__global__ __launch_bounds__(320) void k_st_setup(Geo g, const u32x4* __restrict__ I, const double* __restrict__ bdict,
+                                                  double* __restrict__ coef, unsigned* __restrict__ ids, int faces) {
+  __shared__ unsigned wsel[2][8];  // [0] the interior's words, [1] this class's; [.][7] = found
+  const int c = blockIdx.x, t = threadIdx.x;
+  if (t == 0) {
+    for (int pass = 0; pass < (c ? 2 : 1); pass++) {
+      const int cc = pass ? c : 0;
+      int cand[5][3];
+      auto pos = [](int n, int a) { return max(0, min(n - 1, a)); };
+      if (cc == 0) {
+        const int xs[5] = {g.nx / 2, 2, g.nx - 3, 2, g.nx - 3}, ys[5] = {g.ny / 2, 2, g.ny - 3, g.ny - 3, 2},
+                  zs[5] = {g.nz / 2, 2, g.nz - 3, g.nz / 2, g.nz / 2};
+        for (int q = 0; q < 5; q++) cand[q][0] = pos(g.nx, xs[q]), cand[q][1] = pos(g.ny, ys[q]), cand[q][2] = pos(g.nz, zs[q]);
+      } else {
+        const int ax = (cc - 1) >> 1, hi = (cc - 1) & 1;  // face normal 0/1/2, high side
+        const int n3[3] = {g.nx, g.ny, g.nz};
+        const int ua = ax == 0 ? 1 : 0, va = ax == 2 ? 1 : 2;  // the in-face axes
+        const int us[5] = {n3[ua] / 2, 2, n3[ua] - 3, 2, n3[ua] - 3}, vs[5] = {n3[va] / 2, 2, 2, n3[va] - 3, n3[va] - 3};
+        for (int q = 0; q < 5; q++) {
+          cand[q][ax] = hi ? n3[ax] - 1 : 0;
+          cand[q][ua] = pos(n3[ua], us[q]);
+          cand[q][va] = pos(n3[va], vs[q]);
+        }
+      }
+      unsigned w[5][7];
+      bool ok[5];
+      for (int q = 0; q < 5; q++) {
+        int nf = 0;
+        const int cl = st_class(g, cand[q][0], cand[q][1], cand[q][2], nf);
+        const int n = cand[q][0] + g.nx * (cand[q][1] + g.ny * cand[q][2]);
+        const u32x4* ip = I + (int64_t)(n >> 6) * (2 * 64) + (n & 63);
+        const u32x4 w0 = ip[0], w1 = ip[64];
+        for (int r = 0; r < 7; r++) w[q][r] = r < 4 ? w0[r] : w1[r - 4];
+        ok[q] = g.nown > 0 && cl == cc && (cc ? nf == 1 : nf == 0) && w1[3] == 0u;
+      }
+      int best = -1, bestv = 0;
+      for (int q = 0; q < 5; q++) {
+        if (!ok[q]) continue;
+        int v = 0;
+        for (int p = 0; p < 5; p++) {
+          bool same = ok[p];
+          for (int r = 0; r < 7; r++) same = same && w[p][r] == w[q][r];
+          v += same;
+        }
+        if (v > bestv) best = q, bestv = v;
+      }
+      for (int r = 0; r < 7; r++) wsel[pass][r] = best >= 0 ? w[best][r] : 0u;
+      wsel[pass][7] = best >= 0;
+    }
+    wsel[1][7] = c ? wsel[0][7] && wsel[1][7] && ((faces >> c) & 1) : wsel[0][7];
+  }
+  __syncthreads();
+  const unsigned* w = wsel[c ? 1 : 0];
+  if (t < 27 * VIB_STRIDE) {  // rows of VIB_STRIDE doubles like the dictionary's (zeros: class unused)
+    const int nb = t / VIB_STRIDE, q = t % VIB_STRIDE;
+    coef[c * 27 * VIB_STRIDE + t] = q < 9 && wsel[1][7] ? bdict[st_byte(w, nb) * VIB_STRIDE + q] : 0.;
+  }
+  if (t < 7) ids[8 * c + t] = w[t];
+  if (t == 7) ids[8 * c + 7] = wsel[1][7];
+}
+
+// pass 1: flag[n] = 1 for a listed node: an exception node, an edge / corner node, a node of an
+// unusable class, or one whose index words differ from its class representative's; cnt[block] =
+// the block's count (then k_exc_scan / k_exc_assign: list in owned-node order, flag -> slot + 1)
 __global__ __launch_bounds__(TPB) void k_st_flag(Geo g, const u32x4* __restrict__ I, const unsigned* __restrict__ ids,
                                                  unsigned* __restrict__ flag, unsigned* __restrict__ cnt) {
   const int n = blockIdx.x * TPB + threadIdx.x;
   bool nd = false;
   if (n < g.nown) {
+    int i, j, k, nf;
+    node_ijk(g, n, i, j, k);
+    const int cl = st_class(g, i, j, k, nf);
+    const unsigned* id = ids + 8 * cl;
     const u32x4* ip = I + (int64_t)(n >> 6) * (2 * 64) + (n & 63);
     const u32x4 w0 = ip[0], w1 = ip[64];
-    unsigned diff = w1[3];
+    unsigned diff = w1[3] | (nf > 1) | (id[7] ^ 1u);
 #pragma unroll
-    for (int q = 0; q < 7; q++) diff |= (q < 4 ? w0[q] : w1[q - 4]) ^ ids[q];
+    for (int q = 0; q < 7; q++) diff |= (q < 4 ? w0[q] : w1[q - 4]) ^ id[q];
     nd = diff != 0u;
     flag[n] = nd ? 1u : 0u;
   }
@@ -3402,7 +3561,7 @@ __global__ __launch_bounds__(TPB) void k_st_flag(Geo g, const u32x4* __restrict_
 }
 
 // pass 2: one 64-bit mask per 16 x 4 patch and plane (k_spmv_st's wave layout): bit = the lane's
-// node is listed (slot != 0) or outside the domain
+// node is not marched: on a domain face (the face phase), listed (slot != 0), or outside the domain
 __global__ __launch_bounds__(TPB) void k_st_mask(Geo g, const unsigned* __restrict__ slot,
                                                  unsigned long long* __restrict__ mask, int npx, int npy) {
   const int64_t w = (int64_t)blockIdx.x * (TPB / 64) + (threadIdx.x >> 6);
@@ -3413,7 +3572,11 @@ __global__ __launch_bounds__(TPB) void k_st_mask(Geo g, const unsigned* __restri
   const int py = (int)(r % npy), k = (int)(r / npy);
   const int i = px * 16 + (ln & 15), j = py * 4 + (ln >> 4);
   bool skip = true;
-  if (i < g.nx && j < g.ny) skip = slot[i + g.nx * (j + (int64_t)g.ny * k)] != 0u;
+  if (i < g.nx && j < g.ny) {
+    int nf;
+    st_class(g, i, j, k, nf);
+    skip = nf > 0 || slot[i + g.nx * (j + (int64_t)g.ny * k)] != 0u;  // a face node: the face phase's or listed
+  }
   const unsigned long long m = __ballot(skip);
   if (ln == 0) mask[w] = m;
 }
@@ -4703,11 +4866,14 @@ bool fusep(const Ctx& c);
 bool st_used(const Ctx& c) {
   int tx, ty;
   vis_shape(c, tx, ty);
-  return c.vi_st && c.st_ok && c.fmt == FMT_VI && c.vi_block && vi_staged(c) && c.vi_fma && c.vi_uni && c.vi_patch &&
+  return (c.vi_st == 1 || (c.vi_st < 0 && c.g.nown >= ST_MIN_NODES)) && c.st_ok && c.fmt == FMT_VI && c.vi_block && vi_staged(c) && c.vi_fma && c.vi_uni && c.vi_patch &&
          tx == 64 && !fusep(c);
 }
 
-static int64_t fix_blocks(const Ctx& c) { return st_used(c) && !c.vi_st_tail ? (c.st_n + TPB - 1) / TPB : 0; }
+// k_spmv_face's blocks (the face phase and the listed rows as a kernel of their own: vi_st_tail 0)
+static int64_t stface_blocks(const Ctx& c) {
+  return st_used(c) && !c.vi_st_tail ? c.st_faces.u[6] + (c.st_n + 255) / 256 : 0;
+}
 
 // the exception rows' kernel (staged block-indexed storage with exception nodes, vi_exc_kernel)
 static int64_t exc_blocks(const Ctx& c) {
@@ -4717,7 +4883,7 @@ static int64_t exc_blocks(const Ctx& c) {
 
 int64_t spmv_nparts(const Ctx& c) {
   if (c.fmt == FMT_SPLIT && c.dsl.dense) return node_blocks(c);
-  return spmv_grid_blocks(c) + faces_blocks(c) + exc_blocks(c) + fix_blocks(c);
+  return spmv_grid_blocks(c) + faces_blocks(c) + exc_blocks(c) + stface_blocks(c);
 }
 
 int upload_constants(Ctx& c) {
@@ -5186,12 +5352,12 @@ int build_st(Ctx& c) {
   const int npx = (c.g.nx + 15) / 16, npy = (c.g.ny + 3) / 4;
   const int64_t nwp = (int64_t)npx * npy * c.g.nz;
   if (!c.st_coef) {
-    MCX_HIP(hipMalloc(&c.st_coef, 27 * VIB_STRIDE * sizeof(double)));
-    MCX_HIP(hipMalloc(&c.st_ids, 8 * sizeof(unsigned)));
+    MCX_HIP(hipMalloc(&c.st_coef, ST_CLASSES * 27 * VIB_STRIDE * sizeof(double)));
+    MCX_HIP(hipMalloc(&c.st_ids, ST_CLASSES * 8 * sizeof(unsigned)));
     MCX_HIP(hipMalloc(&c.st_slot, c.g.nown * sizeof(unsigned)));
     MCX_HIP(hipMalloc(&c.st_list, c.g.nown * sizeof(int)));
     MCX_HIP(hipMalloc(&c.st_cnt, (node_blocks(c) + 1) * sizeof(unsigned)));
-    c.device_bytes += 27 * VIB_STRIDE * 8 + 32 + c.g.nown * 8 + (node_blocks(c) + 1) * 4;
+    c.device_bytes += ST_CLASSES * (27 * VIB_STRIDE * 8 + 32) + c.g.nown * 8 + (node_blocks(c) + 1) * 4;
   }
   if (nwp * 8 > c.st_mask_bytes) {
     if (c.st_mask) {
@@ -5203,22 +5369,35 @@ int build_st(Ctx& c) {
     c.device_bytes += c.st_mask_bytes;
   }
   const u32x4* I = reinterpret_cast<const u32x4*>(c.vi_idx);
-  const int center = c.g.nx / 2 + c.g.nx * (c.g.ny / 2 + c.g.ny * (c.g.nz / 2));
   const unsigned nbn = nblk(c.g.nown);
-  hipLaunchKernelGGL(k_st_setup, dim3(1), dim3(27 * VIB_STRIDE), 0, c.stream, I, c.vi_bdict, center, c.st_coef, c.st_ids);
+  hipLaunchKernelGGL(k_st_setup, dim3(ST_CLASSES), dim3(320), 0, c.stream, c.g, I, c.vi_bdict, c.st_coef, c.st_ids,
+                     c.vi_st_faces == 1 ? 0x7e : c.vi_st_faces);
   hipLaunchKernelGGL(k_st_flag, dim3(nbn), dim3(TPB), 0, c.stream, c.g, I, c.st_ids, c.st_slot, c.st_cnt);
   hipLaunchKernelGGL(k_exc_scan, dim3(1), dim3(1024), 0, c.stream, c.st_cnt, (int)nbn, c.st_cnt + nbn);
   hipLaunchKernelGGL(k_exc_assign, dim3(nbn), dim3(TPB), 0, c.stream, c.g, c.st_slot, c.st_list, c.st_cnt);
   hipLaunchKernelGGL(k_st_mask, dim3((unsigned)((nwp + TPB / 64 - 1) / (TPB / 64))), dim3(TPB), 0, c.stream, c.g,
                      c.st_slot, c.st_mask, npx, npy);
-  unsigned h[2] = {0u, 0u};
+  unsigned h[1 + 8 * ST_CLASSES] = {};
   MCX_HIP(hipMemcpyAsync(&h[0], c.st_cnt + nbn, sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
-  MCX_HIP(hipMemcpyAsync(&h[1], c.st_ids + 7, sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
+  MCX_HIP(hipMemcpyAsync(&h[1], c.st_ids, 8 * ST_CLASSES * sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
   MCX_HIP(hipStreamSynchronize(c.stream));
   c.st_n = h[0];
   c.st_npx = npx;
   c.st_npy = npy;
-  c.st_ok = h[1] == 0u;  // the middle node is an exception node: no default stencil
+  c.st_fm = 0;
+  for (int k = 0; k < ST_CLASSES; k++) c.st_fm |= (h[1 + 8 * k + 7] != 0u) << k;
+  c.st_ok = c.st_fm & 1u;  // no interior representative (exception nodes): no default stencil
+  // the face phase's patches: class q's face (if usable) in patches of 64 x 4 nodes (fast x slow axis)
+  const Geo& g = c.g;
+  const bool on[7] = {false, g.xs == 0, g.xs + g.nx == g.NX, g.ys == 0, g.ys + g.ny == g.NY, g.zs == 0, g.zs + g.nz == g.NZ};
+  c.st_faces.u[0] = 0;
+  for (int q = 1; q < ST_CLASSES; q++) {
+    const int ax = (q - 1) >> 1;
+    const int nfast = ax == 0 ? g.ny : g.nx, nslow = ax == 2 ? g.ny : g.nz;
+    const bool use = on[q] && ((c.st_fm >> q) & 1u) && !(ax == 0 && g.nx == 1 && q == 2) &&
+                     !(ax == 1 && g.ny == 1 && q == 4) && !(ax == 2 && g.nz == 1 && q == 6);
+    c.st_faces.u[q] = c.st_faces.u[q - 1] + (use ? (int64_t)((nfast + 63) / 64) * ((nslow + 3) / 4) : 0);
+  }
   return 0;
 }
 
@@ -5456,20 +5635,20 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
       int tx, ty;
       vis_shape(c, tx, ty);
       if (st_used(c)) {  // default stencil: two planes per step, the listed rows after the march
-        const int64_t nbf = fix_blocks(c);
+        const int64_t nbfa = stface_blocks(c);
         double* pf = c.partials + nb;
 #define MCX_ST(DV, GV)                                                                                             \
   do {                                                                                                            \
     if (c.vi_st_tail)                                                                                             \
       hipLaunchKernelGGL((k_spmv_st<DV, GV, true>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,   \
                          c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt, c.st_list, c.st_n, I, c.vi_bdict,     \
-                         c.vi_exc);                                                                               \
+                         c.vi_exc, c.st_slot, c.st_faces);                                                        \
     else                                                                                                          \
       hipLaunchKernelGGL((k_spmv_st<DV, GV>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,         \
                          c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);                                      \
-    if (nbf)                                                                                                      \
-      hipLaunchKernelGGL((k_spmv_fix<DV, GV>), dim3((unsigned)nbf), dim3(TPB), 0, c.stream, c.g, c.st_list, c.st_n, \
-                         I, c.vi_bdict, c.vi_exc, xpad, y, pf, c.cg);                                             \
+    if (nbfa)                                                                                                     \
+      hipLaunchKernelGGL((k_spmv_face<DV, GV>), dim3((unsigned)nbfa), dim3(256), 0, c.stream, c.g, c.st_faces,      \
+                         c.st_coef, c.st_slot, xpad, y, pf, c.cg, c.st_list, c.st_n, I, c.vi_bdict, c.vi_exc);    \
   } while (0)
         if (dot && gated) MCX_ST(true, true);
         else if (dot) MCX_ST(true, false);

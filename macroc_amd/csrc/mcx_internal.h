@@ -88,6 +88,13 @@ constexpr int VI_MAX = 256;     // dictionary entries (one index byte per value)
 constexpr int VI_EXC_LIST = 2048;  // staged value-indexed SpMV: exception nodes a tile defers to its block-wide pass
 constexpr int VI_HASH = 4096;   // open-addressing set of the distinct values (bit patterns)
 constexpr int VI_CHUNKS = 16;   // 16-B index chunks per node: 243 slots + 13 zero pad bytes
+// vi_st -1: the default-stencil SpMV from this many owned nodes (at 256^3 it saves 2 % of a CG
+// iteration, at 128^3 the faces' share makes it 6 % slower: profiles/r05p_*)
+constexpr int64_t ST_MIN_NODES = int64_t(1) << 23;
+constexpr int ST_CLASSES = 7;   // default-stencil SpMV: the interior + the 6 domain faces (k_st_setup)
+struct StFaces {  // the face phase of the default-stencil SpMV: class c's patches (64 x 4 nodes) are [u[c-1], u[c])
+  int64_t u[7];
+};
 constexpr int VIB_STRIDE = 10;  // doubles per dictionary block (9 values + pad: 16-B aligned)
 constexpr int VB_GSV = 64;      // single-pass block build: entries of each slot's global value set (6-bit positions)
 
@@ -255,10 +262,12 @@ struct Ctx {
   int vi_lg = 2;             // staged block-indexed SpMV, LDS-dictionary waves: blocks whose reads are issued together (option vi_lg: 1, 2, 3)
   int cg_p2d = 0;            // quad-buffered p update on a (rows, x chunks) grid: no per-node divisions (option cg_p2d; A/B)
   int vi_lg_exc = 1;         // vi_lg 2 also in the exception-node kernel (option vi_lg_exc; 0: per-block waits)
-  int vi_st = 1;             // default-stencil SpMV (k_spmv_st + k_spmv_fix, option vi_st; FMA rows, 64 x 16 tiles)
-  int vi_st_tail = 1;        // its listed rows in the same blocks after the march (option vi_st_tail; 0: k_spmv_fix)
-  double* st_coef = nullptr;            // [27][VIB_STRIDE] the default stencil's blocks
-  unsigned* st_ids = nullptr;           // [8] its 7 index words, [7] = center is an exception node
+  int vi_st = -1;            // default-stencil SpMV (k_spmv_st + k_spmv_face, option vi_st; FMA rows, 64 x 16 tiles):
+                             // -1 (default) from ST_MIN_NODES owned nodes up, 0 off, 1 on
+  int vi_st_faces = 1;       // the domain faces as stencil classes of their own (option vi_st_faces: 1 all, 0 none (listed), else bit c = class c)
+  int vi_st_tail = 0;        // its faces and listed rows in the march's blocks after the march (option vi_st_tail; 0: k_spmv_face)
+  double* st_coef = nullptr;            // [ST_CLASSES][27][VIB_STRIDE] the stencil classes' blocks
+  unsigned* st_ids = nullptr;           // [ST_CLASSES][8] their 7 index words, [7] = class usable
   unsigned* st_slot = nullptr;          // [nown] list position + 1 of a non-default node, 0 = default
   int* st_list = nullptr;               // [nown] non-default nodes in owned-node order
   unsigned* st_cnt = nullptr;           // [node blocks + 1] scan scratch
@@ -266,6 +275,8 @@ struct Ctx {
   int64_t st_mask_bytes = 0, st_n = 0;
   int st_npx = 0, st_npy = 0;
   bool st_ok = false;                   // built for the current block indices
+  unsigned st_fm = 0;                   // bit c: stencil class c usable (k_st_setup)
+  StFaces st_faces = {};                // the face phase's units per class
   int vi_exc_kernel = 1;     // staged SpMV: exception rows in their own kernel after the march (k_spmv_exc, option
                              // vi_exc_kernel; 0: round 4's block-wide pass in each tile's tail)
   int vi_wdesc = 1;          // staged block-indexed SpMV: wave descriptors (option vi_wdesc): 1 = uniform waves (default since round 5: -2.1 % per CG iteration), 2 = also two-set waves (FMA rows), 0 = per-lane index words

@@ -734,9 +734,10 @@ def test_aij_vi_production_tiles(NX, NY, NZ, vi_tx, tile):
             m.set_option("vi_st", 0)
             assert np.array_equal(m.spmv(x), yf), (zblocks, "vi_st 0")
             m.set_option("vi_st", 1)
-            m.set_option("vi_st_tail", 0)  # the listed rows by k_spmv_fix instead of the march blocks' tail
-            assert np.array_equal(m.spmv(x), yf), (zblocks, "vi_st_tail 0")
-            m.set_option("vi_st_tail", 1)
+            assert np.array_equal(m.spmv(x), yf), (zblocks, "vi_st 1")
+            m.set_option("vi_st_tail", 1)  # the faces and listed rows by the march blocks instead of k_spmv_face
+            assert np.array_equal(m.spmv(x), yf), (zblocks, "vi_st_tail 1")
+            m.set_option("vi_st_tail", 0)
             m.set_option("vi_ypair", 1)
             assert np.array_equal(m.spmv(x), yf), (zblocks, "ypair")
             m.set_option("vi_ypair", 0)
@@ -774,6 +775,44 @@ def test_round4_options_refused():
                 m.set_option(name, bad)
         its1, _, _ = m.solve_Ax()
         assert its1 == its0 and np.array_equal(m.du(), du0)
+
+
+@pytest.mark.parametrize("N", [37, 48])
+def test_st_face_classes(N):
+    """The default-stencil SpMV's stencil classes (k_st_setup): the interior is marched, the 6 domain
+    faces computed in patches with their class's stencil (st_faces); only edge / corner nodes, nodes
+    next to Dirichlet nodes and exception nodes are listed.  On a cube (37: partial tiles, patches
+    and face patches, an odd plane count against the two-plane steps; 48: whole tiles) the rows are
+    bitwise the per-node index path's (vi_st 0), with the faces in k_spmv_face (default) and in the
+    march blocks' tail, and the listed count is a small fraction of the face nodes."""
+    rtol = 1e-12
+    P = O.Problem(N, N, N, rtol=rtol)
+    with M.Macroc(argv_for(N, N, N, rtol)) as m:
+        m.set_option("vi_stage", 1)  # the staged tiles (at this size the default rule chunks z finer)
+        m.set_option("vi_st", 1)  # (by default from 2^23 nodes)
+        for ts in (0, 1):
+            m.apply_bc_on_u(m.get_displacement(ts))
+            P.apply_bc_u(P.get_displacement(ts))
+        m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
+        P.set_strains(); P.homogenize(); P.assembly_res(); P.assembly_jac()
+        x = np.random.default_rng(5).uniform(-1, 1, m.n)
+        y_ref = P.spmv(x)
+        rp, ci, v = m.dump_csr()
+        absrow = np.add.reduceat(np.abs(v) * np.abs(x[ci]), rp[:-1])
+        info = m.get_info()
+        faces = 6 * (N - 2) ** 2
+        assert 0 < info["st_listed"] < faces // 4, (info["st_listed"], faces)
+        y = m.spmv(x)
+        assert np.all(np.abs(y - y_ref) <= 1e-14 * absrow + 1e-300)
+        for zblocks in (0, 1, 5):
+            m.set_option("spmv_zblocks", zblocks)
+            y = m.spmv(x)
+            m.set_option("vi_st", 0)
+            assert np.array_equal(m.spmv(x), y), zblocks
+            m.set_option("vi_st", 1)
+            m.set_option("vi_st_tail", 1)
+            assert np.array_equal(m.spmv(x), y), zblocks
+            m.set_option("vi_st_tail", 0)
 
 
 @pytest.mark.parametrize("maxits", [None, 37, 38, 39, 40, 1, 2, 3, 4, 5])
@@ -818,12 +857,15 @@ def test_cg_fused_p_update_bitwise(maxits):
     """Option cg_fusep: the CG's p update inside the value-indexed SpMV (two p buffers) and
     VecAXPY(x) every second iteration in the update kernel give bitwise the solve of the separate
     kernels — converged, and stopped by maxits after an odd and an even number of iterations
-    (the pending x update of the last iteration, k_cg_xfinal)."""
+    (the pending x update of the last iteration, k_cg_xfinal).  The default-stencil SpMV (vi_st)
+    does not fuse the p update and sums p.Ap over other partials: off here, so both sides run the
+    same SpMV kernel."""
     NX, NY, NZ = 70, 20, 12
     argv = argv_for(NX, NY, NZ, 1e-12) + (["-ksp_max_it", maxits] if maxits else [])
     out = []
     with M.Macroc(argv) as m:
         m.set_option("vi_stage", 1)
+        m.set_option("vi_st", 0)
         m.apply_bc_on_u(m.get_displacement(1))
         m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
         for fusep in (0, 1, 0):

@@ -22,5 +22,5 @@ for spec in a.sets.split(";"):
     for kv in [kv for kv in spec.split(",") if kv]:
         k, v = kv.split("=")
         m.set_option(k, float(v))
-    print(spec, "avg ms per SpMV (events):", m.time_spmv(a.iters), flush=True)
+    print(spec, "avg ms per SpMV (events):", m.time_spmv(a.iters), "st_listed", m.get_info()["st_listed"], flush=True)
 m.finish()
