@@ -62,9 +62,11 @@ KERNEL_NAME = {0: "k_spmv (AIJ stencil blocks, CPU AIJ row order)",
                      "multiply-adds)",
                "3be": "k_spmv_vibm (block-indexed AIJ as above, -mat_vi_fma 0: multiply then add in the CPU AIJ "
                       "row order, bit-exact)",
-               "3bs": "k_spmv_st (block-indexed AIJ, default-stencil path: the interior stencil's blocks from scalar "
-                      "loads, two z-planes per step, x ring in LDS, no index bytes; the listed non-default rows from "
-                      "their index bytes in the same blocks after the march; rows summed with fused multiply-adds)"}
+               "3bs": "k_spmv_st + k_spmv_face, one SpMV = the two launches (block-indexed AIJ, default-stencil "
+                      "path: k_spmv_st marches the interior with the interior stencil's blocks from scalar loads, two "
+                      "z-planes per step, x ring in LDS, no index bytes; k_spmv_face computes the 6 domain faces with "
+                      "their class stencils from LDS-staged 64x4 patches and the listed rows from their index bytes; "
+                      "rows summed with fused multiply-adds)"}
 
 
 def kernel_name(r):
