@@ -30,13 +30,27 @@ def per_dispatch(counter):
 
 
 fetch, names = per_dispatch("FETCH_SIZE")
-write, _ = per_dispatch("WRITE_SIZE")
-# gated launches of a converged chunk do no work: keep launches that read > 1 % of the median max
-big = max(fetch.values())
-f_real = [v for v in fetch.values() if v > 0.01 * big]
-bigw = max(write.values())
-w_real = [v for v in write.values() if v > 0.01 * bigw]
-fk, wk = statistics.median(f_real), statistics.median(w_real)
+write, wnames = per_dispatch("WRITE_SIZE")
+
+
+def per_kernel(vals, nm):
+    """median per kernel (gated launches of a converged chunk do no work: launches that moved > 1 %
+    of the kernel's maximum), summed over the kernels: one SpMV may be two launches (the
+    default-stencil path: k_spmv_st + k_spmv_face)"""
+    by = {}
+    for d, v in vals.items():
+        by.setdefault(nm[d].split("(")[0], []).append(v)
+    med, cnt = {}, 0
+    for k, vs in by.items():
+        real = [v for v in vs if v > 0.01 * max(vs)]
+        med[k] = statistics.median(real)
+        cnt = max(cnt, len(real))
+    return sum(med.values()), med, cnt
+
+
+fk, fmed, nf = per_kernel(fetch, names)
+wk, wmed, nw = per_kernel(write, wnames)
+f_real, w_real = range(nf), range(nw)
 hbm = (2 * fk + wk) * 1024
 kern = sorted(set(n.split("(")[0] for n in names.values()))
 summary = (f"{mat} {grid}^3 kernels {kern}: FETCH_SIZE dispatches={len(fetch)} real={len(f_real)} "
@@ -54,6 +68,7 @@ try:
 except (OSError, ValueError):
     d = {}
 d[f"{mat}:{grid}x{grid}x{grid}"] = {"hbm_bytes_per_launch": hbm, "fetch_kb_median": fk, "write_kb_median": wk,
+                                     "per_kernel_kb": {k: {"fetch": fmed[k], "write": wmed.get(k)} for k in fmed},
                                      "launches": len(f_real), "kernels": kern,
                                      "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes, "
                                                "--kernel-include-regex, bench.py --steps 1 --warmup 0",

@@ -7,7 +7,7 @@ set -euo pipefail
 MAT=${1:-aij-split}
 G=${2:-256}
 case $MAT in
-  aij-vi) RE='k_spmv_vib|k_spmv_st'; BM=aij ;;  # value-indexed: k_spmv_vibm, or the default-stencil k_spmv_st (vi_st)
+  aij-vi) RE='k_spmv_vib|k_spmv_st|k_spmv_face'; BM=aij ;;  # value-indexed: k_spmv_vibm, or the default-stencil k_spmv_st + k_spmv_face (vi_st)
   aij-split) RE='k_spmv_symp'; BM=aij-split ;;
   aij-blocks) RE='k_spmv<'; BM=aij-blocks ;;
   sbaij) RE='k_spmv_sym'; BM=sbaij ;;
@@ -20,4 +20,4 @@ for C in FETCH_SIZE WRITE_SIZE; do
     python3 bench.py --steps 1 --warmup 0 --grid $G --mat-type $BM --variants '' --cpu-grid 0 --config5 0 --bending 0 --no-check \
     > $OUT/$C.log 2>&1
 done
-python3 tools/pmc_parse.py $MAT $G $OUT
+MCX_COMMIT=${MCX_COMMIT:-} python3 tools/pmc_parse.py $MAT $G $OUT
