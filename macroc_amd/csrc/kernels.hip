@@ -4863,10 +4863,19 @@ bool fusep(const Ctx& c);
 
 // the default-stencil SpMV (k_spmv_st + k_spmv_fix): FMA rows on the 64 x 16 staged tiles with the
 // scalar-dictionary patches, not the fused p update
+// vi_st -1: from ST_MIN_NODES owned nodes, or with exception nodes up to a tenth of the owned nodes
+// (their rows are listed rows there; the z-march's exception instantiations cost every wave:
+// config 5 226.7 vs 236.7 ms per Newton iteration, 128^3 sweep 0.1511 / 0.1689 / 0.2018 vs
+// 0.1604 / 0.1671 / 0.2128 ms per CG iteration at 1.6 / 3.1 / 7.0 % exception nodes, 0.3567 vs
+// 0.3362 at 25.8 %: profiles/r05s_*, r05t_exc_sweep128.log)
+static bool st_auto(const Ctx& c) {
+  return c.g.nown >= ST_MIN_NODES || (c.vi_nexc > 0 && c.vi_nexc * 10 <= (int64_t)c.g.nown);
+}
+
 bool st_used(const Ctx& c) {
   int tx, ty;
   vis_shape(c, tx, ty);
-  return (c.vi_st == 1 || (c.vi_st < 0 && c.g.nown >= ST_MIN_NODES)) && c.st_ok && c.fmt == FMT_VI && c.vi_block && vi_staged(c) && c.vi_fma && c.vi_uni && c.vi_patch &&
+  return (c.vi_st == 1 || (c.vi_st < 0 && st_auto(c))) && c.st_ok && c.fmt == FMT_VI && c.vi_block && vi_staged(c) && c.vi_fma && c.vi_uni && c.vi_patch &&
          tx == 64 && !fusep(c);
 }
 

@@ -263,7 +263,7 @@ struct Ctx {
   int cg_p2d = 0;            // quad-buffered p update on a (rows, x chunks) grid: no per-node divisions (option cg_p2d; A/B)
   int vi_lg_exc = 1;         // vi_lg 2 also in the exception-node kernel (option vi_lg_exc; 0: per-block waits)
   int vi_st = -1;            // default-stencil SpMV (k_spmv_st + k_spmv_face, option vi_st; FMA rows, 64 x 16 tiles):
-                             // -1 (default) from ST_MIN_NODES owned nodes up, 0 off, 1 on
+                             // -1 (default) from ST_MIN_NODES owned nodes up or with <= 10 % exception nodes, 0 off, 1 on
   int vi_st_faces = 1;       // the domain faces as stencil classes of their own (option vi_st_faces: 1 all, 0 none (listed), else bit c = class c)
   int vi_st_tail = 0;        // its faces and listed rows in the march's blocks after the march (option vi_st_tail; 0: k_spmv_face)
   double* st_coef = nullptr;            // [ST_CLASSES][27][VIB_STRIDE] the stencil classes' blocks
