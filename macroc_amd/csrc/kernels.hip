@@ -3125,7 +3125,9 @@ __device__ __forceinline__ void st_tail(const Geo& g, const int* __restrict__ li
 // cache (the patch's class is uniform) and its x from LDS in the FMA rows' order of k_spmv_vibm, so
 // y is bitwise the same.  A face node that is listed (slot != 0: an edge node, next to a Dirichlet
 // node, an exception node, or not its class's stencil) is left to the listed rows.
-constexpr int SFP_N = 66 * 6 * 9;  // staged doubles per patch (= 6 * 3 * 198 = 3 * 6 * 198)
+constexpr int SFP_S = 4;                     // patch rows along the slow axis (a wave each; 6: 42.8 vs 40.7 us, r05w)
+constexpr int SFP_T = 64 * SFP_S;            // threads per patch
+constexpr int SFP_N = 66 * (SFP_S + 2) * 9;  // staged doubles per patch (= (SFP_S+2) * 3 * 198)
 
 struct SfPatch {  // patch p's class, axis, side and origin
   int c, ax, f0, s0;
@@ -3140,43 +3142,43 @@ __device__ __forceinline__ SfPatch sf_patch(const Geo& g, const StFaces& sf, int
   q.hi = !(q.c & 1);
   const int fb = ((q.ax == 0 ? g.ny : g.nx) + 63) >> 6;
   const int64_t lp = p - sf.u[q.c - 1];
-  q.s0 = (int)(lp / fb) * 4;
-  q.f0 = (int)(lp - (int64_t)(q.s0 / 4) * fb) * 64;
+  q.s0 = (int)(lp / fb) * SFP_S;
+  q.f0 = (int)(lp - (int64_t)(q.s0 / SFP_S) * fb) * 64;
   return q;
 }
 
-// stage patch q's x into S (t = 0 .. 255: the patch's threads)
+// stage patch q's x into S (t = 0 .. SFP_T-1: the patch's threads)
 __device__ __forceinline__ void sf_stage(const Geo& g, const SfPatch& q, const double* __restrict__ x, double* S,
                                          int t) {
   const int PX = g.PX, PXY = g.PX * g.PY;
   const int iface = q.hi ? g.nx - 1 : 0, jface = q.hi ? g.ny - 1 : 0, kface = q.hi ? g.nz - 1 : 0;
-  constexpr int NE = (SFP_N + 255) / 256;
-  double v[NE];  // all loads in flight before the LDS stores (a load-store round trip each: 14 HBM latencies)
+  constexpr int NE = (SFP_N + SFP_T - 1) / SFP_T;
+  double v[NE];  // all loads in flight before the LDS stores (a load-store round trip each: NE HBM latencies)
 #pragma unroll
   for (int m = 0; m < NE; m++) {
-    const int e = t + m * 256;
+    const int e = t + m * SFP_T;
     int pi, jp, kp, o;  // padded column of the chunk / segment start, local j', k', offset
     bool ok;
-    if (q.ax == 0) {  // 9-double chunks, (kk, jj) of 6 x 66
+    if (q.ax == 0) {  // 9-double chunks, (kk, jj) of (SFP_S+2) x 66
       const int ch = e / 9, jj = ch % 66;
       o = e - ch * 9;
       pi = iface;
       jp = q.f0 - 1 + jj;
       kp = q.s0 - 1 + ch / 66;
       ok = e < SFP_N && jp <= g.ny && kp <= g.nz;
-    } else {  // 198-double segments: y-face (kk, dy) of 6 x 3, z-face (dz, jj) of 3 x 6
+    } else {  // 198-double segments: y-face (kk, dy) of (SFP_S+2) x 3, z-face (dz, jj) of 3 x (SFP_S+2)
       const int r = e / 198;
       o = e - r * 198;
       pi = q.f0;
       if (q.ax == 1) jp = jface - 1 + r % 3, kp = q.s0 - 1 + r / 3;
-      else jp = q.s0 - 1 + r % 6, kp = kface - 1 + r / 6;
+      else jp = q.s0 - 1 + r % (SFP_S + 2), kp = kface - 1 + r / (SFP_S + 2);
       ok = e < SFP_N && o < 3 * (g.nx + 2 - q.f0) && jp <= g.ny && kp <= g.nz;
     }
     v[m] = ok ? x[3 * ((int64_t)pi + (jp + 1) * (int64_t)PX + (kp + 1) * (int64_t)PXY) + o] : 0.;
   }
 #pragma unroll
   for (int m = 0; m < NE; m++)
-    if (t + m * 256 < SFP_N) S[t + m * 256] = v[m];
+    if (t + m * SFP_T < SFP_N) S[t + m * SFP_T] = v[m];
 }
 
 // the rows of patch q's nodes from S (after a barrier)
@@ -3202,7 +3204,7 @@ __device__ __forceinline__ void sf_rows(const Geo& g, const SfPatch& q, const do
     const int dy = g9 % 3 - 1, dz = g9 / 3 - 1;
     const int base = q.ax == 0 ? ((w + 1 + dz) * 66 + (ln + 1 + dy)) * 9
                    : q.ax == 1 ? ((w + 1 + dz) * 3 + (dy + 1)) * 198 + 3 * ln
-                               : ((dz + 1) * 6 + (w + 1 + dy)) * 198 + 3 * ln;
+                               : ((dz + 1) * (SFP_S + 2) + (w + 1 + dy)) * 198 + 3 * ln;
     double xw[9], av[27];
 #pragma unroll
     for (int qq = 0; qq < 9; qq++) xw[qq] = Sl[base + qq];
@@ -3228,16 +3230,17 @@ __device__ __forceinline__ void sf_rows(const Geo& g, const SfPatch& q, const do
   }
 }
 
-// a 1024-thread block's share of the patches [b P / nb, (b+1) P / nb), 4 at a time (a quarter
-// block each, S: 4 SFP_N doubles); every thread takes part in every barrier
+// a 1024-thread block's share of the patches [b P / nb, (b+1) P / nb), 1024 / SFP_T at a time
+// (SFP_T threads and SFP_N doubles of S each); every thread takes part in every barrier
 __device__ __forceinline__ void st_faces(const Geo& g, const StFaces& sf, const double* __restrict__ coef,
                                          const unsigned* __restrict__ slot, const double* __restrict__ x,
                                          double* __restrict__ y, double& dot, double* S) {
   const int64_t P = sf.u[6], lo = (int64_t)blockIdx.x * P / gridDim.x, hi = (int64_t)(blockIdx.x + 1) * P / gridDim.x;
-  const int q4 = threadIdx.x >> 8, t = threadIdx.x & 255;
-  for (int64_t p0 = lo; p0 < hi; p0 += 4) {  // (uniform)
+  constexpr int NPB = 1024 / SFP_T;
+  const int q4 = threadIdx.x / SFP_T, t = threadIdx.x - q4 * SFP_T;
+  for (int64_t p0 = lo; p0 < hi; p0 += NPB) {  // (uniform)
     const int64_t p = p0 + q4;
-    const bool has = p < hi;
+    const bool has = q4 < NPB && p < hi;
     SfPatch q{};
     if (has) {
       q = sf_patch(g, sf, p);
@@ -3422,10 +3425,10 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
   }
 }
 
-// the face phase and the listed rows as a kernel of their own (vi_st_tail 0): blocks [0, P) one face
-// patch each, then 256 listed rows per block (the dictionary staged in the patch's LDS)
+// the face phase and the listed rows as a kernel of their own (vi_st_tail 0): SFP_T listed rows per
+// block (the dictionary staged in the patch's LDS), then one face patch per block
 template <bool DOT, bool GATED>
-__global__ __launch_bounds__(256) void k_spmv_face(Geo g, StFaces sf, const double* __restrict__ coef,
+__global__ __launch_bounds__(SFP_T) void k_spmv_face(Geo g, StFaces sf, const double* __restrict__ coef,
                                                    const unsigned* __restrict__ slot, const double* __restrict__ x,
                                                    double* __restrict__ y, double* __restrict__ part,
                                                    const CgState* __restrict__ cg, const int* __restrict__ list,
@@ -3433,21 +3436,23 @@ __global__ __launch_bounds__(256) void k_spmv_face(Geo g, StFaces sf, const doub
                                                    const double* __restrict__ bdict, const double* __restrict__ exc) {
   static_assert(SFP_N >= VI_MAX * VIB_STRIDE, "the dictionary fits the patch's LDS");
   __shared__ __attribute__((aligned(16))) double S[SFP_N];
-  __shared__ double sh[4];
+  __shared__ double sh[SFP_T / 64];
   if (GATED && cg->reason) return;
   double dot = 0.;
-  const int64_t P = sf.u[6];
-  if ((int64_t)blockIdx.x < P) {
-    const SfPatch q = sf_patch(g, sf, blockIdx.x);
+  // the listed rows' blocks first: their nine dependent gather rounds per node are the longest
+  // chains of the launch, started before the patches instead of after them
+  const int64_t NLB = (cnt + SFP_T - 1) / SFP_T;
+  if ((int64_t)blockIdx.x >= NLB) {
+    const SfPatch q = sf_patch(g, sf, blockIdx.x - NLB);
     sf_stage(g, q, x, S, threadIdx.x);
     __syncthreads();
     sf_rows(g, q, coef, slot, S, y, dot, threadIdx.x);
   } else {
-    const int64_t lo = ((int64_t)blockIdx.x - P) * 256;
-    st_tail<256>(g, list, lo, min(cnt, lo + 256), I, bdict, exc, x, y, reinterpret_cast<double2*>(S), dot);
+    const int64_t lo = (int64_t)blockIdx.x * SFP_T;
+    st_tail<SFP_T>(g, list, lo, min(cnt, lo + SFP_T), I, bdict, exc, x, y, reinterpret_cast<double2*>(S), dot);
   }
   if (DOT) {
-    const double sm = block_sum<256>(dot, sh);
+    const double sm = block_sum<SFP_T>(dot, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = sm;
   }
 }
@@ -4881,7 +4886,7 @@ bool st_used(const Ctx& c) {
 
 // k_spmv_face's blocks (the face phase and the listed rows as a kernel of their own: vi_st_tail 0)
 static int64_t stface_blocks(const Ctx& c) {
-  return st_used(c) && !c.vi_st_tail ? c.st_faces.u[6] + (c.st_n + 255) / 256 : 0;
+  return st_used(c) && !c.vi_st_tail ? c.st_faces.u[6] + (c.st_n + SFP_T - 1) / SFP_T : 0;
 }
 
 // the exception rows' kernel (staged block-indexed storage with exception nodes, vi_exc_kernel)
@@ -5396,7 +5401,7 @@ int build_st(Ctx& c) {
   c.st_fm = 0;
   for (int k = 0; k < ST_CLASSES; k++) c.st_fm |= (h[1 + 8 * k + 7] != 0u) << k;
   c.st_ok = c.st_fm & 1u;  // no interior representative (exception nodes): no default stencil
-  // the face phase's patches: class q's face (if usable) in patches of 64 x 4 nodes (fast x slow axis)
+  // the face phase's patches: class q's face (if usable) in patches of 64 x SFP_S nodes (fast x slow axis)
   const Geo& g = c.g;
   const bool on[7] = {false, g.xs == 0, g.xs + g.nx == g.NX, g.ys == 0, g.ys + g.ny == g.NY, g.zs == 0, g.zs + g.nz == g.NZ};
   c.st_faces.u[0] = 0;
@@ -5405,7 +5410,7 @@ int build_st(Ctx& c) {
     const int nfast = ax == 0 ? g.ny : g.nx, nslow = ax == 2 ? g.ny : g.nz;
     const bool use = on[q] && ((c.st_fm >> q) & 1u) && !(ax == 0 && g.nx == 1 && q == 2) &&
                      !(ax == 1 && g.ny == 1 && q == 4) && !(ax == 2 && g.nz == 1 && q == 6);
-    c.st_faces.u[q] = c.st_faces.u[q - 1] + (use ? (int64_t)((nfast + 63) / 64) * ((nslow + 3) / 4) : 0);
+    c.st_faces.u[q] = c.st_faces.u[q - 1] + (use ? (int64_t)((nfast + 63) / 64) * ((nslow + SFP_S - 1) / SFP_S) : 0);
   }
   return 0;
 }
@@ -5656,7 +5661,7 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
       hipLaunchKernelGGL((k_spmv_st<DV, GV>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,         \
                          c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);                                      \
     if (nbfa)                                                                                                     \
-      hipLaunchKernelGGL((k_spmv_face<DV, GV>), dim3((unsigned)nbfa), dim3(256), 0, c.stream, c.g, c.st_faces,      \
+      hipLaunchKernelGGL((k_spmv_face<DV, GV>), dim3((unsigned)nbfa), dim3(SFP_T), 0, c.stream, c.g, c.st_faces,    \
                          c.st_coef, c.st_slot, xpad, y, pf, c.cg, c.st_list, c.st_n, I, c.vi_bdict, c.vi_exc);    \
   } while (0)
         if (dot && gated) MCX_ST(true, true);
