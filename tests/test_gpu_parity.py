@@ -264,6 +264,8 @@ def test_aij_vi_exception_nodes(grid, stage, vi_tx, tile):
         m.set_option("vi_fma", 1)
         y = m.spmv(x)
         assert np.all(np.abs(y - y1) <= 1e-14 * absrow + 1e-300)
+        if tile == (64, 16):  # vi_st -1 with exception nodes (<= 10 %): the default-stencil path, exceptions listed
+            assert m.get_info()["st_listed"] >= info["vi_exc_nodes"], m.get_info()
         m.set_option("vi_st", 0)  # the exception rows through k_spmv_exc / the in-tile pass below
         for xk, xl in ((0, 0), (0, 3), (0, 2048), (1, 2048)):
             m.set_option("vi_exc_kernel", xk)
