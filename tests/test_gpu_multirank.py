@@ -311,6 +311,30 @@ def test_multirank_vi_production_tiles(grid, procs, fma, vi_tx, tile):
     assert np.linalg.norm(du - ref.du()) <= 1e-10 * np.linalg.norm(ref.du())
 
 
+@pytest.mark.parametrize("grid,procs", [((516, 5, 4), (2, 1, 1)), ((260, 9, 10), (1, 1, 2)), ((72, 40, 36), (2, 2, 1))])
+def test_multirank_st_bitwise(grid, procs):
+    """The default-stencil SpMV (vi_st 1: the interior marched with one stencil, the GLOBAL domain's
+    faces by their class stencils, the rest listed) on decomposed subdomains: a rank's internal
+    faces are interior nodes of the march (their neighbours from the halo exchange), only the
+    global faces are classes.  Every rank's y bitwise the per-node index path's (vi_st 0, the
+    z-march with index bytes), and the solve within the north-star bar of the one-rank oracle."""
+    NX, NY, NZ = grid
+    px, py, pz = procs
+    rtol = 1e-12
+    argv = ["-da_grid_x", NX, "-da_grid_y", NY, "-da_grid_z", NZ, "-da_processors_x", px, "-da_processors_y", py,
+            "-da_processors_z", pz, "-ksp_rtol", repr(rtol)]
+    ref = O.Problem(NX, NY, NZ, rtol=rtol)
+    ref.newton_step1()
+    x = np.random.default_rng(29).uniform(-1, 1, ref.ndofs)
+    outs = [run_group(argv, px * py * pz, newton_step(x, [("vi_stage", 1), ("vi_st", st)])) for st in (0, 1)]
+    du = np.zeros(ref.ndofs)
+    for a, b in zip(*outs):
+        assert a["info"]["st_listed"] == -1 and b["info"]["st_listed"] >= 0, (a["info"], b["info"])
+        assert np.array_equal(a["y"], b["y"])
+        du[b["nat"]] = b["du"]
+    assert np.linalg.norm(du - ref.du()) <= 1e-10 * np.linalg.norm(ref.du())
+
+
 @pytest.mark.parametrize("grid,procs,stage", [((20, 12, 10), (2, 2, 1), 0), ((130, 9, 12), (2, 1, 1), 1),
                                               ((24, 16, 14), (2, 2, 2), 0)])
 def test_multirank_vi_exception_nodes(grid, procs, stage):
