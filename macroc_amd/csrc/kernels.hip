@@ -3036,22 +3036,23 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
 
 // ---------------------------------------------------------------------------- default-stencil SpMV
 // Round 5 (vi_st).  On the block-indexed storage almost every node carries the same 27 block
-// indices: the interior stencil of the uniform grid (at 256^3 all but the ~3 % of nodes on the
+// indices: the interior stencil of the uniform grid (at 256^3 all but the 2.3 % of nodes on the
 // domain faces, next to Dirichlet nodes, or exception nodes).  The matrix is then held as
-//   * the default stencil: the 27 blocks of one interior node (st_coef, rows of VIB_STRIDE doubles,
-//     read by every wave with scalar loads),
-//   * a 64-bit mask per 16 x 4 node patch and plane: the lanes whose node is not default (its
-//     index bytes differ, or it is an exception node, or it is outside the domain),
-//   * the list of the non-default nodes (ordered compaction, owned-node order), whose rows come
-//     from their own index bytes / exception blocks exactly as before.
+//   * the stencil classes (k_st_setup): the interior and the 6 domain faces, 27 blocks each
+//     (st_coef, rows of VIB_STRIDE doubles, read with scalar loads),
+//   * a 64-bit mask per 16 x 4 node patch and plane: the lanes the march leaves (face nodes,
+//     listed nodes, outside the domain),
+//   * the list of the other nodes (ordered compaction, owned-node order: edges, neighbours of
+//     Dirichlet nodes, exception nodes, nodes unlike their class), whose rows come from their own
+//     index bytes / exception blocks exactly as before.
 // k_spmv_st marches a 64 x 16 tile up its z-chunk two planes per step (nodes k and k+1 per lane):
 // each group of 3 blocks (one (dy, dz) stencil row) is loaded once for two nodes, so the scalar
 // loads and their waits per node halve; the x ring in LDS holds planes k-1 .. k+2, and planes k+3,
 // k+4 are loaded into registers during the step and stored after a barrier.  The default path
 // reads no index bytes.  Rows are the FMA rows of k_spmv_vibm (one fused multiply-add per term in
-// (nb, c) order), so y is bitwise what k_spmv_vibm computes; a non-default lane's row is left to
-// k_spmv_fix, which computes it from its index bytes (dictionary in global memory) or exception
-// blocks, x gathered, in the same order.  p.w partials: the march's blocks, then k_spmv_fix's.
+// (nb, c) order), so y is bitwise what k_spmv_vibm computes; a face node's row is computed by
+// k_spmv_face from its class stencil, a listed node's from its index bytes or exception blocks, x
+// gathered, in the same order.  p.w partials: the march's blocks, then k_spmv_face's.
 // k_spmv_st TAIL: this block's share of the listed (non-default) rows, in list order, the
 // dictionary staged in tab (the freed ring); x gathered, one stencil row (9 x, 3 blocks) per
 // round; the FMA rows of k_spmv_vibm (an exception node's blocks from exc)
@@ -3252,11 +3253,10 @@ __device__ __forceinline__ void st_faces(const Geo& g, const StFaces& sf, const 
   }
 }
 
-// TAIL (option vi_st_tail, default): the listed rows are computed by the same blocks after their
-// march, each block a fixed share of the list (idle blocks too), with the dictionary staged in the
-// freed x ring: 16 waves per CU hide the gathers' latency that a separate kernel at 2 waves per SIMD
-// exposed (k_spmv_fix: 52 us at 256^3).  Same rows; the listed nodes' p.w terms go to the block's
-// partial.
+// TAIL (option vi_st_tail, off): the face patches and the listed rows are computed by the same
+// blocks after their march, each block a fixed share (idle blocks too), in the freed x ring.  The
+// march is one resident round of blocks, so the tail adds its latency to every block: 0.326 vs
+// 0.285 ms with k_spmv_face (profiles/r05p_*).  Same rows; the p.w terms go to the block's partial.
 template <bool DOT, bool GATED, bool TAIL = false>
 __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restrict__ coef,
                                                   const unsigned long long* __restrict__ mask, int npx, int npy,
@@ -3334,7 +3334,7 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
         xr[1][m] = xload(k + 4, m);
       }
     }
-    unsigned long long m0 = ~0ull, m1 = ~0ull;  // lanes to leave to k_spmv_fix
+    unsigned long long m0 = ~0ull, m1 = ~0ull;  // lanes the march leaves (faces, listed rows)
     if (wvin) {
       m0 = mask[((int64_t)k * npy + gpy) * npx + gpx];
       if (two) m1 = mask[((int64_t)(k + 1) * npy + gpy) * npx + gpx];
@@ -4866,7 +4866,7 @@ static int64_t faces_blocks(const Ctx& c) {
 
 bool fusep(const Ctx& c);
 
-// the default-stencil SpMV (k_spmv_st + k_spmv_fix): FMA rows on the 64 x 16 staged tiles with the
+// the default-stencil SpMV (k_spmv_st + k_spmv_face): FMA rows on the 64 x 16 staged tiles with the
 // scalar-dictionary patches, not the fused p update
 // vi_st -1: from ST_MIN_NODES owned nodes, or with exception nodes up to a tenth of the owned nodes
 // (their rows are listed rows there; the z-march's exception instantiations cost every wave:

@@ -271,7 +271,7 @@ struct Ctx {
   unsigned* st_slot = nullptr;          // [nown] list position + 1 of a non-default node, 0 = default
   int* st_list = nullptr;               // [nown] non-default nodes in owned-node order
   unsigned* st_cnt = nullptr;           // [node blocks + 1] scan scratch
-  unsigned long long* st_mask = nullptr;  // [nz][npy][npx] 16 x 4 patch masks (bit = leave the lane to k_spmv_fix)
+  unsigned long long* st_mask = nullptr;  // [nz][npy][npx] 16 x 4 patch masks (bit = the march leaves the lane: faces, listed rows)
   int64_t st_mask_bytes = 0, st_n = 0;
   int st_npx = 0, st_npy = 0;
   bool st_ok = false;                   // built for the current block indices
@@ -412,7 +412,7 @@ bool vi_staged(const Ctx& c);
 int build_wdesc(Ctx& c);    // wave descriptors of the block-indexed storage (after build_vi)
 bool wd_used(const Ctx& c);  // the staged SpMV reads them
 int build_st(Ctx& c);       // default-stencil SpMV structures (after build_vi)
-bool st_used(const Ctx& c);  // the SpMV runs k_spmv_st + k_spmv_fix
+bool st_used(const Ctx& c);  // the SpMV runs k_spmv_st + k_spmv_face
 bool fusep(const Ctx& c);  // the CG's p update runs inside the value-indexed SpMV
 bool cg_pdb(const Ctx& c);  // the CG's p update double-buffered (x every second iteration)
 int64_t cg_vec_bytes_per_node(const Ctx& c);  // the last solve's CG vector kernels, bytes per owned node and iteration
