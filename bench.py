@@ -7,7 +7,7 @@ rows/columns), KSPSolve(CG, Jacobi, rtol 1e-8) and u += du — every step redoes
 the same state, nothing is cached across steps.  Workload: 256^3 nodes per GPU
 (BASELINE configs[2]; weak scaling: N GPUs own a global grid of 256*(px,py,pz)).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W]      (N > 1: starts the N ranks itself)
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 The headline storage is the default AIJ one: value-indexed (one index byte per 3x3 block into
@@ -30,6 +30,58 @@ import tempfile
 import time
 
 T_START = time.perf_counter()  # wall-clock budget of the whole invocation (variants are guarded by it)
+
+
+def launch_ranks():
+    """`--gpus N` with N > 1 and no WORLD_SIZE in the environment (a plain `python bench.py --gpus 8`):
+    start the N ranks here, one process per GPU through torch.distributed.run on 127.0.0.1, and
+    exit with its status.  Runs before torch or the library is imported, so this parent never
+    touches a GPU and never execs: the ranks are children.  Under a launcher (WORLD_SIZE set) a
+    --gpus that differs from WORLD_SIZE is an error, never a silent one-rank run."""
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=None)
+    pre.add_argument("--dry-run", action="store_true")
+    a, _ = pre.parse_known_args()
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is not None:
+        if a.gpus is not None and a.gpus != int(ws):
+            sys.exit(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={ws} ranks")
+        return
+    if a.gpus is None or a.gpus == 1:
+        return
+    if a.gpus < 1:
+        sys.exit(f"bench.py: --gpus {a.gpus}")
+    import socket
+
+    ndev = a.gpus if a.dry_run else device_count()
+    if ndev < a.gpus:
+        sys.exit(f"bench.py: --gpus {a.gpus} but {ndev} GPU(s) are visible; one rank per GPU needs {a.gpus}")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    print(f"bench.py: --gpus {a.gpus}: starting {a.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    sys.exit(subprocess.run(cmd).returncode)
+
+
+def device_count():
+    """GPUs visible to this process, counted without creating a device context (the parent of
+    launch_ranks must not initialise the GPU): /dev/kfd absent -> 0, else torch's count, which
+    on this image does not initialise the runtime; HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES
+    respected by torch."""
+    if not os.path.exists("/dev/kfd"):
+        return 0
+    out = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                         capture_output=True, text=True, timeout=300)
+    try:
+        return int(out.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        return 0
+
+
+if __name__ == "__main__":
+    launch_ranks()
 
 # torch first: the library then binds to the HIP runtime torch already loaded (one runtime per
 # process); torch is only plumbing here (process group for barriers / max-over-ranks).
@@ -232,6 +284,11 @@ def measure(argv, rank, world, comm_id, args, steps, warmup):
     per phase and per SpMV launch of the first 256 CG iterations of each solve."""
     t_setup = time.perf_counter()
     m = M.Macroc(argv, rank=rank, nranks=world, comm_id=comm_id)
+    # the ranks that really joined the communicator (ncclCommCount): n_gpus in the line is this
+    comm_n, comm_r, comm_dev = m.comm_info()
+    log(f"[rank {rank}] device {comm_dev}, communicator: rank {comm_r} of {comm_n}")
+    if comm_n != world or comm_r != rank:
+        raise SystemExit(f"rank {rank}: the communicator has {comm_n} ranks (this one {comm_r}), expected {world}")
     # a peer that stopped or a mismatched collective fails the waiting rank with its rank and the
     # operation named (communicator aborted) instead of hanging the job until the driver's timeout
     m.set_option("comm_timeout", args.comm_timeout)
@@ -308,7 +365,7 @@ def measure(argv, rank, world, comm_id, args, steps, warmup):
             "vi_values": storage["vi_values"], "vi_bits": storage["vi_bits"], "vi_blocks": storage["vi_blocks"],
             "st_listed": storage["st_listed"],
             "achieved": spmv_bytes / (spmv_avg_ms * 1e-3) / 1e9, "ms_step": dt / max(steps, 1) * 1e3,
-            "warmup_s": t_warm}
+            "warmup_s": t_warm, "comm_ranks": comm_n}
 
 
 def cg_iter_roofline(r):
@@ -355,7 +412,9 @@ def nonlinear_leg(G, ts, dt, rtol, device, extra=()):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs = ranks (default: WORLD_SIZE under a launcher, else 1); N > 1 without a launcher "
+                         "starts the N ranks itself (torch.distributed.run)")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--grid", type=int, default=256, help="nodes per direction per GPU")
@@ -384,13 +443,31 @@ def main():
                          "and the run fails with the rank and the operation named")
     ap.add_argument("--tail", type=float, default=30.0, help="seconds reserved after the timed steps (check, CPU "
                                                              "baseline)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="bootstrap only: every rank joins the process group (gloo) and rank 0 prints the ranks that "
+                         "joined; no GPU is touched (tests of the --gpus launch path on a CPU host)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus is not None and args.gpus != world:  # (launch_ranks handled the no-launcher case)
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     if args.variants is None:
         args.variants = "aij-vi-exact,aij-split" if world == 1 and args.mat_type == "aij" else ""
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+            t = torch.ones(1)
+            dist.all_reduce(t)
+            joined = int(t[0])
+            dist.destroy_process_group()
+        else:
+            joined = 1
+        log(f"[rank {rank}] dry run: local rank {local}, {joined} ranks joined")
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": joined, "world_size": world}), flush=True)
+        return
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
         if torch.cuda.is_available():
@@ -465,7 +542,7 @@ def main():
             "metric": "Newton-iter DOF/s (assembly+CG) at 256^3 grid per GPU; SpMV achieved HBM GB/s",
             "value": ndofs / (ms_step * 1e-3),
             "unit": "DOF/s",
-            "n_gpus": world,
+            "n_gpus": r["comm_ranks"],
             "steps": args.steps,
             "warmup": args.warmup,
             "warmup_run": len(r["warmup_s"]),

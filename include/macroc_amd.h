@@ -6,8 +6,9 @@
  * reference's PetscErrorCode convention (src/assembly.c:37-42 ... CHKERRQ); the message of
  * the last failure (per calling thread) is available from mcx_last_error().  No C++ exception
  * crosses this interface: an internal one (e.g. a failed host allocation) returns 90 with its
- * message.  Multi-rank host waits (CG polls, all-reduced norms) are bounded: after
- * MCX_COMM_TIMEOUT seconds (default 300; option "comm_timeout"), or on an RCCL asynchronous
+ * message.  Multi-rank host waits (CG polls, all-reduced norms, the in-process group's barrier
+ * inside collective entries) are bounded: after the context's "comm_timeout" option (default
+ * MCX_COMM_TIMEOUT seconds at mcx_init, else 300), or on an RCCL asynchronous
  * error, the communicator is aborted and the call returns 24 / 25 naming the rank and the
  * operation; later collectives of that context fail at once.  Host buffers are caller-owned;
  * the context owns all device memory.  A context is not thread-safe; different contexts
@@ -51,6 +52,12 @@ extern "C" {
 #endif
 
 #define MCX_COMM_ID_BYTES 128 /* size of an ncclUniqueId */
+
+/* ABI revision of this header.  Revision 3 (round 6) adds mcx_abi_version and mcx_comm_info;
+   revision 2 (round 5) grew the structs mcx_info by st_listed and mcx_timing by cg_vec_bytes_per_iter, so a
+   caller built against an older header passes smaller structs: check
+   mcx_abi_version() == MCX_ABI_VERSION before calling mcx_get_info / mcx_get_timing / mcx_plan. */
+#define MCX_ABI_VERSION 3
 
 enum { MCX_BC_BENDING = 0, MCX_BC_CIRCLE = 1 }; /* include/macroc.h:58 */
 
@@ -173,6 +180,7 @@ typedef struct {
 
 const char* mcx_last_error(void);
 const char* mcx_version(void);
+int mcx_abi_version(void); /* MCX_ABI_VERSION of the library's build */
 
 void mcx_default_opts(mcx_opts* o);
 /* parse the reference's command-line surface (PETSc options-DB names); unknown flags are
@@ -209,6 +217,11 @@ int mcx_local_group_barrier(void* group, int rank);
 int mcx_init_local(const mcx_opts* o, int rank, void* group, void** ctx);
 int mcx_finalize(void* ctx);
 int mcx_get_info(void* ctx, mcx_info* info);
+/* the ranks that actually joined this context's communicator (MPI_Comm_size / MPI_Comm_rank of
+   PETSC_COMM_WORLD): ncclCommCount, ncclCommUserRank and ncclCommCuDevice of the RCCL
+   communicator; the group size and member rank of the in-process transport; 1, 0 and the
+   context's device without a communicator.  Any pointer may be NULL. */
+int mcx_comm_info(void* ctx, int* comm_ranks, int* comm_rank, int* device);
 
 /* Gauss-point constitutive model (micropp_C_material_set(id,E,nu,Sy,Ka,type)) */
 int mcx_material_set(void* ctx, int id, double E, double nu, double Sy, double Ka, int type);

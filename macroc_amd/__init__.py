@@ -23,6 +23,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmacroc_amd.so")
 COMM_ID_BYTES = 128
+ABI_VERSION = 3  # MCX_ABI_VERSION of include/macroc_amd.h this mirror's structs follow
 
 BC_BENDING, BC_CIRCLE = 0, 1
 KSP_REASONS = {2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL", -3: "DIVERGED_ITS", -4: "DIVERGED_DTOL",
@@ -30,7 +31,7 @@ KSP_REASONS = {2: "CONVERGED_RTOL", 3: "CONVERGED_ATOL", -3: "DIVERGED_ITS", -4:
 
 # symbols declared in include/macroc_amd.h (checked by tests/test_abi.py)
 EXPORTS = [
-    "mcx_last_error", "mcx_version", "mcx_default_opts", "mcx_parse_args", "mcx_comm_unique_id", "mcx_plan", "mcx_plan_halo", "mcx_init",
+    "mcx_last_error", "mcx_version", "mcx_abi_version", "mcx_comm_info", "mcx_default_opts", "mcx_parse_args", "mcx_comm_unique_id", "mcx_plan", "mcx_plan_halo", "mcx_init",
     "mcx_local_group_create", "mcx_local_group_destroy", "mcx_local_group_barrier", "mcx_init_local",
     "mcx_finalize", "mcx_get_info", "mcx_material_set", "mcx_get_displacement", "mcx_zero_u", "mcx_apply_bc_u",
     "mcx_set_strains", "mcx_homogenize", "mcx_assembly_res", "mcx_assembly_jac", "mcx_solve", "mcx_update_u", "mcx_update_vars",
@@ -134,6 +135,8 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise MacrocError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build())")
     L = C.CDLL(LIB_PATH)
+    if L.mcx_abi_version() != ABI_VERSION:  # the structs below would not match the library's
+        raise MacrocError(f"{LIB_PATH}: ABI {L.mcx_abi_version()}, this mirror needs {ABI_VERSION}: rebuild (`make`)")
     vp, d, i64 = C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int64)
     L.mcx_last_error.restype = C.c_char_p
     L.mcx_version.restype = C.c_char_p
@@ -150,6 +153,7 @@ def lib():
     L.mcx_init_local.argtypes = [C.POINTER(Opts), C.c_int, vp, C.POINTER(C.c_void_p)]
     L.mcx_finalize.argtypes = [vp]
     L.mcx_get_info.argtypes = [vp, C.POINTER(Info)]
+    L.mcx_comm_info.argtypes = [vp, C.POINTER(C.c_int), C.POINTER(C.c_int), C.POINTER(C.c_int)]
     L.mcx_material_set.argtypes = [vp, C.c_int, C.c_double, C.c_double, C.c_double, C.c_double, C.c_int]
     L.mcx_get_displacement.argtypes = [vp, C.c_int]
     L.mcx_get_displacement.restype = C.c_double
@@ -342,6 +346,13 @@ class Macroc:
         inf = Info()
         _check(lib().mcx_get_info(self._ctx, C.byref(inf)), "mcx_get_info")
         return inf.as_dict()
+
+    def comm_info(self):
+        """(ranks in the communicator, this rank in it, HIP device): ncclCommCount /
+        ncclCommUserRank / ncclCommCuDevice for RCCL, the group for the in-process transport."""
+        n, r, d = C.c_int(), C.c_int(), C.c_int()
+        _check(lib().mcx_comm_info(self._ctx, C.byref(n), C.byref(r), C.byref(d)), "mcx_comm_info")
+        return n.value, r.value, d.value
 
     def nonlinear_stats(self):
         """micropp_C_get_non_linear_gps / get_f_trial_max of this rank."""

@@ -25,9 +25,16 @@ int exc_return(const char* fn, const char* what) {
   return MCX_EXC;
 }
 
-void test_inject(const char* fn) {
+// MCX_TEST_THROW (a comma list of entry names) is read once, when the library is loaded: no
+// getenv per call (not thread-safe against a concurrent setenv), nothing to do when it is unset
+static const std::string g_test_throw = [] {
   const char* e = std::getenv("MCX_TEST_THROW");
-  if (e && !std::strcmp(e, fn)) throw std::bad_alloc();
+  return e ? "," + std::string(e) + "," : std::string();
+}();
+
+void test_inject(const char* fn) {
+  if (!g_test_throw.empty() && g_test_throw.find("," + std::string(fn) + ",") != std::string::npos)
+    throw std::bad_alloc();
 }
 
 // padded node vectors (u, p and its buffers): the allocation is shifted by pad_off bytes so that
@@ -228,7 +235,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   if (lg) {
     lg->members[rank] = &c;
     MCX_HIP(hipMemcpy(lg->d_red_ptrs + rank, &c.red_loc, sizeof(double*), hipMemcpyHostToDevice));
-    if ((rc = group_barrier(lg, rank, BAR_INIT))) {
+    if ((rc = group_barrier(lg, rank, BAR_INIT, c.comm_timeout))) {
       lg->members[rank] = nullptr;
       return rc;
     }
@@ -353,7 +360,8 @@ using namespace mcx;
 extern "C" {
 
 const char* mcx_last_error(void) { return g_err.c_str(); }
-const char* mcx_version(void) { return "macroc_amd 0.1 (gfx950)"; }
+const char* mcx_version(void) { return "macroc_amd 0.3 (gfx950, abi 3)"; }
+int mcx_abi_version(void) { return MCX_ABI_VERSION; }
 
 void mcx_default_opts(mcx_opts* o) {
   std::memset(o, 0, sizeof(*o));
@@ -517,7 +525,7 @@ int mcx_finalize(void* ctx) try {
     // no member still copies from this context's buffers: every member drained its streams
     // before crossing.  If the group broke (a member stopped, or reached another collective),
     // the members' enqueued copies may still read these buffers: wait for the whole device.
-    if ((rc = group_barrier(c->lg, c->rank, BAR_FINALIZE))) (void)hipDeviceSynchronize();
+    if ((rc = group_barrier(c->lg, c->rank, BAR_FINALIZE, c->comm_timeout))) (void)hipDeviceSynchronize();
     c->lg->members[c->rank] = nullptr;
   }
   const std::string e = g_err;
@@ -592,6 +600,23 @@ int mcx_get_info(void* ctx, mcx_info* in) try {
   GUARD(ctx);
   CTX(ctx);
   fill_info(c, in);
+  return 0;
+} MCX_CATCH
+
+int mcx_comm_info(void* ctx, int* comm_ranks, int* comm_rank, int* device) try {
+  MCX_ENTRY();
+  GUARD(ctx);
+  CTX(ctx);
+  int n = 1, r = 0, d = c.device;
+  if (c.lg) {
+    n = c.lg->nranks;
+    r = c.rank;
+  } else if (int rc = comm_query(c, &n, &r, &d)) {
+    return rc;
+  }
+  if (comm_ranks) *comm_ranks = n;
+  if (comm_rank) *comm_rank = r;
+  if (device) *device = d;
   return 0;
 } MCX_CATCH
 
@@ -1491,16 +1516,20 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
   GUARD(ctx);
   CTX(ctx);
   if (!std::strcmp(name, "spmv_subl")) {
+    const int old = c.spmv_subl;
     c.spmv_subl = (int)value;
-    if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
+    if (!partials_fit(c)) {
+      c.spmv_subl = old;
       set_error("spmv_subl: partials buffer too small");
       return 2;
     }
     return 0;
   }
   if (!std::strcmp(name, "spmv_zblocks")) {
+    const int old = c.spmv_zblocks;
     c.spmv_zblocks = (int)value;
-    if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
+    if (!partials_fit(c)) {
+      c.spmv_zblocks = old;
       set_error("spmv_zblocks: partials buffer too small");
       return 2;
     }
@@ -1530,8 +1559,10 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
       set_error("split_tx: 0, 64, 128 or 256");
       return 2;
     }
+    const int old = c.split_tx;
     c.split_tx = v;
-    if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
+    if (!partials_fit(c)) {
+      c.split_tx = old;
       set_error("split_tx: partials buffer too small");
       return 2;
     }
@@ -1559,8 +1590,10 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
       set_error("split_ty: 0, 2, 4, 8 or 16");
       return 2;
     }
+    const int old = c.split_ty;
     c.split_ty = v;
-    if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
+    if (!partials_fit(c)) {
+      c.split_ty = old;
       set_error("split_ty: partials buffer too small");
       return 2;
     }
@@ -1625,12 +1658,24 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
     return 0;
   }
   if (!std::strcmp(name, "vi_st_faces")) {  // rebuilds the default-stencil structures if built
+    const int old = c.vi_st_faces;
     c.vi_st_faces = (int)value & 0x7f;  // 1: all 6 faces; else bit c = face class c (1..6)
-    if (c.st_ok && build_st(c)) return 1;
+    if ((c.st_ok || c.st_pending) && build_st(c)) return 1;
+    if (!partials_fit(c)) {
+      c.vi_st_faces = old;
+      set_error("vi_st_faces: partials buffer too small");
+      return (c.st_ok || c.st_pending) && build_st(c) ? 1 : 2;
+    }
     return 0;
   }
   if (!std::strcmp(name, "vi_st_tail")) {
+    const int old = c.vi_st_tail;
     c.vi_st_tail = value != 0.;
+    if (!partials_fit(c)) {
+      c.vi_st_tail = old;
+      set_error("vi_st_tail: partials buffer too small");
+      return 2;
+    }
     return 0;
   }
   if (!std::strcmp(name, "vi_st")) {  // takes effect at once if the structures were built (they are by default)
@@ -1638,11 +1683,24 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
       set_error("vi_st: -1 (by size), 0 or 1");
       return 1;
     }
+    const int old = c.vi_st;
     c.vi_st = (int)value;
+    if (c.st_pending && st_wanted(c) && build_st(c)) return 1;  // built lazily: the path turned on
+    if (!partials_fit(c)) {
+      c.vi_st = old;
+      set_error("vi_st: partials buffer too small");
+      return 2;
+    }
     return 0;
   }
   if (!std::strcmp(name, "vi_exc_kernel")) {
+    const bool old = c.vi_exc_kernel;
     c.vi_exc_kernel = value != 0.;
+    if (!partials_fit(c)) {
+      c.vi_exc_kernel = old;
+      set_error("vi_exc_kernel: partials buffer too small");
+      return 2;
+    }
     return 0;
   }
   if (!std::strcmp(name, "vi_lg_exc")) {
@@ -1689,7 +1747,7 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
     }
     const int old = c.vi_tx;
     c.vi_tx = v;
-    if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
+    if (!partials_fit(c)) {
       c.vi_tx = old;
       set_error("vi_tx: partials buffer too small");
       return 7;
@@ -1726,8 +1784,10 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
     return 0;
   }
   if (!std::strcmp(name, "vi_stage")) {
+    const int old = c.vi_stage;
     c.vi_stage = value < 0. ? -1 : (value != 0. ? 1 : 0);
-    if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
+    if (!partials_fit(c)) {
+      c.vi_stage = old;
       set_error("vi_stage: partials buffer too small");
       return 2;
     }
@@ -1764,8 +1824,10 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
     return 0;
   }
   if (!std::strcmp(name, "spmv_kernel")) {
+    const int old = c.spmv_kernel;
     c.spmv_kernel = (int)value;
-    if (2 * std::max(spmv_grid_blocks(c), node_blocks(c)) + 64 > c.partials_cap) {
+    if (!partials_fit(c)) {
+      c.spmv_kernel = old;
       set_error("spmv_kernel: partials buffer too small");
       return 2;
     }

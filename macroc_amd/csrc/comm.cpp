@@ -53,6 +53,18 @@ void comm_destroy(Ctx& c) {
   }
 }
 
+// the communicator as RCCL reports it (ncclCommCount / ncclCommUserRank / ncclCommCuDevice):
+// what the ranks actually joined, not what the caller asked for; no communicator: 1, 0, c.device
+int comm_query(Ctx& c, int* n, int* r, int* dev) {
+  *n = 1, *r = 0, *dev = c.device;
+  if (int rc = comm_check(c)) return rc;
+  if (!c.comm) return 0;
+  MCX_NCCL(ncclCommCount((ncclComm_t)c.comm, n));
+  MCX_NCCL(ncclCommUserRank((ncclComm_t)c.comm, r));
+  MCX_NCCL(ncclCommCuDevice((ncclComm_t)c.comm, dev));
+  return 0;
+}
+
 double comm_timeout_default() {
   const char* e = std::getenv("MCX_COMM_TIMEOUT");
   const double v = e ? std::atof(e) : 0.;
@@ -76,8 +88,11 @@ static const char* bar_name(int tag) {
 // arrival of the open generation breaks the group (the RCCL analogue is a mismatched collective,
 // which hangs).  A generation still open after timeout_s breaks it too (a member that stopped,
 // e.g. after an error of its own).  A broken group fails every later crossing at once, so no
-// member proceeds to read a peer's buffers on an exchange the peer is not part of.
-int group_barrier(LocalGroup* g, int rank, int tag) {
+// member proceeds to read a peer's buffers on an exchange the peer is not part of.  timeout_s <= 0:
+// the group's own deadline (MCX_COMM_TIMEOUT at creation); the collective entry points pass their
+// context's comm_timeout option.
+int group_barrier(LocalGroup* g, int rank, int tag, double timeout_s) {
+  if (timeout_s <= 0.) timeout_s = g->timeout_s;
   auto* m = static_cast<std::mutex*>(g->mtx);
   auto* cv = static_cast<std::condition_variable*>(g->cv);
   std::unique_lock<std::mutex> lk(*m);
@@ -103,10 +118,10 @@ int group_barrier(LocalGroup* g, int rank, int tag) {
     cv->notify_all();
     return 0;
   }
-  const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(g->timeout_s);
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::duration<double>(timeout_s);
   if (!cv->wait_until(lk, deadline, [&] { return g->generation != gen || g->broken; })) {
     g->broken = true;
-    g->why = "rank " + std::to_string(rank) + " waited " + std::to_string((int)g->timeout_s) + " s in " +
+    g->why = "rank " + std::to_string(rank) + " waited " + std::to_string((int)timeout_s) + " s in " +
              bar_name(tag) + ": " + std::to_string(g->count) + " of " + std::to_string(g->nranks) +
              " members arrived (a member stopped or skipped the collective)";
     cv->notify_all();
@@ -200,7 +215,7 @@ int halo_start(Ctx& c, double* xpad) {
     // the copies below overwrite my receive buffer: order them after my compute stream's last
     // reader of it (the previous halo's k_unpack), as the RCCL branch does
     MCX_HIP(hipStreamWaitEvent(c.comm_stream, g->ev_packed[c.rank], 0));
-    if (int rc = group_barrier(g, c.rank, BAR_HALO_PACKED)) return rc;
+    if (int rc = group_barrier(g, c.rank, BAR_HALO_PACKED, c.comm_timeout)) return rc;
     for (size_t t = 0; t < h.nbr_rank.size(); t++) {
       const Ctx& q = *g->members[h.nbr_rank[t]];
       size_t idx = 0;
@@ -216,7 +231,7 @@ int halo_start(Ctx& c, double* xpad) {
     MCX_HIP(hipEventRecord(g->ev_halo_done[c.rank], c.comm_stream));
     MCX_HIP(hipEventRecord(c.ev_comm, c.comm_stream));
     // every member recorded ev_halo_done before anyone waits on it again
-    if (int rc = group_barrier(g, c.rank, BAR_HALO_DONE)) return rc;
+    if (int rc = group_barrier(g, c.rank, BAR_HALO_DONE, c.comm_timeout)) return rc;
     return 0;
   }
   launch_pack(c, xpad);
@@ -255,11 +270,11 @@ static int allreduce_op(Ctx& c, const double* in, double* out, int count, int op
   if (c.lg) {
     LocalGroup* g = c.lg;
     MCX_HIP(hipEventRecord(g->ev_red[c.rank], c.stream));
-    if (int rc = group_barrier(g, c.rank, BAR_RED_IN)) return rc;
+    if (int rc = group_barrier(g, c.rank, BAR_RED_IN, c.comm_timeout)) return rc;
     for (int q = 0; q < g->nranks; q++) MCX_HIP(hipStreamWaitEvent(c.stream, g->ev_red[q], 0));
     launch_group_sum(c, (const double* const*)g->d_red_ptrs, g->nranks, count, out, op);
     MCX_HIP(hipEventRecord(g->ev_sum[c.rank], c.stream));
-    if (int rc = group_barrier(g, c.rank, BAR_RED_SUM)) return rc;
+    if (int rc = group_barrier(g, c.rank, BAR_RED_SUM, c.comm_timeout)) return rc;
     return 0;
   }
   MCX_NCCL(ncclAllReduce(in, out, count, ncclDouble, op ? ncclMax : ncclSum, (ncclComm_t)c.comm, c.stream));
@@ -323,7 +338,7 @@ extern "C" int mcx_local_group_barrier(void* group, int rank) try {
     set_error("mcx_local_group_barrier: bad arguments");
     return 1;
   }
-  return group_barrier(g, rank, BAR_USER);
+  return group_barrier(g, rank, BAR_USER, 0.);
 } MCX_CATCH
 
 extern "C" int mcx_comm_unique_id(void* id) try {

@@ -4880,7 +4880,7 @@ static bool st_auto(const Ctx& c) {
 bool st_used(const Ctx& c) {
   int tx, ty;
   vis_shape(c, tx, ty);
-  return (c.vi_st == 1 || (c.vi_st < 0 && st_auto(c))) && c.st_ok && c.fmt == FMT_VI && c.vi_block && vi_staged(c) && c.vi_fma && c.vi_uni && c.vi_patch &&
+  return st_wanted(c) && c.st_ok && c.fmt == FMT_VI && c.vi_block && vi_staged(c) && c.vi_fma && c.vi_uni && c.vi_patch &&
          tx == 64 && !fusep(c);
 }
 
@@ -4899,6 +4899,16 @@ int64_t spmv_nparts(const Ctx& c) {
   if (c.fmt == FMT_SPLIT && c.dsl.dense) return node_blocks(c);
   return spmv_grid_blocks(c) + faces_blocks(c) + exc_blocks(c) + stface_blocks(c);
 }
+
+// the SpMV's partial sums (every kernel of one SpMV, the face / listed / exception blocks included)
+// and the node-block partials fit one half of the partials buffer: the fused update kernels read
+// the SpMV's half while they write the other (partials2), so an SpMV spilling past the half would
+// corrupt the p.Ap / z.r sums
+bool partials_fit(const Ctx& c) {
+  return std::max(spmv_nparts(c), node_blocks(c)) + 32 <= c.partials_cap / 2;
+}
+
+bool st_wanted(const Ctx& c) { return c.vi_st == 1 || (c.vi_st < 0 && st_auto(c)); }
 
 int upload_constants(Ctx& c) {
   double B[8][6][24];
@@ -5360,9 +5370,16 @@ int build_wdesc(Ctx& c) {
 
 // default-stencil structures (k_spmv_st): the stencil of the middle node, the list of the other
 // nodes (ordered compaction), the patch masks; one host round trip for the list's length
+// Built lazily: only when the SpMV would take the path (vi_st 1, or -1 by size); else
+// marked pending, and the vi_st option handler builds them when it turns the path on.
 int build_st(Ctx& c) {
   c.st_ok = false;
+  c.st_pending = false;
   if (!(c.fmt == FMT_VI && c.vi_block && vi_staged(c) && c.g.nown > 0)) return 0;
+  if (!st_wanted(c)) {
+    c.st_pending = true;
+    return 0;
+  }
   const int npx = (c.g.nx + 15) / 16, npy = (c.g.ny + 3) / 4;
   const int64_t nwp = (int64_t)npx * npy * c.g.nz;
   if (!c.st_coef) {
@@ -5412,6 +5429,7 @@ int build_st(Ctx& c) {
                      !(ax == 1 && g.ny == 1 && q == 4) && !(ax == 2 && g.nz == 1 && q == 6);
     c.st_faces.u[q] = c.st_faces.u[q - 1] + (use ? (int64_t)((nfast + 63) / 64) * ((nslow + SFP_S - 1) / SFP_S) : 0);
   }
+  if (c.st_ok && !partials_fit(c)) c.st_ok = false;  // its partials would spill into partials2: k_spmv_vibm
   return 0;
 }
 

@@ -138,7 +138,7 @@ struct LocalGroup {
 };
 // barrier tags (which collective a crossing belongs to)
 enum { BAR_INIT = 1, BAR_HALO_PACKED, BAR_HALO_DONE, BAR_RED_IN, BAR_RED_SUM, BAR_FINALIZE, BAR_USER };
-int group_barrier(LocalGroup* g, int rank, int tag);  // 0, or 23 with the reason in mcx_last_error
+int group_barrier(LocalGroup* g, int rank, int tag, double timeout_s);  // 0, or 23 with the reason in mcx_last_error
 double comm_timeout_default();                       // MCX_COMM_TIMEOUT, default 300 s
 
 struct Ctx {
@@ -275,6 +275,7 @@ struct Ctx {
   int64_t st_mask_bytes = 0, st_n = 0;
   int st_npx = 0, st_npy = 0;
   bool st_ok = false;                   // built for the current block indices
+  bool st_pending = false;              // not built: the last assembly's SpMV did not want the path
   unsigned st_fm = 0;                   // bit c: stencil class c usable (k_st_setup)
   StFaces st_faces = {};                // the face phase's units per class
   int vi_exc_kernel = 1;     // staged SpMV: exception rows in their own kernel after the march (k_spmv_exc, option
@@ -374,6 +375,7 @@ int allreduce_prepare(Ctx& c);
 // aborts the communicator on either; one rank without a communicator waits plainly
 int comm_wait(Ctx& c, hipEvent_t ev, const char* what);
 int comm_check(Ctx& c);  // a communicator aborted earlier: fail the collective
+int comm_query(Ctx& c, int* n, int* r, int* dev);  // ncclCommCount / UserRank / CuDevice (1, 0, device: none)
 int group_setup(Ctx& c);  // the in-process group's events (first member on the device)
 void launch_group_sum(Ctx& c, const double* const* ptrs, int nranks, int count, double* out, int op = 0);
 void launch_vtu_cells(Ctx& c, const int* lo, const int* cnt, double* out);
@@ -406,7 +408,9 @@ void launch_unpack(Ctx& c, double* xpad);
 void launch_copy_owned_to_pad(Ctx& c, const double* owned, double* pad);
 void launch_copy_pad_to_owned(Ctx& c, const double* pad, double* owned);
 int64_t spmv_grid_blocks(const Ctx& c);
-int64_t spmv_nparts(const Ctx& c);   // partial sums the CG's SpMV leaves (its own grid, or the dense pass's)
+int64_t spmv_nparts(const Ctx& c);
+bool partials_fit(const Ctx& c);     // the SpMV's and the node blocks' partials fit half the buffer
+bool st_wanted(const Ctx& c);        // option vi_st asks for the default-stencil SpMV   // partial sums the CG's SpMV leaves (its own grid, or the dense pass's)
 int64_t node_blocks(const Ctx& c);
 bool vi_staged(const Ctx& c);
 int build_wdesc(Ctx& c);    // wave descriptors of the block-indexed storage (after build_vi)

@@ -4,6 +4,7 @@ import glob
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -90,23 +91,47 @@ def test_init_without_gpu_fails_loudly():
         M.Macroc(["-da_grid_x", "4", "-da_grid_y", "4", "-da_grid_z", "2"])
 
 
-def test_no_exception_crosses_the_abi(monkeypatch):
-    """every extern "C" entry is a function-try-block.  MCX_TEST_THROW=<entry>
-    makes that entry throw std::bad_alloc at its start (the failure of an absurd host allocation);
-    the caller gets code 90 and the message instead of std::terminate killing the process."""
+def test_no_exception_crosses_the_abi():
+    """every extern "C" entry is a function-try-block.  MCX_TEST_THROW=<entries>
+    (read once when the library loads: ADVICE r05) makes those entries throw std::bad_alloc at their
+    start (the failure of an absurd host allocation); the caller gets code 90 and the message
+    instead of std::terminate killing the process.  Run in a child process that loads the library
+    with the variable set; this process (loaded without it) is unaffected."""
+    fns = ["mcx_plan", "mcx_parse_args", "mcx_init", "mcx_local_group_create"]
+    code = f"""
+import ctypes as C, sys
+sys.path.insert(0, {ROOT!r})
+import macroc_amd as M
+L = M.lib()
+o = M.Opts(); L.mcx_default_opts(C.byref(o))
+inf = M.Info()
+calls = {{"mcx_plan": lambda: L.mcx_plan(C.byref(o), 0, 1, C.byref(inf)),
+          "mcx_parse_args": lambda: L.mcx_parse_args(C.byref(o), 0, None),
+          "mcx_init": lambda: L.mcx_init(C.byref(o), 0, 1, None, C.byref(C.c_void_p())),
+          "mcx_local_group_create": lambda: L.mcx_local_group_create(2, 0, C.byref(C.c_void_p()))}}
+for fn, call in calls.items():
+    rc = call()
+    msg = L.mcx_last_error().decode()
+    assert rc == 90 and fn in msg and "bad_alloc" in msg, (fn, rc, msg)
+assert L.mcx_get_info(None, C.byref(inf)) != 90  # an entry not listed does not throw
+print("ok")
+"""
+    env = dict(os.environ, MCX_TEST_THROW=",".join(fns))
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stdout + out.stderr
     L = M.lib()
     o = M.parse_args(["-da_grid_x", 8, "-da_grid_y", 8, "-da_grid_z", 8])
     inf = M.Info()
-    for fn, call in (("mcx_plan", lambda: L.mcx_plan(M.C.byref(o), 0, 1, M.C.byref(inf))),
-                     ("mcx_parse_args", lambda: L.mcx_parse_args(M.C.byref(o), 0, None)),
-                     ("mcx_init", lambda: L.mcx_init(M.C.byref(o), 0, 1, None, M.C.byref(M.C.c_void_p()))),
-                     ("mcx_local_group_create", lambda: L.mcx_local_group_create(2, 0, M.C.byref(M.C.c_void_p())))):
-        monkeypatch.setenv("MCX_TEST_THROW", fn)
-        assert call() == 90, fn
-        msg = L.mcx_last_error().decode()
-        assert fn in msg and "bad_alloc" in msg, msg
-        monkeypatch.delenv("MCX_TEST_THROW")
     assert L.mcx_plan(M.C.byref(o), 0, 1, M.C.byref(inf)) == 0 and inf.nx == 8
+
+
+def test_abi_version_and_comm_info_without_context():
+    """the struct-carrying entries changed size in round 5; the library reports its ABI
+    revision (the mirror refuses another), and mcx_comm_info rejects a NULL context."""
+    L = M.lib()
+    assert L.mcx_abi_version() == M.ABI_VERSION == 3
+    assert "abi 3" in L.mcx_version().decode()
+    assert L.mcx_comm_info(None, None, None, None) != 0
 
 
 def test_local_group_withheld_member_fails_within_deadline(monkeypatch):

@@ -4,7 +4,9 @@ bootstraps a communicator id the way bench.py does (broadcast_object_list), exch
 values with gloo send/recv in the plan's message order, and runs a distributed PETSc-CG
 (Jacobi) on its owned rows of the oracle's matrix.  The gathered solution must match the
 single-process oracle solve."""
+import json
 import os
+import subprocess
 import socket
 import sys
 
@@ -175,3 +177,35 @@ def test_gloo_world2_warmup_guard_is_collective():
         p.join(60)
         assert p.exitcode == 0
     assert res == [(0, False, True), (1, False, True)]
+
+
+def _bench(args, env=None, timeout=300):
+    e = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                          timeout=timeout, env=e, cwd=ROOT)
+
+
+def test_bench_gpus_flag_starts_the_ranks():
+    """`python bench.py --gpus 2` without a launcher starts two ranks itself
+    (torch.distributed.run, 127.0.0.1); in --dry-run they bootstrap over gloo and rank 0 reports
+    the ranks that joined -- never a one-rank line."""
+    out = _bench(["--gpus", "2", "--dry-run"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = json.loads(out.stdout.strip().splitlines()[-1])
+    assert line == {"dry_run": True, "n_gpus": 2, "world_size": 2}, line
+    assert "starting 2 ranks" in out.stderr and "[rank 1] dry run" in out.stderr
+
+
+def test_bench_gpus_flag_fails_loudly():
+    """Without enough GPUs, or under a launcher whose WORLD_SIZE differs, --gpus N exits non-zero with
+    the reason instead of measuring one GPU and printing n_gpus 1."""
+    if not os.path.exists("/dev/kfd"):
+        out = _bench(["--gpus", "2"])
+        assert out.returncode != 0 and "--gpus 2 but 0 GPU(s) are visible" in out.stderr, out.stderr[-2000:]
+        assert not out.stdout.strip()
+    out = _bench(["--gpus", "1"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert out.returncode != 0 and "--gpus 1 but the launcher started WORLD_SIZE=2" in out.stderr, out.stderr[-2000:]
+    assert not out.stdout.strip()
