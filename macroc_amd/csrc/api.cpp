@@ -1550,7 +1550,7 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
     return 0;
   }
   if (!std::strcmp(name, "split_dbg")) {
-    c.split_dbg = std::max(0, std::min(3, (int)value));
+    c.split_dbg = std::max(0, std::min(63, (int)value));  // (k_spmv_sp DBG: bits, see the kernel)
     return 0;
   }
   if (!std::strcmp(name, "split_tx")) {
@@ -1666,6 +1666,10 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
       set_error("vi_st_faces: partials buffer too small");
       return (c.st_ok || c.st_pending) && build_st(c) ? 1 : 2;
     }
+    return 0;
+  }
+  if (!std::strcmp(name, "vi_st_pair")) {  // the same grid and partials either way
+    c.vi_st_pair = value != 0.;
     return 0;
   }
   if (!std::strcmp(name, "vi_st_tail")) {

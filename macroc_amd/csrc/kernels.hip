@@ -3457,6 +3457,321 @@ __global__ __launch_bounds__(SFP_T) void k_spmv_face(Geo g, StFaces sf, const do
   }
 }
 
+// ------------------------------------------------------- default-stencil SpMV, x-pair lanes (round 6)
+// k_spmv_st (one node per lane, nodes k and k+1) read each node's 81 x values from LDS as 8-B reads
+// and stored y as 8-B lane stores 24 B apart.  k_spmv_sp: every lane computes two x-adjacent nodes
+// of ONE plane; the x row (dy, dz) both need is 4 nodes = 12 doubles, six 16-B LDS reads (the pair's
+// 48-B lane stride keeps them 16-B aligned; a wave row is 32 lanes = 64 nodes, so every 16-lane group
+// of a ds_read_b128 lies in one staged row and covers the 16 bank slots 3 l mod 16: conflict-free
+// for any row pitch).  The block marches a 64 x 16 tile two planes per step with the same 4-slot x
+// ring and blocks -> tiles map as k_spmv_st (z-chunks, XCD slabs): waves 0-7 compute plane k, waves
+// 8-15 plane k+1, a wave two tile rows.  y leaves through LDS: a wave row's 64 nodes (192 doubles) are
+// written to a per-wave scratch and read back lane-consecutively, so every store instruction writes
+// 512 B of whole lines -- the pair's three 16-B stores 48 B apart wrote partial lines (measured: the
+// march's y stores alone 257 us with non-temporal partial-line stores, profiles/r06i_*).  The rows are
+// the fused multiply-adds of k_spmv_st / k_spmv_vibm / k_spmv_face in (nb, c) order, so y is bitwise
+// theirs; face and listed nodes (k_st_mask's 16 x 4 patch masks) are left to k_spmv_face.
+constexpr int SP_RLP = 200;
+// FP (the CG's p update fused into the march, option cg_fusep; single rank, no exception nodes, as
+// k_spmv_vibm's FP): the ring is staged from r, the Jacobi index byte and p(i-1) instead of x,
+// p(i) = z + beta p(i-1) with z = D^-1 r (k_cg_pupdate's expression, so p is bitwise the
+// unfused update's), written to p's buffer i & 1 for the tile's own nodes and multiplied in the
+// same step; k_spmv_face then reads that buffer.
+
+template <bool DOT, bool GATED, bool FP = false, int DBG = 0>
+__global__ __launch_bounds__(1024) void k_spmv_sp(Geo g, const double* __restrict__ coef,
+                                                  const unsigned long long* __restrict__ mask, int npx, int npy,
+                                                  const double* __restrict__ x, double* __restrict__ y,
+                                                  double* __restrict__ part, const CgState* __restrict__ cg,
+                                                  ZTiling zt, FusedP fp = {}) {
+  constexpr int TX = 64, TY = 16, T = 1024, RW = 3 * (TX + 2), RLP = SP_RLP, PR = TY + 2, PLANE = PR * RLP;
+  constexpr int SR = T / RW, NL = (PR + SR - 1) / SR;  // staged rows per pass (5), passes (4)
+  static_assert(RLP >= RW && RLP % 2 == 0, "ring rows: 198 doubles, 16-B aligned");
+  __shared__ __attribute__((aligned(16))) double xs[4 * PLANE];
+  __shared__ __attribute__((aligned(16))) double ysc[T / 64][3 * TX];  // per wave: one tile row's y
+  __shared__ double sh[T / 64];
+  __shared__ double s9[27];  // value 8 of the default stencil's blocks
+  __shared__ double s_jdd[FP ? 3 * VI_MAX : 1];
+  if (GATED && cg->reason) return;
+  const int b = blockIdx.x;
+  const int xcd = b & 7, t8 = b >> 3;
+  const int slab = (zt.nty + 7) >> 3;
+  const int ty0 = xcd * slab;
+  const int nty_here = min(slab, zt.nty - ty0);
+  const int per = max(nty_here, 0) * zt.ntx * zt.nzc;
+  const int me = threadIdx.x;
+  double dot = 0.;
+  if (t8 >= per) {  // whole block idle (uniform): its partial only
+    if (DOT) {
+      const double s = block_sum<T>(dot, sh);
+      if (threadIdx.x == 0) part[blockIdx.x] = s;
+    }
+    return;
+  }
+  const int txi = t8 % zt.ntx, r8 = t8 / zt.ntx;
+  const int tyi = ty0 + r8 % nty_here, zc = r8 / nty_here;
+  const int i0 = txi * TX, j0 = tyi * TY;
+  const int k0 = zc * zt.kc, k1 = min(g.nz, k0 + zt.kc);
+  if (me < 27) s9[me] = coef[me * VIB_STRIDE + 8];
+  // FP: the CG step's scalars and p's buffers of this iteration
+  const int cgi = FP ? cg->i : 0;
+  const double cb = FP ? cg->bcoef : 0.;
+  const double* psrc = FP ? fp.pb[(cgi & 1) ^ 1] : x;
+  double* pdst = FP ? fp.pb[cgi & 1] : nullptr;
+  if (FP)
+    for (int t = me; t < 3 * VI_MAX; t += T) s_jdd[t] = fp.jdd[t];
+  const int wv = me >> 6, ln = me & 63;
+  const int h = __builtin_amdgcn_readfirstlane(wv >> 3), w8 = __builtin_amdgcn_readfirstlane(wv & 7);
+  const int rw = ln >> 5;          // the lane's row of the wave's two (plane k + h, tile rows 2 w8, 2 w8 + 1)
+  const int ix = 2 * (ln & 31);    // tile x of the lane's first node
+  const int ly = 2 * w8 + rw;
+  // k_st_mask's 16 x 4 patches of the wave's rows: patch row gpy, patch columns gpx0 .. gpx0 + 3;
+  // bits 16 q .. 16 q + 15 of a row's patch word: the row's nodes in patch row position q
+  const int gpx0 = i0 >> 4, gpy = (j0 >> 2) + (w8 >> 1), q0 = (2 * w8) & 3;  // (uniform)
+  const int PX = g.PX, PXY = g.PX * g.PY;
+  const int len = 3 * min(TX + 2, g.nx + 2 - i0);
+  const int rows = min(TY + 2, g.ny + 2 - j0);
+  // Staging map (plane-invariant): threads 0 .. SR RW - 1 stage, thread t the column so = t % RW of
+  // the rows sr0 + SR m (sr0 = t / RW, m = 0 .. NL-1): every element's addresses are affine in m and
+  // in the plane, so staging costs a few adds per element instead of a division chain
+  const bool stg = me < SR * RW;
+  const int so = me % RW, sr0 = me / RW;
+  const bool sx = stg && so < len;                     // the column exists in the padded box
+  const int spo = 3 * (i0 + (j0 + sr0) * PX) + so;     // padded offset of element 0 within its plane
+  const int sro = sr0 * RLP + so;                      // its ring offset
+  const int64_t PXY3 = 3 * (int64_t)PXY;
+  auto srow = [&](int m) { return sx && sr0 + SR * m < rows; };
+  auto xload = [&](int p, int m) -> double {  // x of padded plane p + 1 (p = -1 .. nz)
+    if (!srow(m) || p > g.nz) return 0.;
+    return x[(int64_t)(p + 1) * PXY3 + spo + 3 * SR * m * PX];
+  };
+  auto xstore = [&](int slot, int m, double v) {
+    if (stg && sr0 + SR * m < PR) xs[slot * PLANE + sro + SR * m * RLP] = v;
+  };
+  // FP: the element's owned node (else the zero ghost layer); jx carries 0x100 = owned node,
+  // 0x200 = one of this tile's own nodes (its p is written)
+  const int sgi = i0 - 1 + so / 3, sd = so - 3 * (so / 3);
+  const bool sox = sgi >= 0 && sgi < g.nx, stx = sgi >= i0 && sgi < i0 + TX;
+  struct Fe {
+    double po, rv;
+    unsigned jx;
+  };
+  auto fload = [&](int p, int m, Fe& f) {
+    f.po = f.rv = 0.;
+    f.jx = 0u;
+    const int gj = j0 - 1 + sr0 + SR * m;
+    if (!srow(m) || !sox || gj < 0 || gj >= g.ny || p < 0 || p >= g.nz) return;
+    const int64_t n = sgi + (int64_t)g.nx * (gj + (int64_t)g.ny * p);
+    f.rv = fp.r[3 * n + sd];
+    f.jx = fp.jix[n] | 0x100u | (stx && gj >= j0 && gj < j0 + TY && p >= k0 && p < k1 ? 0x200u : 0u);
+    if (cgi > 0) f.po = psrc[(int64_t)(p + 1) * PXY3 + spo + 3 * SR * m * PX];
+  };
+  // p(i) of a staged element (k_cg_pupdate's expression: z = D^-1 r, p = z (i = 0) or z + beta p(i-1));
+  // a tile's own node's p goes to p's buffer of this iteration
+  auto fpn = [&](int p, int m, const Fe& f) -> double {
+    const double z = f.rv * s_jdd[3 * (f.jx & 255u) + sd];
+    const double pn = cgi == 0 ? z : z + cb * f.po;
+    if (f.jx & 0x200u) pdst[(int64_t)(p + 1) * PXY3 + spo + 3 * SR * m * PX] = pn;
+    return (f.jx & 0x100u) ? pn : 0.;
+  };
+  // prologue: planes k0-1 .. k0+2 in ring slots 0 .. 3, every load issued before the first store
+  // (one memory round trip, not one per element)
+  if (FP) {
+    __syncthreads();  // s_jdd
+#pragma unroll
+    for (int s2 = 0; s2 < 2; s2++) {
+      Fe fe[2][NL];
+#pragma unroll
+      for (int s = 0; s < 2; s++)
+#pragma unroll
+        for (int m = 0; m < NL; m++) fload(k0 - 1 + 2 * s2 + s, m, fe[s][m]);
+#pragma unroll
+      for (int s = 0; s < 2; s++)
+#pragma unroll
+        for (int m = 0; m < NL; m++) xstore(2 * s2 + s, m, fpn(k0 - 1 + 2 * s2 + s, m, fe[s][m]));
+    }
+  } else {
+    double v[4][NL];
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+#pragma unroll
+      for (int m = 0; m < NL; m++) v[s][m] = xload(k0 - 1 + s, m);
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+#pragma unroll
+      for (int m = 0; m < NL; m++) xstore(s, m, v[s][m]);
+  }
+  __syncthreads();
+  typedef double d2v __attribute__((ext_vector_type(2)));
+  typedef const __attribute__((address_space(3))) d2v lds_d2v;
+  lds_d2v* xs2 = (lds_d2v*)&xs[0];
+  // DBG (timing-only diagnostics, option split_dbg; wrong products): 1 = one row's coefficients
+  // loaded once before the march (no scalar loads in the row loop), 2 = no x reads in the row loop
+  // (the lane's x fixed), 3 = both
+  double dav[(DBG & 1) ? 27 : 1], dxw[(DBG & 2) ? 12 : 1];
+  if constexpr ((DBG & 1) != 0) {
+#pragma unroll
+    for (int q = 0; q < 27; q++) dav[q] = coef[(q / 9) * VIB_STRIDE + q % 9];
+  }
+  if constexpr ((DBG & 2) != 0) {
+#pragma unroll
+    for (int q = 0; q < 12; q++) dxw[q] = xs[q + ln];
+  }
+  // y of the wave's two rows from the last step, transposed (yd[r2][q]: double q 64 + lane of row
+  // r2), stored at the start of the next step before its loads: the stores then have the whole
+  // row phase to complete before the step's wait for its loads (vmcnt counts loads and stores in
+  // issue order) instead of holding the barrier
+  double yd[2][3] = {{0., 0., 0.}, {0., 0., 0.}};
+  unsigned long long lvd[2] = {0ull, 0ull};
+  int64_t ybd[2] = {0, 0};
+  bool pend = false;  // (uniform)
+  auto ystore = [&]() {
+    if (!pend || (DBG & 32)) return;
+#pragma unroll
+    for (int r2 = 0; r2 < 2; r2++)
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        const int d = q * 64 + ln;  // double d of the row: node d / 3
+        if ((lvd[r2] >> (d / 3)) & 1ull) {
+          if (DBG & 16) y[ybd[r2] + d] = yd[r2][q];
+          else __builtin_nontemporal_store(yd[r2][q], &y[ybd[r2] + d]);
+        }
+      }
+    pend = false;
+  };
+  for (int k = k0; k < k1; k += 2) {
+    const bool more = k + 2 < k1;
+    const int kk = k + h;
+    const bool act = kk < k1;  // (uniform per wave) an odd last plane: waves 8-15 idle
+    double xr[2][NL];
+    Fe fe[2][FP ? NL : 1];
+    ystore();
+    if (more && !(DBG & 4)) {  // planes k+3 and k+4, in flight during the step
+#pragma unroll
+      for (int m = 0; m < NL; m++) {
+        if (FP) {
+          fload(k + 3, m, fe[0][m]);
+          fload(k + 4, m, fe[1][m]);
+        } else {
+          xr[0][m] = xload(k + 3, m);
+          xr[1][m] = xload(k + 4, m);
+        }
+      }
+    }
+    if ((DBG & 4) && more) {
+#pragma unroll
+      for (int m = 0; m < NL; m++) xr[0][m] = xr[1][m] = 0.;
+    }
+    if (act) {
+      // the live nodes of the wave's two rows (bit x: node i0 + x is marched; faces, listed rows and
+      // nodes outside the domain are not): from the 4 patch masks, scalar
+      unsigned long long lv[2] = {0ull, 0ull};
+#pragma unroll
+      for (int p4 = 0; p4 < 4; p4++) {
+        unsigned long long mk = ~0ull;
+        if (gpx0 + p4 < npx && gpy < npy) mk = mask[((int64_t)kk * npy + gpy) * npx + gpx0 + p4];
+#pragma unroll
+        for (int r2 = 0; r2 < 2; r2++) lv[r2] |= ((~mk >> (16 * (q0 + r2))) & 0xffffull) << (16 * p4);
+      }
+      const unsigned long long lvr = rw ? lv[1] : lv[0];
+      const bool live0 = (lvr >> ix) & 1ull, live1 = (lvr >> (ix + 1)) & 1ull;
+      double y00 = 0., y01 = 0., y02 = 0., y10 = 0., y11 = 0., y12 = 0.;
+      // a rolled loop over the 9 stencil rows (see k_spmv_st: unrolled, the compiler hoists the
+      // rows' scalar loads and spills)
+#pragma unroll 1
+      for (int g9 = 0; g9 < ((DBG & 8) ? 0 : 9); g9++) {  // stencil row (dy, dz): blocks nb = 3 g9 .. 3 g9 + 2
+        const int dy = g9 % 3 - 1, dz = g9 / 3 - 1;
+        double av[27], xw[12];
+        if constexpr ((DBG & 1) != 0) {
+#pragma unroll
+          for (int q = 0; q < 27; q++) av[q] = dav[q];
+        } else {
+#pragma unroll
+          for (int t = 0; t < 3; t++) {
+#pragma unroll
+            for (int q = 0; q < 8; q++) av[t * 9 + q] = coef[(g9 * 3 + t) * VIB_STRIDE + q];
+            av[t * 9 + 8] = s9[g9 * 3 + t];
+          }
+        }
+        // nodes ix-1 .. ix+2 of the row: 12 doubles, six 16-B reads
+        const int ro = (((kk + dz - k0 + 1) & 3) * PLANE + (ly + 1 + dy) * RLP + 3 * ix) >> 1;
+        if constexpr ((DBG & 2) != 0) {
+#pragma unroll
+          for (int q = 0; q < 12; q++) xw[q] = dxw[q] + (double)g9;
+        } else {
+#pragma unroll
+          for (int q = 0; q < 6; q++) {
+            const d2v v = xs2[ro + q];
+            xw[2 * q] = v.x;
+            xw[2 * q + 1] = v.y;
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int t = 0; t < 3; t++) {
+#pragma unroll
+          for (int q = 0; q < 9; q++) {
+            const int r = q / 3, cc = q % 3;
+            const double a = av[t * 9 + q];
+            double& ya = r == 0 ? y00 : (r == 1 ? y01 : y02);
+            double& yb = r == 0 ? y10 : (r == 1 ? y11 : y12);
+            ya = __builtin_fma(a, xw[3 * t + cc], ya);
+            yb = __builtin_fma(a, xw[3 * t + 3 + cc], yb);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // y through the wave's scratch: row r2's 32 lanes write their pairs (6 doubles, 48 B apart),
+      // then all 64 lanes take 3 lane-consecutive doubles each (stored next step as whole 512-B runs)
+      typedef __attribute__((address_space(3))) d2v lds_d2vw;
+      typedef __attribute__((address_space(3))) double lds_dw;
+      lds_d2vw* ys2 = (lds_d2vw*)&ysc[wv][0];
+      const lds_dw* ys1 = (const lds_dw*)&ysc[wv][0];
+#pragma unroll
+      for (int r2 = 0; r2 < 2; r2++) {
+        if (rw == r2) {
+          ys2[3 * (ln & 31) + 0] = d2v{y00, y01};
+          ys2[3 * (ln & 31) + 1] = d2v{y02, y10};
+          ys2[3 * (ln & 31) + 2] = d2v{y11, y12};
+        }
+#pragma unroll
+        for (int q = 0; q < 3; q++) yd[r2][q] = ys1[q * 64 + ln];
+        lvd[r2] = lv[r2];
+        ybd[r2] = 3 * ((int64_t)i0 + g.nx * ((int64_t)(j0 + 2 * w8 + r2) + (int64_t)g.ny * kk));
+      }
+      pend = true;
+      if (DOT) {  // p.w with the nodes' own x from the ring (block 13 of the rows: not kept live)
+        const int rc = (((kk - k0 + 1) & 3) * PLANE + (ly + 1) * RLP + 3 * ix) >> 1;
+        const d2v c0 = xs2[rc + 1], c1 = xs2[rc + 2], c2 = xs2[rc + 3], c3 = xs2[rc + 4];
+        // c0 = (x[2], x[3]) ... : node 0's x at doubles 3..5, node 1's at 6..8 of the row segment
+        if (live0) dot += c0.y * y00 + c1.x * y01 + c1.y * y02;
+        if (live1) dot += c2.x * y10 + c2.y * y11 + c3.x * y12;
+      }
+    }
+    if (more) {  // (uniform) planes k+3, k+4 replace k-1, k (no longer read)
+      if (FP) {  // their p before the barrier (the loads landed during the rows): off the barrier's path
+#pragma unroll
+        for (int m = 0; m < NL; m++) {
+          xr[0][m] = fpn(k + 3, m, fe[0][m]);
+          xr[1][m] = fpn(k + 4, m, fe[1][m]);
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int m = 0; m < NL; m++) {
+        xstore((k + 3 - k0 + 1) & 3, m, xr[0][m]);
+        xstore((k + 4 - k0 + 1) & 3, m, xr[1][m]);
+      }
+      __syncthreads();
+    }
+  }
+  ystore();
+  if (DOT) {
+    const double s = block_sum<T>(dot, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+  }
+}
+
 // Stencil classes of the default-stencil SpMV: 0 the interior (marched), 1/2 the x-lo/x-hi domain
 // face, 3/4 y-lo/y-hi, 5/6 z-lo/z-hi (an owned node on exactly one face of the GLOBAL domain: the
 // face phase st_faces; a node on two or three is an edge / corner node and always listed).  On the
@@ -4865,6 +5180,7 @@ static int64_t faces_blocks(const Ctx& c) {
 }
 
 bool fusep(const Ctx& c);
+bool st_fusep(const Ctx& c);
 
 // the default-stencil SpMV (k_spmv_st + k_spmv_face): FMA rows on the 64 x 16 staged tiles with the
 // scalar-dictionary patches, not the fused p update
@@ -4881,8 +5197,11 @@ bool st_used(const Ctx& c) {
   int tx, ty;
   vis_shape(c, tx, ty);
   return st_wanted(c) && c.st_ok && c.fmt == FMT_VI && c.vi_block && vi_staged(c) && c.vi_fma && c.vi_uni && c.vi_patch &&
-         tx == 64 && !fusep(c);
+         tx == 64 && (!fusep(c) || st_fusep(c));
 }
+
+// the fused p update on the default-stencil path: k_spmv_sp's FP instantiation (not k_spmv_st, not the tail)
+bool st_fusep(const Ctx& c) { return c.vi_st_pair && !c.vi_st_tail; }
 
 // k_spmv_face's blocks (the face phase and the listed rows as a kernel of their own: vi_st_tail 0)
 static int64_t stface_blocks(const Ctx& c) {
@@ -5637,6 +5956,18 @@ static void launch_spmv_fusep(Ctx& c, double* y) {
   fp.jix = c.jix;
   fp.pb[0] = c.p_pad;
   fp.pb[1] = c.p_pad2;
+  if (st_used(c)) {  // the default-stencil march with the p update (k_spmv_sp FP), then the faces and
+                     // listed rows from p's buffer of this iteration (the host's count cg_it is the
+                     // device's cg->i for every iteration that runs; finished ones return at once)
+    hipLaunchKernelGGL((k_spmv_sp<true, true, true>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,
+                       c.st_npx, c.st_npy, nullptr, y, c.partials, c.cg, zt, fp);
+    const int64_t nbfa = stface_blocks(c);
+    if (nbfa)
+      hipLaunchKernelGGL((k_spmv_face<true, true>), dim3((unsigned)nbfa), dim3(SFP_T), 0, c.stream, c.g, c.st_faces,
+                         c.st_coef, c.st_slot, c.cg_it & 1 ? c.p_pad2 : c.p_pad, y, c.partials + nb, c.cg, c.st_list,
+                         c.st_n, I, c.vi_bdict, c.vi_exc);
+    return;
+  }
 #define MCX_VIBM_FP(TXV, TYV, FV)                                                                                   \
   hipLaunchKernelGGL((k_spmv_vibm<true, true, TXV, TYV, true, true, true, FV, true>), dim3(nb), dim3(1024), 0,        \
                      c.stream, c.g, I, c.vi_bdict, c.p_pad, y, c.partials, c.cg, zt, fp)
@@ -5650,6 +5981,32 @@ static void launch_spmv_fusep(Ctx& c, double* y) {
     else MCX_VIBM_FP(64, 16, false);
   }
 #undef MCX_VIBM_FP
+}
+
+// k_spmv_sp's timing-only diagnostic instantiations (option split_dbg; wrong products, see DBG)
+template <bool DV, bool GV, int D>
+static void sp_dbg1(Ctx& c, int nb, const double* xpad, double* y, const ZTiling& zt) {
+  hipLaunchKernelGGL((k_spmv_sp<DV, GV, false, D>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,
+                     c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);
+}
+template <bool DV, bool GV>
+static void sp_dbg(Ctx& c, int nb, const double* xpad, double* y, const ZTiling& zt) {
+  switch (zt.dbg) {
+    case 1: sp_dbg1<DV, GV, 1>(c, nb, xpad, y, zt); break;
+    case 2: sp_dbg1<DV, GV, 2>(c, nb, xpad, y, zt); break;
+    case 3: sp_dbg1<DV, GV, 3>(c, nb, xpad, y, zt); break;
+    case 4: sp_dbg1<DV, GV, 4>(c, nb, xpad, y, zt); break;
+    case 8: sp_dbg1<DV, GV, 8>(c, nb, xpad, y, zt); break;
+    case 12: sp_dbg1<DV, GV, 12>(c, nb, xpad, y, zt); break;
+    case 16: sp_dbg1<DV, GV, 16>(c, nb, xpad, y, zt); break;
+    case 28: sp_dbg1<DV, GV, 28>(c, nb, xpad, y, zt); break;
+    case 44: sp_dbg1<DV, GV, 44>(c, nb, xpad, y, zt); break;
+    case 36: sp_dbg1<DV, GV, 36>(c, nb, xpad, y, zt); break;
+    case 40: sp_dbg1<DV, GV, 40>(c, nb, xpad, y, zt); break;
+    case 32: sp_dbg1<DV, GV, 32>(c, nb, xpad, y, zt); break;
+    case 35: sp_dbg1<DV, GV, 35>(c, nb, xpad, y, zt); break;
+    default: sp_dbg1<DV, GV, 0>(c, nb, xpad, y, zt); break;
+  }
 }
 
 void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
@@ -5669,12 +6026,18 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
       if (st_used(c)) {  // default stencil: two planes per step, the listed rows after the march
         const int64_t nbfa = stface_blocks(c);
         double* pf = c.partials + nb;
+#define MCX_SP_DBG(DV, GV) sp_dbg<DV, GV>(c, nb, xpad, y, zt)
 #define MCX_ST(DV, GV)                                                                                             \
   do {                                                                                                            \
     if (c.vi_st_tail)                                                                                             \
       hipLaunchKernelGGL((k_spmv_st<DV, GV, true>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,   \
                          c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt, c.st_list, c.st_n, I, c.vi_bdict,     \
                          c.vi_exc, c.st_slot, c.st_faces);                                                        \
+    else if (c.vi_st_pair && zt.dbg > 0)                                                                        \
+      MCX_SP_DBG(DV, GV);                                                                                         \
+    else if (c.vi_st_pair)                                                                                        \
+      hipLaunchKernelGGL((k_spmv_sp<DV, GV>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,         \
+                         c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);                                      \
     else                                                                                                          \
       hipLaunchKernelGGL((k_spmv_st<DV, GV>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,         \
                          c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);                                      \
@@ -5686,6 +6049,7 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
         else if (dot) MCX_ST(true, false);
         else MCX_ST(false, false);
 #undef MCX_ST
+#undef MCX_SP_DBG
         return;
       }
 #define MCX_VIBM(TXV, TYV, XVV, UV, PV, ...)                                                                          \

@@ -854,20 +854,22 @@ def test_cg_pdb_bitwise(maxits, storage):
     if maxits:
         assert out[0][:2] == (maxits, -3)
 
+@pytest.mark.parametrize("st", [0, 1])
 @pytest.mark.parametrize("maxits", [0, 5, 6])
-def test_cg_fused_p_update_bitwise(maxits):
+def test_cg_fused_p_update_bitwise(maxits, st):
     """Option cg_fusep: the CG's p update inside the value-indexed SpMV (two p buffers) and
     VecAXPY(x) every second iteration in the update kernel give bitwise the solve of the separate
     kernels — converged, and stopped by maxits after an odd and an even number of iterations
-    (the pending x update of the last iteration, k_cg_xfinal).  The default-stencil SpMV (vi_st)
-    does not fuse the p update and sums p.Ap over other partials: off here, so both sides run the
-    same SpMV kernel."""
+    (the pending x update of the last iteration, k_cg_xfinal).  vi_st 0: k_spmv_vibm's FP march;
+    vi_st 1: the default-stencil march k_spmv_sp's FP instantiation (round 6), then k_spmv_face
+    from p's buffer of the iteration.  Both sides of a comparison run the same SpMV kernels (the
+    default-stencil path sums p.Ap over other partials than k_spmv_vibm)."""
     NX, NY, NZ = 70, 20, 12
     argv = argv_for(NX, NY, NZ, 1e-12) + (["-ksp_max_it", maxits] if maxits else [])
     out = []
     with M.Macroc(argv) as m:
         m.set_option("vi_stage", 1)
-        m.set_option("vi_st", 0)
+        m.set_option("vi_st", st)
         m.apply_bc_on_u(m.get_displacement(1))
         m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
         for fusep in (0, 1, 0):

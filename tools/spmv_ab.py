@@ -58,6 +58,8 @@ ys = []
 for v in variants:
     select(v)
     ys.append(m.spmv(x))
+    inf = m.get_info()
+    print(f"  variant {v}: st_listed {inf['st_listed']} tile {inf['spmv_tx']}x{inf['spmv_ty']}x{inf['spmv_kc']}", flush=True)
 res = [[] for _ in variants]
 for r in range(a.rounds):
     for q, v in enumerate(variants):
