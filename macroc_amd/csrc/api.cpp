@@ -1550,7 +1550,7 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
     return 0;
   }
   if (!std::strcmp(name, "split_dbg")) {
-    c.split_dbg = std::max(0, std::min(63, (int)value));  // (k_spmv_sp DBG: bits, see the kernel)
+    c.split_dbg = std::max(0, std::min(2047, (int)value));  // (k_spmv_sp DBG: bits, see the kernel)
     return 0;
   }
   if (!std::strcmp(name, "split_tx")) {
@@ -1668,8 +1668,28 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
     }
     return 0;
   }
-  if (!std::strcmp(name, "vi_st_pair")) {  // the same grid and partials either way
+  if (!std::strcmp(name, "vi_st_pair")) {
+    const int old = c.vi_st_pair;
     c.vi_st_pair = value != 0.;
+    if (!partials_fit(c)) {
+      c.vi_st_pair = old;
+      set_error("vi_st_pair: partials buffer too small");
+      return 2;
+    }
+    return 0;
+  }
+  if (!std::strcmp(name, "vi_st_ty")) {
+    if (!(value == 8. || value == 16.)) {
+      set_error("vi_st_ty: 8 or 16");
+      return 1;
+    }
+    const int old = c.vi_st_ty;
+    c.vi_st_ty = (int)value;
+    if (!partials_fit(c)) {
+      c.vi_st_ty = old;
+      set_error("vi_st_ty: partials buffer too small");
+      return 2;
+    }
     return 0;
   }
   if (!std::strcmp(name, "vi_st_tail")) {

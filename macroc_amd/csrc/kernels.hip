@@ -3035,6 +3035,14 @@ __global__ __launch_bounds__(TX * TY) void k_spmv_vibm(Geo g, const u32x4* __res
 }
 
 // ---------------------------------------------------------------------------- default-stencil SpMV
+// buffer resource over `bytes` from `base` (a raw buffer: out-of-range loads return 0, out-of-range
+// stores are dropped; at most 2 GB, the offsets used are 32-bit)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sp_rsrc(const double* base, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(base), (short)0,
+                                           (int)(bytes > 0x7fffffffLL ? 0x7fffffff : bytes), 0x00020000);
+}
+constexpr unsigned SP_OOB = 0x80000000u;  // a buffer offset past every record: load 0 / store dropped
+
 // Round 5 (vi_st).  On the block-indexed storage almost every node carries the same 27 block
 // indices: the interior stencil of the uniform grid (at 256^3 all but the 2.3 % of nodes on the
 // domain faces, next to Dirichlet nodes, or exception nodes).  The matrix is then held as
@@ -3308,19 +3316,30 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
   const bool wvin = gpx < npx && gpy < npy;  // (uniform) the patch has a mask
   const int len = 3 * min(TX + 2, g.nx + 2 - i0);
   const int rows = min(TY + 2, g.ny + 2 - j0);
-  auto xload = [&](int p, int m) -> double {  // x of padded plane p + 1 (p = -1 .. nz), staged element me + m T
+  // x of padded plane p + 1 (p = -1 .. nz), staged element me + m T: a buffer load, 0 outside the box
+  // (no branch: the compiler counts the loads, and the step's wait for them leaves the y stores in flight)
+  auto xload = [&](int p, int m) -> double {
     const int e = me + m * T;
     const int rr = e / RL, o = e - rr * RL;
-    if (e >= PLANE || o >= len || rr >= rows || p > g.nz) return 0.;
-    return x[3 * (int64_t)(i0 + (j0 + rr) * PX + (p + 1) * PXY) + o];
+    const __amdgpu_buffer_rsrc_t rx = sp_rsrc(x + (int64_t)(p + 1) * PXY * 3, p > g.nz ? 0 : (int64_t)PXY * 24);
+    const unsigned off = e >= PLANE || o >= len || rr >= rows ? SP_OOB : 8u * (unsigned)(3 * (i0 + (j0 + rr) * PX) + o);
+    typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rx, off, 0, 0));
   };
+  {  // prologue: planes k0-1 .. k0+2 in ring slots 0 .. 3, every load issued before the first store
+    double v[4][NL];
 #pragma unroll
-  for (int s = 0; s < 4; s++)  // prologue: planes k0-1 .. k0+2 in ring slots 0 .. 3
+    for (int s = 0; s < 4; s++)
 #pragma unroll
-    for (int m = 0; m < NL; m++) {
-      const int e = me + m * T;
-      if (e < PLANE) xs[s][e] = xload(k0 - 1 + s, m);
-    }
+      for (int m = 0; m < NL; m++) v[s][m] = xload(k0 - 1 + s, m);
+#pragma unroll
+    for (int s = 0; s < 4; s++)
+#pragma unroll
+      for (int m = 0; m < NL; m++) {
+        const int e = me + m * T;
+        if (e < PLANE) xs[s][e] = v[s][m];
+      }
+  }
   __syncthreads();
   typedef const volatile __attribute__((address_space(3))) double lds_vdouble;
   lds_vdouble* xsv = (lds_vdouble*)&xs[0][0];
@@ -3386,19 +3405,20 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
       }
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (inxy && !((m0 >> ln) & 1ull)) {
-      const int64_t n = i + g.nx * (j + (int64_t)g.ny * k);
-      __builtin_nontemporal_store(ya0, &y[3 * n + 0]);
-      __builtin_nontemporal_store(ya1, &y[3 * n + 1]);
-      __builtin_nontemporal_store(ya2, &y[3 * n + 2]);
-      if (DOT) dot += ca0 * ya0 + ca1 * ya1 + ca2 * ya2;
-    }
-    if (two && inxy && !((m1 >> ln) & 1ull)) {
-      const int64_t n = i + g.nx * (j + (int64_t)g.ny * (k + 1));
-      __builtin_nontemporal_store(yb0, &y[3 * n + 0]);
-      __builtin_nontemporal_store(yb1, &y[3 * n + 1]);
-      __builtin_nontemporal_store(yb2, &y[3 * n + 2]);
-      if (DOT) dot += cb0 * yb0 + cb1 * yb1 + cb2 * yb2;
+    {  // y of both nodes: branch-free buffer stores, a node the march leaves at an out-of-range offset
+      const bool la = inxy && !((m0 >> ln) & 1ull), lb = two && inxy && !((m1 >> ln) & 1ull);
+      const int64_t pls = 3 * (int64_t)g.nx * g.ny;
+      const __amdgpu_buffer_rsrc_t ra = sp_rsrc(y + pls * k, pls * 8), rb = sp_rsrc(y + pls * min(k + 1, g.nz - 1), pls * 8);
+      const unsigned o = 24u * (unsigned)(i + g.nx * j), oa = la ? o : SP_OOB, ob = lb ? o : SP_OOB;
+      typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, ya0), ra, oa, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, ya1), ra, oa + 8, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, ya2), ra, oa + 16, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, yb0), rb, ob, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, yb1), rb, ob + 8, 0, 2);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, yb2), rb, ob + 16, 0, 2);
+      if (DOT && la) dot += ca0 * ya0 + ca1 * ya1 + ca2 * ya2;
+      if (DOT && lb) dot += cb0 * yb0 + cb1 * yb1 + cb2 * yb2;
     }
     if (more) {  // (uniform) planes k+3, k+4 replace k-1, k (no longer read)
       __syncthreads();
@@ -3458,37 +3478,38 @@ __global__ __launch_bounds__(SFP_T) void k_spmv_face(Geo g, StFaces sf, const do
 }
 
 // ------------------------------------------------------- default-stencil SpMV, x-pair lanes (round 6)
-// k_spmv_st (one node per lane, nodes k and k+1) read each node's 81 x values from LDS as 8-B reads
-// and stored y as 8-B lane stores 24 B apart.  k_spmv_sp: every lane computes two x-adjacent nodes
-// of ONE plane; the x row (dy, dz) both need is 4 nodes = 12 doubles, six 16-B LDS reads (the pair's
-// 48-B lane stride keeps them 16-B aligned; a wave row is 32 lanes = 64 nodes, so every 16-lane group
-// of a ds_read_b128 lies in one staged row and covers the 16 bank slots 3 l mod 16: conflict-free
-// for any row pitch).  The block marches a 64 x 16 tile two planes per step with the same 4-slot x
-// ring and blocks -> tiles map as k_spmv_st (z-chunks, XCD slabs): waves 0-7 compute plane k, waves
-// 8-15 plane k+1, a wave two tile rows.  y leaves through LDS: a wave row's 64 nodes (192 doubles) are
-// written to a per-wave scratch and read back lane-consecutively, so every store instruction writes
-// 512 B of whole lines -- the pair's three 16-B stores 48 B apart wrote partial lines (measured: the
-// march's y stores alone 257 us with non-temporal partial-line stores, profiles/r06i_*).  The rows are
-// the fused multiply-adds of k_spmv_st / k_spmv_vibm / k_spmv_face in (nb, c) order, so y is bitwise
-// theirs; face and listed nodes (k_st_mask's 16 x 4 patch masks) are left to k_spmv_face.
-constexpr int SP_RLP = 200;
+// k_spmv_st (one node per lane, nodes k and k+1) read each node's 81 x values from LDS as 8-B reads.
+// k_spmv_sp: every lane computes two x-adjacent nodes of ONE plane; the x row (dy, dz) both need is
+// 4 nodes = 12 doubles, six 16-B LDS reads (the pair's 48-B lane stride keeps them 16-B aligned; a
+// wave row is 32 lanes = 64 nodes, so every 16-lane group of a ds_read_b128 lies in one staged row
+// and covers the 16 bank slots 3 l mod 16: conflict-free for any row pitch).  The block marches a
+// 64 x TY tile two planes per step with a 4-slot x ring and k_spmv_st's blocks -> tiles map (z-chunks,
+// XCD slabs): the first TY/2 waves compute plane k, the others plane k+1, a wave two tile rows.
+// Loads and stores are buffer instructions whose out-of-range offsets the hardware drops (a load
+// returns 0): staging and the masked y stores carry no branches, so the compiler counts them and the
+// step's wait for its loads (vmcnt counts loads and stores in issue order) leaves the just-issued y
+// stores in flight.  With branchy global loads and stores that wait was vmcnt(0): every step waited
+// for its y stores' round trip to HBM before refilling the ring (profiles/r06r_*).
+// The rows are the fused multiply-adds of k_spmv_st / k_spmv_vibm / k_spmv_face in (nb, c) order, so y
+// is bitwise theirs; face and listed nodes (k_st_mask's 16 x 4 patch masks) are left to k_spmv_face.
+// TY = 8 (512 threads, two blocks per CU with independent barriers) or 16 (option vi_st_ty).
+constexpr int SP_RLP = 198;
 // FP (the CG's p update fused into the march, option cg_fusep; single rank, no exception nodes, as
 // k_spmv_vibm's FP): the ring is staged from r, the Jacobi index byte and p(i-1) instead of x,
 // p(i) = z + beta p(i-1) with z = D^-1 r (k_cg_pupdate's expression, so p is bitwise the
 // unfused update's), written to p's buffer i & 1 for the tile's own nodes and multiplied in the
 // same step; k_spmv_face then reads that buffer.
 
-template <bool DOT, bool GATED, bool FP = false, int DBG = 0>
-__global__ __launch_bounds__(1024) void k_spmv_sp(Geo g, const double* __restrict__ coef,
-                                                  const unsigned long long* __restrict__ mask, int npx, int npy,
-                                                  const double* __restrict__ x, double* __restrict__ y,
-                                                  double* __restrict__ part, const CgState* __restrict__ cg,
-                                                  ZTiling zt, FusedP fp = {}) {
-  constexpr int TX = 64, TY = 16, T = 1024, RW = 3 * (TX + 2), RLP = SP_RLP, PR = TY + 2, PLANE = PR * RLP;
-  constexpr int SR = T / RW, NL = (PR + SR - 1) / SR;  // staged rows per pass (5), passes (4)
+template <bool DOT, bool GATED, int TY = 8, bool FP = false, int DBG = 0>
+__global__ __launch_bounds__(64 * TY) __attribute__((amdgpu_waves_per_eu(4))) void k_spmv_sp(
+    Geo g, const double* __restrict__ coef, const unsigned long long* __restrict__ mask, int npx, int npy,
+    const double* __restrict__ x, double* __restrict__ y, double* __restrict__ part, const CgState* __restrict__ cg,
+    ZTiling zt, FusedP fp = {}) {
+  static_assert(TY == 8 || TY == 16, "64 x 8 tiles (two blocks per CU) or 64 x 16 (one)");
+  constexpr int TX = 64, T = 64 * TY, WP = TY / 2, RW = 3 * (TX + 2), RLP = SP_RLP, PR = TY + 2, PLANE = PR * RLP;
+  constexpr int SR = T / RW, NL = (PR + SR - 1) / SR;  // staged rows per pass, passes
   static_assert(RLP >= RW && RLP % 2 == 0, "ring rows: 198 doubles, 16-B aligned");
   __shared__ __attribute__((aligned(16))) double xs[4 * PLANE];
-  __shared__ __attribute__((aligned(16))) double ysc[T / 64][3 * TX];  // per wave: one tile row's y
   __shared__ double sh[T / 64];
   __shared__ double s9[27];  // value 8 of the default stencil's blocks
   __shared__ double s_jdd[FP ? 3 * VI_MAX : 1];
@@ -3521,7 +3542,7 @@ __global__ __launch_bounds__(1024) void k_spmv_sp(Geo g, const double* __restric
   if (FP)
     for (int t = me; t < 3 * VI_MAX; t += T) s_jdd[t] = fp.jdd[t];
   const int wv = me >> 6, ln = me & 63;
-  const int h = __builtin_amdgcn_readfirstlane(wv >> 3), w8 = __builtin_amdgcn_readfirstlane(wv & 7);
+  const int h = __builtin_amdgcn_readfirstlane(wv / WP), w8 = __builtin_amdgcn_readfirstlane(wv % WP);
   const int rw = ln >> 5;          // the lane's row of the wave's two (plane k + h, tile rows 2 w8, 2 w8 + 1)
   const int ix = 2 * (ln & 31);    // tile x of the lane's first node
   const int ly = 2 * w8 + rw;
@@ -3541,9 +3562,14 @@ __global__ __launch_bounds__(1024) void k_spmv_sp(Geo g, const double* __restric
   const int sro = sr0 * RLP + so;                      // its ring offset
   const int64_t PXY3 = 3 * (int64_t)PXY;
   auto srow = [&](int m) { return sx && sr0 + SR * m < rows; };
-  auto xload = [&](int p, int m) -> double {  // x of padded plane p + 1 (p = -1 .. nz)
-    if (!srow(m) || p > g.nz) return 0.;
-    return x[(int64_t)(p + 1) * PXY3 + spo + 3 * SR * m * PX];
+  auto xload = [&](int p, int m) -> double {  // x of padded plane p + 1 (p = -1 .. nz): 0 outside the box
+    if (DBG & 1024) {  // (diagnostic) branchy global loads
+      if (!srow(m) || p > g.nz) return 0.;
+      return x[(int64_t)(p + 1) * PXY3 + spo + 3 * SR * m * PX];
+    }
+    const __amdgpu_buffer_rsrc_t rx = sp_rsrc(x + (int64_t)(p + 1) * PXY3, p > g.nz ? 0 : PXY3 * 8);
+    const unsigned off = srow(m) ? 8u * (unsigned)(spo + 3 * SR * m * PX) : SP_OOB;
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rx, off, 0, 0));
   };
   auto xstore = [&](int slot, int m, double v) {
     if (stg && sr0 + SR * m < PR) xs[slot * PLANE + sro + SR * m * RLP] = v;
@@ -3575,7 +3601,6 @@ __global__ __launch_bounds__(1024) void k_spmv_sp(Geo g, const double* __restric
     return (f.jx & 0x100u) ? pn : 0.;
   };
   // prologue: planes k0-1 .. k0+2 in ring slots 0 .. 3, every load issued before the first store
-  // (one memory round trip, not one per element)
   if (FP) {
     __syncthreads();  // s_jdd
 #pragma unroll
@@ -3603,11 +3628,13 @@ __global__ __launch_bounds__(1024) void k_spmv_sp(Geo g, const double* __restric
   }
   __syncthreads();
   typedef double d2v __attribute__((ext_vector_type(2)));
+  typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
+  typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
   typedef const __attribute__((address_space(3))) d2v lds_d2v;
   lds_d2v* xs2 = (lds_d2v*)&xs[0];
   // DBG (timing-only diagnostics, option split_dbg; wrong products): 1 = one row's coefficients
-  // loaded once before the march (no scalar loads in the row loop), 2 = no x reads in the row loop
-  // (the lane's x fixed), 3 = both
+  // loaded once before the march (no scalar loads in the row loop), 2 = no x reads in the row loop,
+  // 4 = no staging loads, 8 = no rows, 32 = no y stores; 1024 = branchy global loads and stores
   double dav[(DBG & 1) ? 27 : 1], dxw[(DBG & 2) ? 12 : 1];
   if constexpr ((DBG & 1) != 0) {
 #pragma unroll
@@ -3617,35 +3644,12 @@ __global__ __launch_bounds__(1024) void k_spmv_sp(Geo g, const double* __restric
 #pragma unroll
     for (int q = 0; q < 12; q++) dxw[q] = xs[q + ln];
   }
-  // y of the wave's two rows from the last step, transposed (yd[r2][q]: double q 64 + lane of row
-  // r2), stored at the start of the next step before its loads: the stores then have the whole
-  // row phase to complete before the step's wait for its loads (vmcnt counts loads and stores in
-  // issue order) instead of holding the barrier
-  double yd[2][3] = {{0., 0., 0.}, {0., 0., 0.}};
-  unsigned long long lvd[2] = {0ull, 0ull};
-  int64_t ybd[2] = {0, 0};
-  bool pend = false;  // (uniform)
-  auto ystore = [&]() {
-    if (!pend || (DBG & 32)) return;
-#pragma unroll
-    for (int r2 = 0; r2 < 2; r2++)
-#pragma unroll
-      for (int q = 0; q < 3; q++) {
-        const int d = q * 64 + ln;  // double d of the row: node d / 3
-        if ((lvd[r2] >> (d / 3)) & 1ull) {
-          if (DBG & 16) y[ybd[r2] + d] = yd[r2][q];
-          else __builtin_nontemporal_store(yd[r2][q], &y[ybd[r2] + d]);
-        }
-      }
-    pend = false;
-  };
   for (int k = k0; k < k1; k += 2) {
     const bool more = k + 2 < k1;
     const int kk = k + h;
-    const bool act = kk < k1;  // (uniform per wave) an odd last plane: waves 8-15 idle
+    const bool act = kk < k1;  // (uniform per wave) an odd last plane: the second half's waves idle
     double xr[2][NL];
     Fe fe[2][FP ? NL : 1];
-    ystore();
     if (more && !(DBG & 4)) {  // planes k+3 and k+4, in flight during the step
 #pragma unroll
       for (int m = 0; m < NL; m++) {
@@ -3662,6 +3666,8 @@ __global__ __launch_bounds__(1024) void k_spmv_sp(Geo g, const double* __restric
 #pragma unroll
       for (int m = 0; m < NL; m++) xr[0][m] = xr[1][m] = 0.;
     }
+    double y00 = 0., y01 = 0., y02 = 0., y10 = 0., y11 = 0., y12 = 0.;
+    bool live0 = false, live1 = false;
     if (act) {
       // the live nodes of the wave's two rows (bit x: node i0 + x is marched; faces, listed rows and
       // nodes outside the domain are not): from the 4 patch masks, scalar
@@ -3674,8 +3680,7 @@ __global__ __launch_bounds__(1024) void k_spmv_sp(Geo g, const double* __restric
         for (int r2 = 0; r2 < 2; r2++) lv[r2] |= ((~mk >> (16 * (q0 + r2))) & 0xffffull) << (16 * p4);
       }
       const unsigned long long lvr = rw ? lv[1] : lv[0];
-      const bool live0 = (lvr >> ix) & 1ull, live1 = (lvr >> (ix + 1)) & 1ull;
-      double y00 = 0., y01 = 0., y02 = 0., y10 = 0., y11 = 0., y12 = 0.;
+      live0 = (lvr >> ix) & 1ull, live1 = (lvr >> (ix + 1)) & 1ull;
       // a rolled loop over the 9 stencil rows (see k_spmv_st: unrolled, the compiler hoists the
       // rows' scalar loads and spills)
 #pragma unroll 1
@@ -3721,31 +3726,48 @@ __global__ __launch_bounds__(1024) void k_spmv_sp(Geo g, const double* __restric
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      // y through the wave's scratch: row r2's 32 lanes write their pairs (6 doubles, 48 B apart),
-      // then all 64 lanes take 3 lane-consecutive doubles each (stored next step as whole 512-B runs)
-      typedef __attribute__((address_space(3))) d2v lds_d2vw;
-      typedef __attribute__((address_space(3))) double lds_dw;
-      lds_d2vw* ys2 = (lds_d2vw*)&ysc[wv][0];
-      const lds_dw* ys1 = (const lds_dw*)&ysc[wv][0];
-#pragma unroll
-      for (int r2 = 0; r2 < 2; r2++) {
-        if (rw == r2) {
-          ys2[3 * (ln & 31) + 0] = d2v{y00, y01};
-          ys2[3 * (ln & 31) + 1] = d2v{y02, y10};
-          ys2[3 * (ln & 31) + 2] = d2v{y11, y12};
-        }
-#pragma unroll
-        for (int q = 0; q < 3; q++) yd[r2][q] = ys1[q * 64 + ln];
-        lvd[r2] = lv[r2];
-        ybd[r2] = 3 * ((int64_t)i0 + g.nx * ((int64_t)(j0 + 2 * w8 + r2) + (int64_t)g.ny * kk));
-      }
-      pend = true;
       if (DOT) {  // p.w with the nodes' own x from the ring (block 13 of the rows: not kept live)
         const int rc = (((kk - k0 + 1) & 3) * PLANE + (ly + 1) * RLP + 3 * ix) >> 1;
         const d2v c0 = xs2[rc + 1], c1 = xs2[rc + 2], c2 = xs2[rc + 3], c3 = xs2[rc + 4];
         // c0 = (x[2], x[3]) ... : node 0's x at doubles 3..5, node 1's at 6..8 of the row segment
         if (live0) dot += c0.y * y00 + c1.x * y01 + c1.y * y02;
         if (live1) dot += c2.x * y10 + c2.y * y11 + c3.x * y12;
+      }
+    }
+    {
+      // y: the pair's 6 doubles (48 B), per node (a node's doubles at an out-of-range offset when it is
+      // not marched; the compiler merges each node's three 8-B stores into a 16-B and an 8-B one).
+      // Outside `act`: every wave issues the same stores (the idle half's all dropped)
+      const int64_t pl = 3 * (int64_t)g.nx * g.ny * min(kk, g.nz - 1);  // (uniform) the plane's first double
+      const unsigned o0 = 24u * (unsigned)(i0 + ix + g.nx * (j0 + ly));
+      if (DBG & 32) {
+      } else if (DBG & 1024) {  // (diagnostic) branchy global stores
+        double* yp = y + pl + o0 / 8;
+        if (live0 && live1) {
+          __builtin_nontemporal_store(y00, yp + 0), __builtin_nontemporal_store(y01, yp + 1);
+          __builtin_nontemporal_store(y02, yp + 2), __builtin_nontemporal_store(y10, yp + 3);
+          __builtin_nontemporal_store(y11, yp + 4), __builtin_nontemporal_store(y12, yp + 5);
+        } else {
+          if (live0)
+            __builtin_nontemporal_store(y00, yp + 0), __builtin_nontemporal_store(y01, yp + 1),
+                __builtin_nontemporal_store(y02, yp + 2);
+          if (live1)
+            __builtin_nontemporal_store(y10, yp + 3), __builtin_nontemporal_store(y11, yp + 4),
+                __builtin_nontemporal_store(y12, yp + 5);
+        }
+      } else {
+        // no branch: every lane issues the same stores (the compiler then counts them, and the
+        // step's wait for its loads leaves them in flight); an unmarched node's at an out-of-range offset
+        const __amdgpu_buffer_rsrc_t ry = sp_rsrc(y + pl, 24 * (int64_t)g.nx * g.ny);
+        {
+          const unsigned a0 = live0 ? o0 : SP_OOB, a1 = live1 ? o0 + 24 : SP_OOB;
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, y00), ry, a0, 0, 2);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, y01), ry, a0 + 8, 0, 2);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, y02), ry, a0 + 16, 0, 2);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, y10), ry, a1, 0, 2);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, y11), ry, a1 + 8, 0, 2);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, y12), ry, a1 + 16, 0, 2);
+        }
       }
     }
     if (more) {  // (uniform) planes k+3, k+4 replace k-1, k (no longer read)
@@ -3765,7 +3787,6 @@ __global__ __launch_bounds__(1024) void k_spmv_sp(Geo g, const double* __restric
       __syncthreads();
     }
   }
-  ystore();
   if (DOT) {
     const double s = block_sum<T>(dot, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = s;
@@ -5144,7 +5165,14 @@ bool vi_staged(const Ctx& c) {
   return vis_tiling(c).kc >= 4;
 }
 
+static bool sp_used(const Ctx& c);
+static ZTiling sp_tiling(const Ctx& c);
+
 int64_t spmv_grid_blocks(const Ctx& c) {
+  if (sp_used(c)) {
+    const ZTiling t = sp_tiling(c);
+    return 8 * (int64_t)(((t.nty + 7) / 8) * t.ntx * t.nzc);
+  }
   if (c.fmt == FMT_VI && vi_staged(c) && (c.vi_bits == 4 || c.vi_block)) {  // launch_spmv's staged kernels
     const ZTiling t = vis_tiling(c);
     return 8 * (int64_t)(((t.nty + 7) / 8) * t.ntx * t.nzc);
@@ -5162,7 +5190,11 @@ int64_t spmv_grid_blocks(const Ctx& c) {
 }
 void spmv_tile(const Ctx& c, int* tx, int* ty, int* kc) {
   *tx = *ty = *kc = 0;
-  if (c.fmt == FMT_VI && vi_staged(c) && (c.vi_bits == 4 || c.vi_block)) {
+  if (sp_used(c)) {
+    *tx = 64;
+    *ty = c.vi_st_ty;
+    *kc = sp_tiling(c).kc;
+  } else if (c.fmt == FMT_VI && vi_staged(c) && (c.vi_bits == 4 || c.vi_block)) {
     vis_shape(c, *tx, *ty);
     *kc = vis_tiling(c).kc;
   } else if (c.fmt == FMT_SPLIT || (c.fmt == FMT_U && c.spmv_kernel >= 1)) {
@@ -5202,6 +5234,22 @@ bool st_used(const Ctx& c) {
 
 // the fused p update on the default-stencil path: k_spmv_sp's FP instantiation (not k_spmv_st, not the tail)
 bool st_fusep(const Ctx& c) { return c.vi_st_pair && !c.vi_st_tail; }
+
+// the default-stencil march is k_spmv_sp (x-pair lanes, 64 x vi_st_ty tiles)
+static bool sp_used(const Ctx& c) { return st_used(c) && c.vi_st_pair && !c.vi_st_tail; }
+
+// k_spmv_sp's tiling: 64 x vi_st_ty tiles, z-chunks for one resident round (1024 / (64 ty) blocks per CU)
+static ZTiling sp_tiling(const Ctx& c) {
+  const int ty = c.vi_st_ty;
+  ZTiling t;
+  t.ntx = (c.g.nx + 63) / 64;
+  t.nty = (c.g.ny + ty - 1) / ty;
+  const int tiles = t.ntx * t.nty, want = c.spmv_zblocks > 0 ? c.spmv_zblocks : c.g.ncu * (16 / ty);
+  t.nzc = std::max(1, std::min(c.g.nz, (want + tiles - 1) / tiles));
+  t.kc = (c.g.nz + t.nzc - 1) / t.nzc;
+  t.nzc = (c.g.nz + t.kc - 1) / t.kc;
+  return t;
+}
 
 // k_spmv_face's blocks (the face phase and the listed rows as a kernel of their own: vi_st_tail 0)
 static int64_t stface_blocks(const Ctx& c) {
@@ -5959,8 +6007,13 @@ static void launch_spmv_fusep(Ctx& c, double* y) {
   if (st_used(c)) {  // the default-stencil march with the p update (k_spmv_sp FP), then the faces and
                      // listed rows from p's buffer of this iteration (the host's count cg_it is the
                      // device's cg->i for every iteration that runs; finished ones return at once)
-    hipLaunchKernelGGL((k_spmv_sp<true, true, true>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,
-                       c.st_npx, c.st_npy, nullptr, y, c.partials, c.cg, zt, fp);
+    zt = sp_tiling(c);
+    if (c.vi_st_ty == 16)
+      hipLaunchKernelGGL((k_spmv_sp<true, true, 16, true>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef,
+                         c.st_mask, c.st_npx, c.st_npy, nullptr, y, c.partials, c.cg, zt, fp);
+    else
+      hipLaunchKernelGGL((k_spmv_sp<true, true, 8, true>), dim3(nb), dim3(512), 0, c.stream, c.g, c.st_coef,
+                         c.st_mask, c.st_npx, c.st_npy, nullptr, y, c.partials, c.cg, zt, fp);
     const int64_t nbfa = stface_blocks(c);
     if (nbfa)
       hipLaunchKernelGGL((k_spmv_face<true, true>), dim3((unsigned)nbfa), dim3(SFP_T), 0, c.stream, c.g, c.st_faces,
@@ -5986,8 +6039,12 @@ static void launch_spmv_fusep(Ctx& c, double* y) {
 // k_spmv_sp's timing-only diagnostic instantiations (option split_dbg; wrong products, see DBG)
 template <bool DV, bool GV, int D>
 static void sp_dbg1(Ctx& c, int nb, const double* xpad, double* y, const ZTiling& zt) {
-  hipLaunchKernelGGL((k_spmv_sp<DV, GV, false, D>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,
-                     c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);
+  if (c.vi_st_ty == 16)
+    hipLaunchKernelGGL((k_spmv_sp<DV, GV, 16, false, D>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef,
+                       c.st_mask, c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);
+  else
+    hipLaunchKernelGGL((k_spmv_sp<DV, GV, 8, false, D>), dim3(nb), dim3(512), 0, c.stream, c.g, c.st_coef,
+                       c.st_mask, c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);
 }
 template <bool DV, bool GV>
 static void sp_dbg(Ctx& c, int nb, const double* xpad, double* y, const ZTiling& zt) {
@@ -5998,9 +6055,8 @@ static void sp_dbg(Ctx& c, int nb, const double* xpad, double* y, const ZTiling&
     case 4: sp_dbg1<DV, GV, 4>(c, nb, xpad, y, zt); break;
     case 8: sp_dbg1<DV, GV, 8>(c, nb, xpad, y, zt); break;
     case 12: sp_dbg1<DV, GV, 12>(c, nb, xpad, y, zt); break;
-    case 16: sp_dbg1<DV, GV, 16>(c, nb, xpad, y, zt); break;
-    case 28: sp_dbg1<DV, GV, 28>(c, nb, xpad, y, zt); break;
     case 44: sp_dbg1<DV, GV, 44>(c, nb, xpad, y, zt); break;
+    case 1024: sp_dbg1<DV, GV, 1024>(c, nb, xpad, y, zt); break;
     case 36: sp_dbg1<DV, GV, 36>(c, nb, xpad, y, zt); break;
     case 40: sp_dbg1<DV, GV, 40>(c, nb, xpad, y, zt); break;
     case 32: sp_dbg1<DV, GV, 32>(c, nb, xpad, y, zt); break;
@@ -6024,6 +6080,11 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
       int tx, ty;
       vis_shape(c, tx, ty);
       if (st_used(c)) {  // default stencil: two planes per step, the listed rows after the march
+        if (sp_used(c)) {
+          const int dbg = zt.dbg;
+          zt = sp_tiling(c);
+          zt.dbg = dbg;
+        }
         const int64_t nbfa = stface_blocks(c);
         double* pf = c.partials + nb;
 #define MCX_SP_DBG(DV, GV) sp_dbg<DV, GV>(c, nb, xpad, y, zt)
@@ -6035,8 +6096,11 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
                          c.vi_exc, c.st_slot, c.st_faces);                                                        \
     else if (c.vi_st_pair && zt.dbg > 0)                                                                        \
       MCX_SP_DBG(DV, GV);                                                                                         \
+    else if (c.vi_st_pair && c.vi_st_ty == 16)                                                                    \
+      hipLaunchKernelGGL((k_spmv_sp<DV, GV, 16>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,     \
+                         c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);                                      \
     else if (c.vi_st_pair)                                                                                        \
-      hipLaunchKernelGGL((k_spmv_sp<DV, GV>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,         \
+      hipLaunchKernelGGL((k_spmv_sp<DV, GV, 8>), dim3(nb), dim3(512), 0, c.stream, c.g, c.st_coef, c.st_mask,       \
                          c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);                                      \
     else                                                                                                          \
       hipLaunchKernelGGL((k_spmv_st<DV, GV>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,         \

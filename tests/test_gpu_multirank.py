@@ -326,11 +326,13 @@ def test_multirank_st_bitwise(grid, procs):
     ref = O.Problem(NX, NY, NZ, rtol=rtol)
     ref.newton_step1()
     x = np.random.default_rng(29).uniform(-1, 1, ref.ndofs)
-    outs = [run_group(argv, px * py * pz, newton_step(x, [("vi_stage", 1), ("vi_st", st)])) for st in (0, 1)]
+    outs = [run_group(argv, px * py * pz, newton_step(x, [("vi_stage", 1), ("vi_st", st), ("vi_st_pair", sp)]))
+            for st, sp in ((0, 0), (1, 0), (1, 1))]
     du = np.zeros(ref.ndofs)
-    for a, b in zip(*outs):
+    for a, b, c in zip(*outs):
         assert a["info"]["st_listed"] == -1 and b["info"]["st_listed"] >= 0, (a["info"], b["info"])
         assert np.array_equal(a["y"], b["y"])
+        assert np.array_equal(a["y"], c["y"])  # k_spmv_sp (x-pair lanes, round 6)
         du[b["nat"]] = b["du"]
     assert np.linalg.norm(du - ref.du()) <= 1e-10 * np.linalg.norm(ref.du())
 

@@ -815,6 +815,12 @@ def test_st_face_classes(N):
             m.set_option("vi_st_tail", 1)
             assert np.array_equal(m.spmv(x), y), zblocks
             m.set_option("vi_st_tail", 0)
+            # the x-pair march k_spmv_sp (round 6), 64 x 16 and 64 x 8 tiles: the same rows
+            m.set_option("vi_st_pair", 1)
+            for ty in (16, 8):
+                m.set_option("vi_st_ty", ty)
+                assert np.array_equal(m.spmv(x), y), (zblocks, "sp", ty)
+            m.set_option("vi_st_pair", 0)
 
 
 @pytest.mark.parametrize("maxits", [None, 37, 38, 39, 40, 1, 2, 3, 4, 5])
@@ -861,7 +867,7 @@ def test_cg_fused_p_update_bitwise(maxits, st):
     VecAXPY(x) every second iteration in the update kernel give bitwise the solve of the separate
     kernels — converged, and stopped by maxits after an odd and an even number of iterations
     (the pending x update of the last iteration, k_cg_xfinal).  vi_st 0: k_spmv_vibm's FP march;
-    vi_st 1: the default-stencil march k_spmv_sp's FP instantiation (round 6), then k_spmv_face
+    vi_st 1 (+ vi_st_pair 1): the default-stencil march k_spmv_sp's FP instantiation (round 6), then k_spmv_face
     from p's buffer of the iteration.  Both sides of a comparison run the same SpMV kernels (the
     default-stencil path sums p.Ap over other partials than k_spmv_vibm)."""
     NX, NY, NZ = 70, 20, 12
@@ -870,6 +876,7 @@ def test_cg_fused_p_update_bitwise(maxits, st):
     with M.Macroc(argv) as m:
         m.set_option("vi_stage", 1)
         m.set_option("vi_st", st)
+        m.set_option("vi_st_pair", st)  # the fused default-stencil march is k_spmv_sp's
         m.apply_bc_on_u(m.get_displacement(1))
         m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
         for fusep in (0, 1, 0):

@@ -22,7 +22,7 @@ ap.add_argument("--vi", type=int, default=1, help="aij: -mat_aij_vi")
 ap.add_argument("--vi-bits", type=int, default=4, help="aij value-indexed: 4 (per-slot nibbles) or 8 (bytes)")
 ap.add_argument("--vi-block", type=int, default=1, help="aij value-indexed: 1 = one byte per 3x3 block when possible")
 ap.add_argument("--variants", default="split_tx=0", help="';'-separated option sets 'name=value,name=value'")
-ap.add_argument("--base", default="split_tx=0,spmv_zblocks=0", help="options every variant starts from")
+ap.add_argument("--base", default="split_tx=0,spmv_zblocks=0,split_dbg=0", help="options every variant starts from")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--iters", type=int, default=20)
 ap.add_argument("--lib", default="", help="another build of libmacroc_amd.so (e.g. the previous commit's)")
