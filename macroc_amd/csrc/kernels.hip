@@ -3582,22 +3582,33 @@ __global__ __launch_bounds__(64 * TY) __attribute__((amdgpu_waves_per_eu(4))) vo
     double po, rv;
     unsigned jx;
   };
+  // (buffer loads and stores, out-of-range offsets for elements off the owned nodes: no branches)
+  const int64_t NXY = (int64_t)g.nx * g.ny;
   auto fload = [&](int p, int m, Fe& f) {
-    f.po = f.rv = 0.;
-    f.jx = 0u;
     const int gj = j0 - 1 + sr0 + SR * m;
-    if (!srow(m) || !sox || gj < 0 || gj >= g.ny || p < 0 || p >= g.nz) return;
-    const int64_t n = sgi + (int64_t)g.nx * (gj + (int64_t)g.ny * p);
-    f.rv = fp.r[3 * n + sd];
-    f.jx = fp.jix[n] | 0x100u | (stx && gj >= j0 && gj < j0 + TY && p >= k0 && p < k1 ? 0x200u : 0u);
-    if (cgi > 0) f.po = psrc[(int64_t)(p + 1) * PXY3 + spo + 3 * SR * m * PX];
+    const bool own = srow(m) && sox && gj >= 0 && gj < g.ny && p >= 0 && p < g.nz;
+    const bool pl_ok = p >= 0 && p < g.nz;  // (uniform)
+    const __amdgpu_buffer_rsrc_t rr_ = sp_rsrc(fp.r + 3 * NXY * (pl_ok ? p : 0), pl_ok ? 24 * NXY : 0);
+    const __amdgpu_buffer_rsrc_t rj = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned char*>(fp.jix) + NXY * (pl_ok ? p : 0), (short)0, (int)(pl_ok ? NXY : 0), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rp = sp_rsrc(psrc + (int64_t)(p + 1) * PXY3, cgi > 0 && p <= g.nz ? PXY3 * 8 : 0);
+    const unsigned nn = (unsigned)(sgi + g.nx * gj);
+    typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+    f.rv = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rr_, own ? 8u * (3u * nn + sd) : SP_OOB, 0, 0));
+    f.jx = (unsigned)__builtin_amdgcn_raw_buffer_load_b8(rj, own ? nn : SP_OOB, 0, 0) | (own ? 0x100u : 0u) |
+           (own && stx && gj >= j0 && gj < j0 + TY && p >= k0 && p < k1 ? 0x200u : 0u);
+    f.po = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(
+                                          rp, own ? 8u * (unsigned)(spo + 3 * SR * m * PX) : SP_OOB, 0, 0));
   };
   // p(i) of a staged element (k_cg_pupdate's expression: z = D^-1 r, p = z (i = 0) or z + beta p(i-1));
   // a tile's own node's p goes to p's buffer of this iteration
   auto fpn = [&](int p, int m, const Fe& f) -> double {
     const double z = f.rv * s_jdd[3 * (f.jx & 255u) + sd];
     const double pn = cgi == 0 ? z : z + cb * f.po;
-    if (f.jx & 0x200u) pdst[(int64_t)(p + 1) * PXY3 + spo + 3 * SR * m * PX] = pn;
+    typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+    const __amdgpu_buffer_rsrc_t rd = sp_rsrc(pdst + (int64_t)(p + 1) * PXY3, p <= g.nz ? PXY3 * 8 : 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, pn), rd,
+                                          (f.jx & 0x200u) ? 8u * (unsigned)(spo + 3 * SR * m * PX) : SP_OOB, 0, 0);
     return (f.jx & 0x100u) ? pn : 0.;
   };
   // prologue: planes k0-1 .. k0+2 in ring slots 0 .. 3, every load issued before the first store
