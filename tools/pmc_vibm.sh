@@ -1,6 +1,6 @@
 #!/bin/bash
-# issue / LDS counters of the block-indexed staged SpMV (k_spmv_sp by default, vi_st_pair 0: k_spmv_st,
-# vi_st 0: k_spmv_vibm) at
+# issue / LDS counters of the block-indexed staged SpMV (k_spmv_st by default, vi_st_pair=1: k_spmv_sp,
+# vi_st=0: k_spmv_vibm) at
 # 256^3: two --pmc passes,
 # kernel trace only, over a short tools/spmv_ab.py run (diagnosis, not the bench)
 #   tools/pmc_vibm.sh [VARIANT] [TAG]   e.g. tools/pmc_vibm.sh vi_uni=1 uni
@@ -37,7 +37,7 @@ with open(OUT + "/summary.txt", "w") as f:
 busy_se, lds_cu = c["SQ_BUSY_CYCLES"] / 32, c["SQ_LDS_IDX_ACTIVE"] / 256
 waves, planes = c["SQ_WAVES"], 64
 d = {"aij-vi:256x256x256": {
-    "kernel": ("k_spmv_vibm" if "vi_st=0" in VAR else "k_spmv_st" if "vi_st_pair=0" in VAR else "k_spmv_sp") +
+    "kernel": ("k_spmv_vibm" if "vi_st=0" in VAR else "k_spmv_sp" if "vi_st_pair=1" in VAR else "k_spmv_st") +
               " 64x16 (" + VAR + ")",
     "commit": os.environ.get("MCX_COMMIT"),
     "method": "rocprofv3 --pmc, two passes of 8 SQ counters, kernel trace only, tools/spmv_ab.py --grid 256 "
