@@ -168,7 +168,7 @@ static int init_ctx(Ctx& c, const mcx_opts* o, int rank, int nranks, const void*
   c.vi_fma = o->mat_vi_fma != 0;
   if (o->mat_type == MCX_MAT_SBAIJ) {
     // phased z-march 256x4 / 128x4 / 64x4 (128^3: 0.436 vs 0.502 ms for symz 128x2; 64^3:
-    // 0.0555 vs 0.0625 ms for symz 64x4; profiles/r02_ab_sbaij{128,64}.log)
+    // 0.0555 vs 0.0625 ms for symz 64x4; profiles/old/r02_ab_sbaij{128,64}.log)
     c.spmv_kernel = c.g.nx >= 256 ? 11 : (c.g.nx >= 128 ? 7 : 8);
     c.fmt = FMT_U;
   }
@@ -1676,6 +1676,14 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
       set_error("vi_st_pair: partials buffer too small");
       return 2;
     }
+    return 0;
+  }
+  if (!std::strcmp(name, "vi_st_pf")) {
+    if (!(value == 1. || value == 2. || value == 3.)) {  // 3: timing-only, the ring never refilled (wrong rows)
+      set_error("vi_st_pf: 1 or 2");
+      return 1;
+    }
+    c.vi_st_pf = (int)value;
     return 0;
   }
   if (!std::strcmp(name, "vi_st_ty")) {

@@ -1562,7 +1562,7 @@ __global__ __launch_bounds__(TX * TY, 4) void k_spmv_symp(Geo g, const double* _
       // sources at dy = -1, row TY-1: dy = +1), computed now by one helper thread each into
       // edge[][h] (the same expression as the pull), so no wave waits on a chain of pulls there.
       // (Helpers for every out-of-tile term, x-edge columns included, and squarer tiles were
-      // slower: profiles/r02b_ab_tiles.log.)
+      // slower: profiles/old/r02b_ab_tiles.log.)
       if constexpr (HELP) {
         //   ph 0: h < 3 TX: row 0, this plane, nb 9 + h / TX;  3 TX <= h < 4 TX: row TY-1, next plane, nb 8
         //   ph 1: h < 2 TX: row TY-1, next plane, nb 6 + h / TX;  ph 2: h < 3 TX: row 0, next plane, nb h / TX
@@ -3265,7 +3265,7 @@ __device__ __forceinline__ void st_faces(const Geo& g, const StFaces& sf, const 
 // blocks after their march, each block a fixed share (idle blocks too), in the freed x ring.  The
 // march is one resident round of blocks, so the tail adds its latency to every block: 0.326 vs
 // 0.285 ms with k_spmv_face (profiles/r05p_*).  Same rows; the p.w terms go to the block's partial.
-template <bool DOT, bool GATED, bool TAIL = false>
+template <bool DOT, bool GATED, bool TAIL = false, bool PF2 = false, bool NOSTAGE = false>
 __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restrict__ coef,
                                                   const unsigned long long* __restrict__ mask, int npx, int npy,
                                                   const double* __restrict__ x, double* __restrict__ y,
@@ -3326,12 +3326,22 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
     typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rx, off, 0, 0));
   };
+  // PF2 (option vi_st_pf 2): the planes a step stores into the ring were loaded one step earlier, so
+  // each load has two steps of rows to land (xa: planes k+3, k+4 at step k)
+  double pfa[2][NL], pfb[2][NL];
   {  // prologue: planes k0-1 .. k0+2 in ring slots 0 .. 3, every load issued before the first store
     double v[4][NL];
 #pragma unroll
     for (int s = 0; s < 4; s++)
 #pragma unroll
       for (int m = 0; m < NL; m++) v[s][m] = xload(k0 - 1 + s, m);
+    if (PF2) {
+#pragma unroll
+      for (int m = 0; m < NL; m++) {
+        pfa[0][m] = xload(k0 + 3, m);
+        pfa[1][m] = xload(k0 + 4, m);
+      }
+    }
 #pragma unroll
     for (int s = 0; s < 4; s++)
 #pragma unroll
@@ -3343,10 +3353,20 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
   __syncthreads();
   typedef const volatile __attribute__((address_space(3))) double lds_vdouble;
   lds_vdouble* xsv = (lds_vdouble*)&xs[0][0];
-  for (int k = k0; k < k1; k += 2) {
+  // one two-plane step; PF2 alternates the two register sets between consecutive steps (no copies:
+  // a copy of a register still being loaded waits for the load)
+  auto step = [&](int k, double (&cur)[2][NL], double (&nxt)[2][NL]) {
     const bool two = k + 1 < k1, more = k + 2 < k1;
+    // PF2: planes k+3, k+4 (cur) were loaded a step earlier; k+5, k+6 go in flight into nxt
+    // (unconditional: a plane past the grid reads zeros, and the compiler keeps counting the loads)
     double xr[2][NL];
-    if (more) {  // planes k+3 and k+4, in flight during the step
+    if (PF2) {
+#pragma unroll
+      for (int m = 0; m < NL; m++) {
+        nxt[0][m] = xload(k + 5, m);
+        nxt[1][m] = xload(k + 6, m);
+      }
+    } else if (more) {  // planes k+3 and k+4, in flight during the step
 #pragma unroll
       for (int m = 0; m < NL; m++) {
         xr[0][m] = xload(k + 3, m);
@@ -3420,18 +3440,26 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
       if (DOT && la) dot += ca0 * ya0 + ca1 * ya1 + ca2 * ya2;
       if (DOT && lb) dot += cb0 * yb0 + cb1 * yb1 + cb2 * yb2;
     }
-    if (more) {  // (uniform) planes k+3, k+4 replace k-1, k (no longer read)
+    if (more && !NOSTAGE) {  // (uniform) planes k+3, k+4 replace k-1, k (no longer read); NOSTAGE: timing-only
       __syncthreads();
 #pragma unroll
       for (int m = 0; m < NL; m++) {
         const int e = me + m * T;
         if (e < PLANE) {
-          xs[(k + 3 - k0 + 1) & 3][e] = xr[0][m];
-          xs[(k + 4 - k0 + 1) & 3][e] = xr[1][m];
+          xs[(k + 3 - k0 + 1) & 3][e] = PF2 ? cur[0][m] : xr[0][m];
+          xs[(k + 4 - k0 + 1) & 3][e] = PF2 ? cur[1][m] : xr[1][m];
         }
       }
       __syncthreads();
     }
+  };
+  if (PF2) {
+    for (int k = k0; k < k1; k += 4) {
+      step(k, pfa, pfb);
+      if (k + 2 < k1) step(k + 2, pfb, pfa);
+    }
+  } else {
+    for (int k = k0; k < k1; k += 2) step(k, pfa, pfb);
   }
   if (TAIL) {
     __syncthreads();  // every wave is done with the ring: it holds the face patches' x, then the dictionary
@@ -4117,9 +4145,9 @@ __global__ __launch_bounds__(TPB) void k_spmv_exc(Geo g, const int* __restrict__
 
 // y = A x on FMT_VI with x staged in LDS, z-marching.  k_spmv_vi's 81 x gathers per node (8 B
 // at a 24-B lane stride: a third of every fetched line used) are a third of its time
-// (profiles/r02_vi_dbg.log: 1.14 ms, 0.78 without them); staging one plane per block and launch
+// (profiles/old/r02_vi_dbg.log: 1.14 ms, 0.78 without them); staging one plane per block and launch
 // was slower still (1.39 ms: one 113-KB block per CU waits on its own staging,
-// profiles/r02_ab_vis_*.log).  Here a 1024-thread block owns a TX x TY node tile and marches it
+// profiles/old/r02_ab_vis_*.log).  Here a 1024-thread block owns a TX x TY node tile and marches it
 // up a z-chunk: LDS holds a ring of three x planes (rows j0-1 .. j0+TY, TX+2 nodes each, as
 // contiguous in the padded box), and while plane k is computed the registers already carry plane
 // k+2's x (coalesced 8-B loads, 1.5 x per owned node at TY = 4) and plane k+1's index chunks,
@@ -4736,7 +4764,7 @@ __global__ void k_cg_xfinal(Geo g, const double* __restrict__ ppad, const double
 // 1024-thread blocks: a quarter of the partials for k_reduce (one block reads them all).  Option
 // cg_ublocks caps the grid (grid-stride: a thread's nodes n, n + grid, ... summed in that order)
 // so that k_reduce sums fewer partials: 0.8676 (2,048 blocks) / 0.8708 (512) against 0.8492 ms
-// per CG iteration uncapped at 256^3 (profiles/r04_cg_ab_ublocks256.log): the update kernel
+// per CG iteration uncapped at 256^3 (profiles/old/r04_cg_ab_ublocks256.log): the update kernel
 // loses more than the reduction saves
 static constexpr int UTPB = 1024;
 
@@ -5136,7 +5164,7 @@ static void split_shape(const Ctx& c, int& ztx, int& zty) {
   ztx = c.split_tx ? c.split_tx : (c.g.nx >= 256 ? 256 : (c.g.nx >= 128 ? 128 : 64));
   // tiles 256x4 (1 block / CU), 128x4 (2), 64x4 (4); 256x2, 128x8, 64x16.  Defaults by subdomain
   // width: 256x4, 128x8 (128^3: 0.478 vs 0.496 ms for 128x4), 64x4 (64^3: 0.0716 ms, best of
-  // six shapes / chunkings), profiles/r02_ab_{64,128}.log
+  // six shapes / chunkings), profiles/old/r02_ab_{64,128}.log
   zty = c.split_ty ? c.split_ty : (ztx == 128 && !c.split_tx ? 8 : 4);
   const bool built = (ztx == 256 && (zty == 2 || zty == 4)) || (ztx == 128 && (zty == 4 || zty == 8)) ||
                      (ztx == 64 && (zty == 4 || zty == 16));
@@ -5146,7 +5174,7 @@ static void split_shape(const Ctx& c, int& ztx, int& zty) {
 // FMT_VI with x staged in LDS (k_spmv_vim): 1024-thread tiles TX x TY marching z-chunks, one
 // resident round of blocks (one per CU: the ring and the dictionaries fill the LDS)
 // 64x16 tiles: with the scalar-dictionary 16x4 patches, 256^3 0.358 vs 0.419 ms (256x4) and
-// 128^3 0.0563 vs 0.0589 ms (128x8) per SpMV (profiles/r03_ab_tx{256b,128}.log): a third less
+// 128^3 0.0563 vs 0.0589 ms (128x8) per SpMV (profiles/old/r03_ab_tx{256b,128}.log): a third less
 // halo than 256x4 (66x18 staged nodes per 1024 instead of 258x6), and tiles away from the x
 // faces have no wave that reads the dictionary from LDS.  Option vi_tx selects 256x4 / 128x8.
 static void vis_shape(const Ctx& c, int& tx, int& ty) {
@@ -5170,7 +5198,7 @@ static ZTiling vis_tiling(const Ctx& c) {
 
 // staged (z-marching) value-indexed SpMV: forced by option vi_stage 0 / 1, else where a block
 // marches at least 4 planes (256^3: 0.49 vs 0.66 ms gathered, 128^3 0.073 vs 0.090; 64^3, one
-// plane per block: 0.024 vs 0.012; profiles/r02_vibm_ab*.log)
+// plane per block: 0.024 vs 0.012; profiles/old/r02_vibm_ab*.log)
 bool vi_staged(const Ctx& c) {
   if (c.vi_stage >= 0) return c.vi_stage != 0;
   return vis_tiling(c).kc >= 4;
@@ -6113,6 +6141,12 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
     else if (c.vi_st_pair)                                                                                        \
       hipLaunchKernelGGL((k_spmv_sp<DV, GV, 8>), dim3(nb), dim3(512), 0, c.stream, c.g, c.st_coef, c.st_mask,       \
                          c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);                                      \
+    else if (c.vi_st_pf == 3)                                                                                     \
+      hipLaunchKernelGGL((k_spmv_st<DV, GV, false, false, true>), dim3(nb), dim3(1024), 0, c.stream, c.g,            \
+                         c.st_coef, c.st_mask, c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);                \
+    else if (c.vi_st_pf == 2)                                                                                     \
+      hipLaunchKernelGGL((k_spmv_st<DV, GV, false, true>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef,       \
+                         c.st_mask, c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);                           \
     else                                                                                                          \
       hipLaunchKernelGGL((k_spmv_st<DV, GV>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,         \
                          c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);                                      \
@@ -6185,7 +6219,7 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
         MCX_VIBM(64, 16, true, true, true, true, false, true);
       } else if (c.vi_fma && tx == 64 && (c.vi_lg == 2 || c.vi_lg == 3)) {
         // LDS-path reads in groups of 2 blocks (default): SpMV 0.3098 vs 0.3228 ms, CG iteration
-        // 0.8295 vs 0.8419 ms; groups of 3 spill (0.3866 ms) (profiles/r04_cg_ab_lg256.log)
+        // 0.8295 vs 0.8419 ms; groups of 3 spill (0.3866 ms) (profiles/old/r04_cg_ab_lg256.log)
         if (c.vi_lg == 2) MCX_VIBM(64, 16, true, true, true, true, false, false, false, false, 2);
         else MCX_VIBM(64, 16, true, true, true, true, false, false, false, false, 3);
       } else if (!c.vi_fma && c.vi_uni && c.vi_patch && tx == 64 && c.vi_lg == 2) {  // exact rows, the same groups
@@ -6595,7 +6629,7 @@ int cg_iteration(Ctx& c, hipEvent_t ev0, hipEvent_t ev1, bool first, bool last) 
   CgState* A = c.cg + 1;  // fused path: the state after the alpha step
   // both folds or none: at 256^3 (16,384 update blocks) the alpha prologue of every block costs
   // more than the k_reduce launch it saves (4.177 vs 4.159 ms per CG iteration); at 64^3 the two
-  // folds save 1.6 % (profiles/r02_cg_ab_fuse{64,256}.log)
+  // folds save 1.6 % (profiles/old/r02_cg_ab_fuse{64,256}.log)
   const bool fa = fused(c) && nbu <= 1024, fb = fa;
   int rc;
   const bool dix = cg_dix(c);
