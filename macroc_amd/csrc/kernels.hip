@@ -3125,6 +3125,101 @@ __device__ __forceinline__ void st_tail(const Geo& g, const int* __restrict__ li
   }
 }
 
+// The listed rows with their loads in parallel (round 6): 16 lanes per
+// listed node, lane g9 = 0..8 holding stencil row g9 -- its 9 x values and its 3 blocks (exception
+// blocks from exc, else the dictionary staged in tab) -- all loaded at once, one memory round trip
+// instead of st_tail's nine dependent ones per node.  The row's three accumulators then pass lane
+// to lane (a 16-lane DPP row shift per round), lane g9 applying its 27 fused multiply-adds in round
+// g9: per output row the same FMAs in the same (nb, c) order as st_tail / k_spmv_vibm, so y is
+// bitwise theirs.  Lane 8 stores the row and its p.w term (the node's own x from lane 4).
+constexpr int ST16 = 16;  // lanes per listed node
+__device__ __forceinline__ double dpp_shr1(double v) {  // lane l takes lane l-1's value within its 16-lane row
+  const unsigned lo = __builtin_amdgcn_update_dpp(0, (int)__double2loint(v), 0x111, 0xf, 0xf, false);
+  const unsigned hi = __builtin_amdgcn_update_dpp(0, (int)__double2hiint(v), 0x111, 0xf, 0xf, false);
+  return __hiloint2double((int)hi, (int)lo);
+}
+template <int T>
+__device__ __forceinline__ void st_tail16(const Geo& g, const int* __restrict__ list, int64_t lo, int64_t hi,
+                                          const u32x4* __restrict__ I, const double* __restrict__ bdict,
+                                          const double* __restrict__ exc, const double* __restrict__ x,
+                                          double* __restrict__ y, double2* tabg, double& dot) {
+  typedef __attribute__((address_space(3))) double lds_double;
+  lds_double* tab = (lds_double*)tabg;
+  const int me = threadIdx.x;
+  if (lo >= hi) return;  // (uniform)
+  for (int q = me; q < VI_MAX * VIB_STRIDE; q += T) tab[q] = bdict[q];
+  __syncthreads();
+  const int PX = g.PX, PXY = g.PX * g.PY;
+  const int g9 = me & (ST16 - 1);
+  for (int64_t t0 = lo; t0 < hi; t0 += T / ST16) {  // (uniform)
+    const int64_t t = t0 + me / ST16;
+    const bool has = t < hi;
+    const bool row = has && g9 < 9;
+    double xw[9], av[27];
+#pragma unroll
+    for (int q = 0; q < 9; q++) xw[q] = 0.;
+#pragma unroll
+    for (int q = 0; q < 27; q++) av[q] = 0.;
+    int64_t n = 0;
+    if (row) {
+      n = list[t];
+      int i, j, k;
+      node_ijk(g, (int)n, i, j, k);
+      const int dy = g9 % 3 - 1, dz = g9 / 3 - 1;
+      const double* xr = x + 3 * ((int64_t)i + (j + 1 + dy) * (int64_t)PX + (k + 1 + dz) * (int64_t)PXY);
+#pragma unroll
+      for (int q = 0; q < 9; q++) xw[q] = xr[q];
+      const u32x4* ip = I + (n >> 6) * (2 * 64) + (n & 63);
+      const u32x4 w0 = ip[0], w1 = ip[64];
+      const unsigned slot = w1[3];  // exception slot + 1
+      const double* eb = exc + exc_base(slot ? slot - 1 : 0);
+#pragma unroll
+      for (int t3 = 0; t3 < 3; t3++) {
+        const int nb = g9 * 3 + t3;
+        if (slot) {
+#pragma unroll
+          for (int q = 0; q < 9; q++) av[t3 * 9 + q] = eb[(nb * 9 + q) * 64];
+        } else {
+          const int wi = nb >> 2;
+          const unsigned word = wi == 0 ? w0[0] : wi == 1 ? w0[1] : wi == 2 ? w0[2] : wi == 3 ? w0[3]
+                              : wi == 4 ? w1[0] : wi == 5 ? w1[1] : w1[2];
+          const lds_double* e = tab + ((word >> (8 * (nb & 3))) & 255u) * VIB_STRIDE;
+#pragma unroll
+          for (int q = 0; q < 9; q++) av[t3 * 9 + q] = e[q];
+        }
+      }
+    }
+    double y0 = 0., y1 = 0., y2 = 0.;
+#pragma unroll
+    for (int rnd = 0; rnd < 9; rnd++) {
+      if (g9 == rnd) {
+#pragma unroll
+        for (int t3 = 0; t3 < 3; t3++)
+#pragma unroll
+          for (int q = 0; q < 9; q++) {
+            const int r = q / 3, cc = q % 3;
+            double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
+            yr = __builtin_fma(av[t3 * 9 + q], xw[3 * t3 + cc], yr);
+          }
+      }
+      if (rnd < 8) {  // lane rnd's sums to lane rnd + 1
+        y0 = dpp_shr1(y0);
+        y1 = dpp_shr1(y1);
+        y2 = dpp_shr1(y2);
+      }
+    }
+    // lane 8: the row; the node's own x (block 13) from lane 4 (xw[3..5]), 4 lanes up
+    const double xc0 = __shfl(xw[3], (me & ~(ST16 - 1)) + 4, 64), xc1 = __shfl(xw[4], (me & ~(ST16 - 1)) + 4, 64),
+                 xc2 = __shfl(xw[5], (me & ~(ST16 - 1)) + 4, 64);
+    if (row && g9 == 8) {
+      __builtin_nontemporal_store(y0, &y[3 * n + 0]);
+      __builtin_nontemporal_store(y1, &y[3 * n + 1]);
+      __builtin_nontemporal_store(y2, &y[3 * n + 2]);
+      dot += xc0 * y0 + xc1 * y1 + xc2 * y2;
+    }
+  }
+}
+
 // The face phase: the domain faces' nodes of a usable stencil class (k_st_setup) in patches of 64
 // nodes along the face's fast axis (x-faces: j; y- and z-faces: i) x 4 along its slow axis, 256
 // threads each.  The patch's x is staged in LDS first (SFP_N doubles: 9-double chunks (i-1 .. i+1)
@@ -3487,17 +3582,18 @@ __global__ __launch_bounds__(SFP_T) void k_spmv_face(Geo g, StFaces sf, const do
   __shared__ double sh[SFP_T / 64];
   if (GATED && cg->reason) return;
   double dot = 0.;
-  // the listed rows' blocks first: their nine dependent gather rounds per node are the longest
-  // chains of the launch, started before the patches instead of after them
-  const int64_t NLB = (cnt + SFP_T - 1) / SFP_T;
+  // the listed rows' blocks first (their gathers are the launch's longest chains: nine dependent
+  // rounds per node before round 6's st_tail16, one now), started before the patches
+  constexpr int LPB = SFP_T / ST16;  // listed rows per block (16 lanes each, st_tail16)
+  const int64_t NLB = (cnt + LPB - 1) / LPB;
   if ((int64_t)blockIdx.x >= NLB) {
     const SfPatch q = sf_patch(g, sf, blockIdx.x - NLB);
     sf_stage(g, q, x, S, threadIdx.x);
     __syncthreads();
     sf_rows(g, q, coef, slot, S, y, dot, threadIdx.x);
   } else {
-    const int64_t lo = (int64_t)blockIdx.x * SFP_T;
-    st_tail<SFP_T>(g, list, lo, min(cnt, lo + SFP_T), I, bdict, exc, x, y, reinterpret_cast<double2*>(S), dot);
+    const int64_t lo = (int64_t)blockIdx.x * LPB;
+    st_tail16<SFP_T>(g, list, lo, min(cnt, lo + LPB), I, bdict, exc, x, y, reinterpret_cast<double2*>(S), dot);
   }
   if (DOT) {
     const double sm = block_sum<SFP_T>(dot, sh);
@@ -5292,7 +5388,7 @@ static ZTiling sp_tiling(const Ctx& c) {
 
 // k_spmv_face's blocks (the face phase and the listed rows as a kernel of their own: vi_st_tail 0)
 static int64_t stface_blocks(const Ctx& c) {
-  return st_used(c) && !c.vi_st_tail ? c.st_faces.u[6] + (c.st_n + SFP_T - 1) / SFP_T : 0;
+  return st_used(c) && !c.vi_st_tail ? c.st_faces.u[6] + (c.st_n + SFP_T / ST16 - 1) / (SFP_T / ST16) : 0;
 }
 
 // the exception rows' kernel (staged block-indexed storage with exception nodes, vi_exc_kernel)
