@@ -1678,6 +1678,20 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
     }
     return 0;
   }
+  if (!std::strcmp(name, "vi_st_l16")) {
+    if (!(value == -1. || value == 0. || value == 1.)) {
+      set_error("vi_st_l16: -1 (by the list's length), 0 or 1");
+      return 1;
+    }
+    const int old = c.vi_st_l16;
+    c.vi_st_l16 = (int)value;
+    if (!partials_fit(c)) {
+      c.vi_st_l16 = old;
+      set_error("vi_st_l16: partials buffer too small");
+      return 2;
+    }
+    return 0;
+  }
   if (!std::strcmp(name, "vi_st_pf")) {
     if (!(value == 1. || value == 2. || value == 3.)) {  // 3: timing-only, the ring never refilled (wrong rows)
       set_error("vi_st_pf: 1 or 2");

@@ -3570,7 +3570,7 @@ __global__ __launch_bounds__(1024) void k_spmv_st(Geo g, const double* __restric
 
 // the face phase and the listed rows as a kernel of their own (vi_st_tail 0): SFP_T listed rows per
 // block (the dictionary staged in the patch's LDS), then one face patch per block
-template <bool DOT, bool GATED>
+template <bool DOT, bool GATED, bool L16 = true>
 __global__ __launch_bounds__(SFP_T) void k_spmv_face(Geo g, StFaces sf, const double* __restrict__ coef,
                                                    const unsigned* __restrict__ slot, const double* __restrict__ x,
                                                    double* __restrict__ y, double* __restrict__ part,
@@ -3584,7 +3584,7 @@ __global__ __launch_bounds__(SFP_T) void k_spmv_face(Geo g, StFaces sf, const do
   double dot = 0.;
   // the listed rows' blocks first (their gathers are the launch's longest chains: nine dependent
   // rounds per node before round 6's st_tail16, one now), started before the patches
-  constexpr int LPB = SFP_T / ST16;  // listed rows per block (16 lanes each, st_tail16)
+  constexpr int LPB = L16 ? SFP_T / ST16 : SFP_T;  // listed rows per block (L16: 16 lanes each, st_tail16)
   const int64_t NLB = (cnt + LPB - 1) / LPB;
   if ((int64_t)blockIdx.x >= NLB) {
     const SfPatch q = sf_patch(g, sf, blockIdx.x - NLB);
@@ -3593,7 +3593,8 @@ __global__ __launch_bounds__(SFP_T) void k_spmv_face(Geo g, StFaces sf, const do
     sf_rows(g, q, coef, slot, S, y, dot, threadIdx.x);
   } else {
     const int64_t lo = (int64_t)blockIdx.x * LPB;
-    st_tail16<SFP_T>(g, list, lo, min(cnt, lo + LPB), I, bdict, exc, x, y, reinterpret_cast<double2*>(S), dot);
+    if (L16) st_tail16<SFP_T>(g, list, lo, min(cnt, lo + LPB), I, bdict, exc, x, y, reinterpret_cast<double2*>(S), dot);
+    else st_tail<SFP_T>(g, list, lo, min(cnt, lo + LPB), I, bdict, exc, x, y, reinterpret_cast<double2*>(S), dot);
   }
   if (DOT) {
     const double sm = block_sum<SFP_T>(dot, sh);
@@ -5386,9 +5387,19 @@ static ZTiling sp_tiling(const Ctx& c) {
   return t;
 }
 
+// the listed rows 16 lanes per node (st_tail16) while they fill at most a fifth of a resident round
+// of the device (1,024 threads per CU); beyond that one thread per node (st_tail): 16 lanes issue
+// every row's 27 FMAs nine times over, which a long list pays in VALU time (128^3 sweep: config 5's
+// few thousand listed rows, face kernel 12.0 vs 24.4 us; 3-7 % exception nodes, CG iteration
+// 0.183-0.252 vs 0.168-0.203 ms, profiles/r06zb_*, r06zc_*).  Option vi_st_l16: 1 / 0 force, -1 = this rule
+static bool st_l16(const Ctx& c) {
+  return c.vi_st_l16 > 0 || (c.vi_st_l16 < 0 && (int64_t)ST16 * c.st_n * 5 <= (int64_t)c.g.ncu * 1024);
+}
+
 // k_spmv_face's blocks (the face phase and the listed rows as a kernel of their own: vi_st_tail 0)
 static int64_t stface_blocks(const Ctx& c) {
-  return st_used(c) && !c.vi_st_tail ? c.st_faces.u[6] + (c.st_n + SFP_T / ST16 - 1) / (SFP_T / ST16) : 0;
+  const int lpb = st_l16(c) ? SFP_T / ST16 : SFP_T;
+  return st_used(c) && !c.vi_st_tail ? c.st_faces.u[6] + (c.st_n + lpb - 1) / lpb : 0;
 }
 
 // the exception rows' kernel (staged block-indexed storage with exception nodes, vi_exc_kernel)
@@ -6150,7 +6161,11 @@ static void launch_spmv_fusep(Ctx& c, double* y) {
       hipLaunchKernelGGL((k_spmv_sp<true, true, 8, true>), dim3(nb), dim3(512), 0, c.stream, c.g, c.st_coef,
                          c.st_mask, c.st_npx, c.st_npy, nullptr, y, c.partials, c.cg, zt, fp);
     const int64_t nbfa = stface_blocks(c);
-    if (nbfa)
+    if (nbfa && !st_l16(c))
+      hipLaunchKernelGGL((k_spmv_face<true, true, false>), dim3((unsigned)nbfa), dim3(SFP_T), 0, c.stream, c.g,
+                         c.st_faces, c.st_coef, c.st_slot, c.cg_it & 1 ? c.p_pad2 : c.p_pad, y, c.partials + nb, c.cg,
+                         c.st_list, c.st_n, I, c.vi_bdict, c.vi_exc);
+    else if (nbfa)
       hipLaunchKernelGGL((k_spmv_face<true, true>), dim3((unsigned)nbfa), dim3(SFP_T), 0, c.stream, c.g, c.st_faces,
                          c.st_coef, c.st_slot, c.cg_it & 1 ? c.p_pad2 : c.p_pad, y, c.partials + nb, c.cg, c.st_list,
                          c.st_n, I, c.vi_bdict, c.vi_exc);
@@ -6246,9 +6261,13 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
     else                                                                                                          \
       hipLaunchKernelGGL((k_spmv_st<DV, GV>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,         \
                          c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);                                      \
-    if (nbfa)                                                                                                     \
+    if (nbfa && st_l16(c))                                                                                        \
       hipLaunchKernelGGL((k_spmv_face<DV, GV>), dim3((unsigned)nbfa), dim3(SFP_T), 0, c.stream, c.g, c.st_faces,    \
                          c.st_coef, c.st_slot, xpad, y, pf, c.cg, c.st_list, c.st_n, I, c.vi_bdict, c.vi_exc);    \
+    else if (nbfa)                                                                                                \
+      hipLaunchKernelGGL((k_spmv_face<DV, GV, false>), dim3((unsigned)nbfa), dim3(SFP_T), 0, c.stream, c.g,         \
+                         c.st_faces, c.st_coef, c.st_slot, xpad, y, pf, c.cg, c.st_list, c.st_n, I, c.vi_bdict,   \
+                         c.vi_exc);                                                                               \
   } while (0)
         if (dot && gated) MCX_ST(true, true);
         else if (dot) MCX_ST(true, false);

@@ -265,6 +265,8 @@ struct Ctx {
   int vi_st = -1;            // default-stencil SpMV (k_spmv_st + k_spmv_face, option vi_st; FMA rows, 64 x 16 tiles):
                              // -1 (default) from ST_MIN_NODES owned nodes up or with <= 10 % exception nodes, 0 off, 1 on
   int vi_st_faces = 1;       // the domain faces as stencil classes of their own (option vi_st_faces: 1 all, 0 none (listed), else bit c = class c)
+  int vi_st_l16 = -1;        // k_spmv_face's listed rows: 16 lanes per node, loads in parallel (option vi_st_l16 1; 0: one
+                             // thread per node, st_tail; -1: 16 lanes while the list is short, kernels.hip st_l16)
   int vi_st_pf = 1;          // k_spmv_st's prefetch distance in steps (option vi_st_pf 1 | 2)
   int vi_st_ty = 16;         // k_spmv_sp's tile height (option vi_st_ty: 8 = 512-thread blocks, two per CU; 16 = 1024)
   int vi_st_pair = 0;        // the march as k_spmv_sp (x-pair lanes, round 6; option vi_st_pair 1; the fused p update

@@ -276,6 +276,9 @@ def test_aij_vi_exception_nodes(grid, stage, vi_tx, tile):
         m.set_option("vi_lg_exc", 1)
         m.set_option("vi_st", 1)  # default-stencil kernel: exception nodes among the listed rows
         assert np.array_equal(m.spmv(x), y)
+        for l16 in (0, 1, -1):  # the listed rows one thread per node / 16 lanes per node (round 6) / by length
+            m.set_option("vi_st_l16", l16)
+            assert np.array_equal(m.spmv(x), y), l16
         its, rn, reason = m.solve_Ax()
         assert reason > 0 and abs(its - ref_its) <= 1
         assert np.linalg.norm(m.du() - P.du()) <= 50 * rtol * np.linalg.norm(P.du())
@@ -815,6 +818,10 @@ def test_st_face_classes(N):
             m.set_option("vi_st_tail", 1)
             assert np.array_equal(m.spmv(x), y), zblocks
             m.set_option("vi_st_tail", 0)
+            for l16 in (0, 1):  # listed rows one thread per node (st_tail) / 16 lanes per node (st_tail16)
+                m.set_option("vi_st_l16", l16)
+                assert np.array_equal(m.spmv(x), y), (zblocks, "l16", l16)
+            m.set_option("vi_st_l16", -1)
             # the x-pair march k_spmv_sp (round 6), 64 x 16 and 64 x 8 tiles: the same rows
             m.set_option("vi_st_pair", 1)
             for ty in (16, 8):

@@ -29,9 +29,12 @@ ap.add_argument("--gamma", type=float, default=1e-2, help="shear strain of the p
 a = ap.parse_args()
 G = a.grid
 ARGS = {"aij-vi": ["-dm_mat_type", "aij"], "aij-vi-exck": ["-dm_mat_type", "aij"], "aij-vi-pass": ["-dm_mat_type", "aij"],
+        "aij-vi-l1": ["-dm_mat_type", "aij"], "aij-vi-l16": ["-dm_mat_type", "aij"],
         "aij-split": ["-dm_mat_type", "aij"], "sbaij": ["-dm_mat_type", "sbaij"]}
 # aij-vi: the default (default-stencil kernel, exception rows among its listed rows); aij-vi-exck: vi_st 0 with
-# the exception kernel; aij-vi-pass: vi_st 0 with round 4's in-tile exception pass (vi_exc_kernel 0)
+# the exception kernel; aij-vi-pass: vi_st 0 with round 4's in-tile exception pass (vi_exc_kernel 0);
+# aij-vi-l1 / aij-vi-l16: as aij-vi with the listed rows one thread per node (vi_st_l16 0, round 5's form) /
+# 16 lanes per node (vi_st_l16 1); aij-vi: the rule (vi_st_l16 -1)
 lx = 50.0
 dx = lx / (G - 1)
 i = np.arange(G)
@@ -55,7 +58,8 @@ for frac in [float(f) for f in a.fracs.split(",")]:
             if st.startswith("aij-vi"):
                 m.set_option("vi_exc_max", 1000)
                 m.set_option("vi_exc_kernel", 0 if st == "aij-vi-pass" else 1)
-                m.set_option("vi_st", 1 if st == "aij-vi" else 0)
+                m.set_option("vi_st", 1 if st in ("aij-vi", "aij-vi-l1", "aij-vi-st") else 0)
+                m.set_option("vi_st_l16", 0 if st == "aij-vi-l1" else (1 if st == "aij-vi-l16" else -1))
             elif st == "aij-split":
                 m.set_option("vi_exc_max", 0)
             m.set_u(u)
