@@ -90,6 +90,7 @@ static int free_ctx(Ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm_stream) (void)hipStreamSynchronize(c->comm_stream);
   if (c->x_stream) (void)hipStreamSynchronize(c->x_stream);
+  if (c->f_stream) (void)hipStreamSynchronize(c->f_stream);
   void* ptrs[] = {c->hist_old, c->hist_new, c->ftrial, c->b, c->du, c->r, c->z, c->w, c->jix, c->jdd, c->V, c->U, c->D, c->d_mask, c->vi_idx, c->wd, c->vi_dict, c->vi_keys, c->vi_slot, c->vi_ctl, c->vi_bdict, c->eps, c->sig, c->ctan, c->Ke,
                   c->vib_keys, c->vib_ctl, c->vib_pos, c->ke_uni, c->xdone, c->esc_node, c->esc_res, c->esc_slot, c->elem_plain, c->cref, c->vi_xslot,
                   c->vi_xlist, c->vi_xcnt, c->vi_exc, c->st_coef, c->st_ids, c->st_slot, c->st_list, c->st_cnt, c->st_mask,
@@ -114,7 +115,8 @@ static int free_ctx(Ctx* c) {
   if (c->ev_comm) (void)hipEventDestroy(c->ev_comm);
   if (c->comm_stream) (void)hipStreamDestroy(c->comm_stream);
   if (c->x_stream) (void)hipStreamDestroy(c->x_stream);
-  for (hipEvent_t e : {c->ev_xp, c->ev_xd[0], c->ev_xd[1]})
+  if (c->f_stream) (void)hipStreamDestroy(c->f_stream);
+  for (hipEvent_t e : {c->ev_xp, c->ev_xd[0], c->ev_xd[1], c->ev_fx, c->ev_fd})
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1676,6 +1678,10 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
       set_error("vi_st_pair: partials buffer too small");
       return 2;
     }
+    return 0;
+  }
+  if (!std::strcmp(name, "vi_st_fstream")) {
+    c.vi_st_fstream = value != 0.;
     return 0;
   }
   if (!std::strcmp(name, "vi_st_l16")) {

@@ -6186,6 +6186,26 @@ static void launch_spmv_fusep(Ctx& c, double* y) {
 #undef MCX_VIBM_FP
 }
 
+// the face kernel on a stream of its own beside the march (option vi_st_fstream): the march holds
+// one 1,024-thread block per CU at 104 VGPRs and 115 KB of LDS, which leaves room for one
+// 256-thread face block (96 VGPRs, 28.5 KB) per CU in the march's idle issue slots.  The stream and
+// its two events are made on first use; any failure keeps the faces on the compute stream.
+static bool fstream_ok(Ctx& c) {
+  if (!c.vi_st_fstream) return false;
+  if (!c.f_stream && hipStreamCreateWithFlags(&c.f_stream, hipStreamNonBlocking) != hipSuccess) {
+    c.f_stream = nullptr;
+    c.vi_st_fstream = 0;
+    return false;
+  }
+  for (hipEvent_t* e : {&c.ev_fx, &c.ev_fd})
+    if (!*e && hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) {
+      *e = nullptr;
+      c.vi_st_fstream = 0;
+      return false;
+    }
+  return true;
+}
+
 // k_spmv_sp's timing-only diagnostic instantiations (option split_dbg; wrong products, see DBG)
 template <bool DV, bool GV, int D>
 static void sp_dbg1(Ctx& c, int nb, const double* xpad, double* y, const ZTiling& zt) {
@@ -6240,6 +6260,9 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
 #define MCX_SP_DBG(DV, GV) sp_dbg<DV, GV>(c, nb, xpad, y, zt)
 #define MCX_ST(DV, GV)                                                                                             \
   do {                                                                                                            \
+    const bool fs = nbfa && !c.vi_st_tail && fstream_ok(c); /* the faces beside the march (vi_st_fstream) */       \
+    hipStream_t fst = fs ? c.f_stream : c.stream;                                                                 \
+    if (fs) (void)hipEventRecord(c.ev_fx, c.stream);                                                              \
     if (c.vi_st_tail)                                                                                             \
       hipLaunchKernelGGL((k_spmv_st<DV, GV, true>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,   \
                          c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt, c.st_list, c.st_n, I, c.vi_bdict,     \
@@ -6261,13 +6284,18 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
     else                                                                                                          \
       hipLaunchKernelGGL((k_spmv_st<DV, GV>), dim3(nb), dim3(1024), 0, c.stream, c.g, c.st_coef, c.st_mask,         \
                          c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);                                      \
+    if (fs) (void)hipStreamWaitEvent(fst, c.ev_fx, 0);                                                            \
     if (nbfa && st_l16(c))                                                                                        \
-      hipLaunchKernelGGL((k_spmv_face<DV, GV>), dim3((unsigned)nbfa), dim3(SFP_T), 0, c.stream, c.g, c.st_faces,    \
+      hipLaunchKernelGGL((k_spmv_face<DV, GV>), dim3((unsigned)nbfa), dim3(SFP_T), 0, fst, c.g, c.st_faces,         \
                          c.st_coef, c.st_slot, xpad, y, pf, c.cg, c.st_list, c.st_n, I, c.vi_bdict, c.vi_exc);    \
     else if (nbfa)                                                                                                \
-      hipLaunchKernelGGL((k_spmv_face<DV, GV, false>), dim3((unsigned)nbfa), dim3(SFP_T), 0, c.stream, c.g,         \
+      hipLaunchKernelGGL((k_spmv_face<DV, GV, false>), dim3((unsigned)nbfa), dim3(SFP_T), 0, fst, c.g,              \
                          c.st_faces, c.st_coef, c.st_slot, xpad, y, pf, c.cg, c.st_list, c.st_n, I, c.vi_bdict,   \
                          c.vi_exc);                                                                               \
+    if (fs) {                                                                                                     \
+      (void)hipEventRecord(c.ev_fd, fst);                                                                         \
+      (void)hipStreamWaitEvent(c.stream, c.ev_fd, 0);                                                             \
+    }                                                                                                             \
   } while (0)
         if (dot && gated) MCX_ST(true, true);
         else if (dot) MCX_ST(true, false);

@@ -176,6 +176,9 @@ struct Ctx {
   int cg_xs = 0;             // quad-buffered p: the four owed VecAXPY(x) terms on a side stream (option cg_xs)
   bool xs_used = false;      // this solve: eight p buffers, k_cg_xwin on x_stream
   hipStream_t x_stream = nullptr;
+  hipStream_t f_stream = nullptr;                  // k_spmv_face beside the march (vi_st_fstream)
+  hipEvent_t ev_fx = nullptr, ev_fd = nullptr;     // p ready for the face stream / the faces done
+  int vi_st_fstream = 0;                           // option vi_st_fstream
   hipEvent_t ev_xp = nullptr, ev_xd[2] = {nullptr, nullptr};
   int cg_fusep = 0;          // option cg_fusep: fuse the CG p update into the value-indexed SpMV (single rank; A/B: no gain)
   bool fusep_used = false;   // the last solve ran the fused kernel (timing: its bytes per launch)

@@ -822,6 +822,9 @@ def test_st_face_classes(N):
                 m.set_option("vi_st_l16", l16)
                 assert np.array_equal(m.spmv(x), y), (zblocks, "l16", l16)
             m.set_option("vi_st_l16", -1)
+            m.set_option("vi_st_fstream", 1)  # the face kernel on its own stream beside the march
+            assert np.array_equal(m.spmv(x), y), (zblocks, "fstream")
+            m.set_option("vi_st_fstream", 0)
             # the x-pair march k_spmv_sp (round 6), 64 x 16 and 64 x 8 tiles: the same rows
             m.set_option("vi_st_pair", 1)
             for ty in (16, 8):
