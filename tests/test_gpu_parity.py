@@ -897,3 +897,37 @@ def test_cg_fused_p_update_bitwise(maxits, st):
         assert (its, reason) == out[0][:2] and np.array_equal(du, out[0][2])
     if maxits:
         assert out[0][:2] == (maxits, -3)
+
+
+def test_partials_guard_near_the_limit():
+    """the SpMV's partial sums (the march's blocks, then k_spmv_face's: its patches and
+    listed-row blocks) must fit half of the partials buffer, because the fused update kernels read
+    the SpMV's half while writing the other.  Every grid-changing option is checked against
+    spmv_nparts (not just the march's grid): spmv_zblocks raised step by step with vi_st 1 is
+    either refused (the setting left as it was) or the solve stays the unperturbed one."""
+    NX, NY, NZ = 70, 20, 12
+    rtol = 1e-12
+    with M.Macroc(argv_for(NX, NY, NZ, rtol)) as m:
+        m.set_option("vi_stage", 1)
+        m.set_option("vi_st", 1)
+        m.apply_bc_on_u(m.get_displacement(1))
+        m.set_strains(); m.homogenize(); m.assembly_res(); m.assembly_jac()
+        assert m.get_info()["st_listed"] >= 0
+        its0, _, reason0 = m.solve_Ax()
+        du0 = m.du()
+        refused = accepted = 0
+        for zb in (1, 4, 16, 64, 256, 1024, 4096, 16384, 65536):
+            try:
+                m.set_option("spmv_zblocks", zb)
+            except M.MacrocError as e:
+                assert "partials buffer too small" in str(e)
+                refused += 1
+                continue
+            accepted += 1
+            its, _, reason = m.solve_Ax()
+            assert reason == reason0 and abs(its - its0) <= 1, (zb, its, its0)
+            assert np.linalg.norm(m.du() - du0) <= 1e-10 * np.linalg.norm(du0), zb
+        assert accepted and refused, (accepted, refused)
+        # a refused value left the last accepted one in place: the solve is still the same
+        its, _, reason = m.solve_Ax()
+        assert reason == reason0 and abs(its - its0) <= 1
