@@ -1555,6 +1555,10 @@ int mcx_set_option(void* ctx, const char* name, double value) try {
     c.split_dbg = std::max(0, std::min(2047, (int)value));  // (k_spmv_sp DBG: bits, see the kernel)
     return 0;
   }
+  if (!std::strcmp(name, "face_dbg")) {  // timing-only (wrong products): bits 1 listed rows, 2 x faces, 4 y/z faces dropped
+    c.face_dbg = std::max(0, std::min(7, (int)value));
+    return 0;
+  }
   if (!std::strcmp(name, "split_tx")) {
     const int v = (int)value;
     if (v != 0 && v != 64 && v != 128 && v != 256) {

@@ -3147,21 +3147,21 @@ __device__ __forceinline__ void st_tail16(const Geo& g, const int* __restrict__ 
   lds_double* tab = (lds_double*)tabg;
   const int me = threadIdx.x;
   if (lo >= hi) return;  // (uniform)
-  for (int q = me; q < VI_MAX * VIB_STRIDE; q += T) tab[q] = bdict[q];
-  __syncthreads();
   const int PX = g.PX, PXY = g.PX * g.PY;
   const int g9 = me & (ST16 - 1);
-  for (int64_t t0 = lo; t0 < hi; t0 += T / ST16) {  // (uniform)
+  // a pass's global loads (list entry, x row, index words): the first pass's are issued before the
+  // dictionary staging and its barrier, so the two round trips overlap (k_spmv_face gives a block
+  // one pass; the barrier waits for LDS only, the loads stay in flight)
+  int64_t n = 0;
+  double xw[9];
+  u32x4 w0 = {0u, 0u, 0u, 0u}, w1 = {0u, 0u, 0u, 0u};
+  auto fetch = [&](int64_t t0) {
     const int64_t t = t0 + me / ST16;
-    const bool has = t < hi;
-    const bool row = has && g9 < 9;
-    double xw[9], av[27];
+    n = 0;
 #pragma unroll
     for (int q = 0; q < 9; q++) xw[q] = 0.;
-#pragma unroll
-    for (int q = 0; q < 27; q++) av[q] = 0.;
-    int64_t n = 0;
-    if (row) {
+    w0 = w1 = u32x4{0u, 0u, 0u, 0u};
+    if (t < hi && g9 < 9) {
       n = list[t];
       int i, j, k;
       node_ijk(g, (int)n, i, j, k);
@@ -3170,7 +3170,30 @@ __device__ __forceinline__ void st_tail16(const Geo& g, const int* __restrict__ 
 #pragma unroll
       for (int q = 0; q < 9; q++) xw[q] = xr[q];
       const u32x4* ip = I + (n >> 6) * (2 * 64) + (n & 63);
-      const u32x4 w0 = ip[0], w1 = ip[64];
+      w0 = ip[0];
+      w1 = ip[64];
+    }
+  };
+  fetch(lo);
+  {
+    constexpr int ND = (VI_MAX * VIB_STRIDE + T - 1) / T;
+    double dv[ND];  // all the staging loads in flight before the LDS stores
+#pragma unroll
+    for (int m = 0; m < ND; m++) dv[m] = me + m * T < VI_MAX * VIB_STRIDE ? bdict[me + m * T] : 0.;
+#pragma unroll
+    for (int m = 0; m < ND; m++)
+      if (me + m * T < VI_MAX * VIB_STRIDE) tab[me + m * T] = dv[m];
+  }
+  __syncthreads();
+  for (int64_t t0 = lo; t0 < hi; t0 += T / ST16) {  // (uniform)
+    if (t0 != lo) fetch(t0);
+    const int64_t t = t0 + me / ST16;
+    const bool has = t < hi;
+    const bool row = has && g9 < 9;
+    double av[27];
+#pragma unroll
+    for (int q = 0; q < 27; q++) av[q] = 0.;
+    if (row) {
       const unsigned slot = w1[3];  // exception slot + 1
       const double* eb = exc + exc_base(slot ? slot - 1 : 0);
 #pragma unroll
@@ -3251,35 +3274,50 @@ __device__ __forceinline__ SfPatch sf_patch(const Geo& g, const StFaces& sf, int
   return q;
 }
 
-// stage patch q's x into S (t = 0 .. SFP_T-1: the patch's threads)
+// stage patch q's x into S (t = 0 .. SFP_T-1: the patch's threads).  Branch-free buffer loads from
+// the patch's origin (a position outside the neighbour grid, or the outward ghost the rows leave
+// out, is the out-of-range offset: the load returns 0), the face axis's index arithmetic chosen once
+// per patch (uniform), all loads in flight before the LDS stores
 __device__ __forceinline__ void sf_stage(const Geo& g, const SfPatch& q, const double* __restrict__ x, double* S,
                                          int t) {
-  const int PX = g.PX, PXY = g.PX * g.PY;
-  const int iface = q.hi ? g.nx - 1 : 0, jface = q.hi ? g.ny - 1 : 0, kface = q.hi ? g.nz - 1 : 0;
+  const int PX = g.PX;
+  const int64_t PXY = (int64_t)g.PX * g.PY;
+  const int gh = q.hi ? 2 : 0;
   constexpr int NE = (SFP_N + SFP_T - 1) / SFP_T;
-  double v[NE];  // all loads in flight before the LDS stores (a load-store round trip each: NE HBM latencies)
+  // origin: padded node (i', j', k') of the staged grid's first element
+  const int iface = q.hi ? g.nx - 1 : 0, jface = q.hi ? g.ny - 1 : 0, kface = q.hi ? g.nz - 1 : 0;
+  int64_t o0;
+  if (q.ax == 0) o0 = iface + (int64_t)q.f0 * PX + (int64_t)q.s0 * PXY;
+  else if (q.ax == 1) o0 = q.f0 + (int64_t)jface * PX + (int64_t)q.s0 * PXY;
+  else o0 = q.f0 + (int64_t)q.s0 * PX + (int64_t)kface * PXY;
+  const __amdgpu_buffer_rsrc_t rx = sp_rsrc(x + 3 * o0, (PXY * g.PZ - o0) * 24);
+  const int PX3 = 3 * PX, PXY3 = (int)(3 * PXY);
+  unsigned off[NE];
+  if (q.ax == 0) {  // 9-double chunks (i-1 .. i+1) of the (SFP_S+2) x 66 (k', j') grid
+    const int jmax = g.ny + 1 - q.f0, kmax = g.nz + 1 - q.s0;  // last staged jj / kk inside the padded box
 #pragma unroll
-  for (int m = 0; m < NE; m++) {
-    const int e = t + m * SFP_T;
-    int pi, jp, kp, o;  // padded column of the chunk / segment start, local j', k', offset
-    bool ok;
-    if (q.ax == 0) {  // 9-double chunks, (kk, jj) of (SFP_S+2) x 66
-      const int ch = e / 9, jj = ch % 66;
-      o = e - ch * 9;
-      pi = iface;
-      jp = q.f0 - 1 + jj;
-      kp = q.s0 - 1 + ch / 66;
-      ok = e < SFP_N && jp <= g.ny && kp <= g.nz;
-    } else {  // 198-double segments: y-face (kk, dy) of (SFP_S+2) x 3, z-face (dz, jj) of 3 x (SFP_S+2)
-      const int r = e / 198;
-      o = e - r * 198;
-      pi = q.f0;
-      if (q.ax == 1) jp = jface - 1 + r % 3, kp = q.s0 - 1 + r / 3;
-      else jp = q.s0 - 1 + r % (SFP_S + 2), kp = kface - 1 + r / (SFP_S + 2);
-      ok = e < SFP_N && o < 3 * (g.nx + 2 - q.f0) && jp <= g.ny && kp <= g.nz;
+    for (int m = 0; m < NE; m++) {
+      const int e = t + m * SFP_T, ch = e / 9, o = e - ch * 9, kk = ch / 66, jj = ch - kk * 66;
+      const bool ok = e < SFP_N && jj <= jmax && kk <= kmax && o / 3 != gh;
+      off[m] = ok ? 8u * (unsigned)(jj * PX3 + kk * PXY3 + o) : SP_OOB;
     }
-    v[m] = ok ? x[3 * ((int64_t)pi + (jp + 1) * (int64_t)PX + (kp + 1) * (int64_t)PXY) + o] : 0.;
+  } else {  // 198-double segments: y-face (kk, dy) of (SFP_S+2) x 3, z-face (dz, jj) of 3 x (SFP_S+2)
+    const int omax = 3 * (g.nx + 2 - q.f0);
+    const int smax = (q.ax == 1 ? g.nz : g.ny) + 1 - q.s0;  // last staged slow-axis row inside the box
+#pragma unroll
+    for (int m = 0; m < NE; m++) {
+      const int e = t + m * SFP_T, r = e / 198, o = e - r * 198;
+      int nr, sr;  // the row's normal-axis position (0 .. 2) and slow-axis position (0 .. SFP_S+1)
+      if (q.ax == 1) nr = r % 3, sr = r / 3;
+      else sr = r % (SFP_S + 2), nr = r / (SFP_S + 2);
+      const bool ok = e < SFP_N && o < omax && sr <= smax && nr != gh;
+      const int ro = q.ax == 1 ? nr * PX3 + sr * PXY3 : sr * PX3 + nr * PXY3;
+      off[m] = ok ? 8u * (unsigned)(ro + o) : SP_OOB;
+    }
   }
+  double v[NE];
+#pragma unroll
+  for (int m = 0; m < NE; m++) v[m] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rx, off[m], 0, 0));
 #pragma unroll
   for (int m = 0; m < NE; m++)
     if (t + m * SFP_T < SFP_N) S[t + m * SFP_T] = v[m];
@@ -3302,29 +3340,38 @@ __device__ __forceinline__ void sf_rows(const Geo& g, const SfPatch& q, const do
   const bool live = in && slot[n] == 0u;
   const double* cf = coef + q.c * 27 * VIB_STRIDE;  // (uniform) the class's stencil
   double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
+  // The outward neighbours of a face node are the global boundary's ghosts (x = 0; their blocks are
+  // zero blocks): their terms are left out (fma(a, 0, y) = y, and y, summed from +0, is never -0),
+  // so y is bitwise the full row's with a third fewer LDS reads, scalar loads and FMAs.
+  const int gh = q.hi ? 2 : 0;  // the ghost's position in the (dx | dy | dz) + 1 range of the face normal
   // a rolled loop over the stencil rows (unrolled, the compiler hoists the rows' scalar loads and spills)
 #pragma unroll 1
   for (int g9 = 0; g9 < 9; g9++) {
     const int dy = g9 % 3 - 1, dz = g9 / 3 - 1;
+    if ((q.ax == 1 && dy + 1 == gh) || (q.ax == 2 && dz + 1 == gh)) continue;  // (uniform) a ghost row
     const int base = q.ax == 0 ? ((w + 1 + dz) * 66 + (ln + 1 + dy)) * 9
                    : q.ax == 1 ? ((w + 1 + dz) * 3 + (dy + 1)) * 198 + 3 * ln
                                : ((dz + 1) * (SFP_S + 2) + (w + 1 + dy)) * 198 + 3 * ln;
     double xw[9], av[27];
 #pragma unroll
-    for (int qq = 0; qq < 9; qq++) xw[qq] = Sl[base + qq];
+    for (int t3 = 0; t3 < 3; t3++) {
+      if (q.ax == 0 && t3 == gh) continue;  // (uniform) the ghost column
 #pragma unroll
-    for (int t3 = 0; t3 < 3; t3++)
+      for (int qq = 0; qq < 3; qq++) xw[3 * t3 + qq] = Sl[base + 3 * t3 + qq];
 #pragma unroll
       for (int qq = 0; qq < 9; qq++) av[t3 * 9 + qq] = cf[(g9 * 3 + t3) * VIB_STRIDE + qq];
+    }
     if (g9 == 4) xc0 = xw[3], xc1 = xw[4], xc2 = xw[5];
 #pragma unroll
-    for (int t3 = 0; t3 < 3; t3++)
+    for (int t3 = 0; t3 < 3; t3++) {
+      if (q.ax == 0 && t3 == gh) continue;
 #pragma unroll
       for (int qq = 0; qq < 9; qq++) {
         const int r = qq / 3, cc = qq % 3;
         double& yr = r == 0 ? y0 : (r == 1 ? y1 : y2);
         yr = __builtin_fma(av[t3 * 9 + qq], xw[3 * t3 + cc], yr);
       }
+    }
   }
   if (live) {
     __builtin_nontemporal_store(y0, &y[3 * n + 0]);
@@ -6255,7 +6302,19 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
           zt = sp_tiling(c);
           zt.dbg = dbg;
         }
-        const int64_t nbfa = stface_blocks(c);
+        StFaces sfv = c.st_faces;
+        int64_t stn = c.st_n, nbfa = stface_blocks(c);
+        if (c.face_dbg && nbfa) {  // timing-only (option face_dbg, wrong products): drop listed rows / x / y-z patches
+          if (c.face_dbg & 1) stn = 0;
+          if (c.face_dbg & 2) {
+            const int64_t d = sfv.u[2];
+            for (int q = 1; q < 7; q++) sfv.u[q] = std::max<int64_t>(0, sfv.u[q] - d);
+          }
+          if (c.face_dbg & 4)
+            for (int q = 3; q < 7; q++) sfv.u[q] = sfv.u[2];
+          const int lpb = st_l16(c) ? SFP_T / ST16 : SFP_T;
+          nbfa = sfv.u[6] + (stn + lpb - 1) / lpb;
+        }
         double* pf = c.partials + nb;
 #define MCX_SP_DBG(DV, GV) sp_dbg<DV, GV>(c, nb, xpad, y, zt)
 #define MCX_ST(DV, GV)                                                                                             \
@@ -6286,11 +6345,11 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
                          c.st_npx, c.st_npy, xpad, y, c.partials, c.cg, zt);                                      \
     if (fs) (void)hipStreamWaitEvent(fst, c.ev_fx, 0);                                                            \
     if (nbfa && st_l16(c))                                                                                        \
-      hipLaunchKernelGGL((k_spmv_face<DV, GV>), dim3((unsigned)nbfa), dim3(SFP_T), 0, fst, c.g, c.st_faces,         \
-                         c.st_coef, c.st_slot, xpad, y, pf, c.cg, c.st_list, c.st_n, I, c.vi_bdict, c.vi_exc);    \
+      hipLaunchKernelGGL((k_spmv_face<DV, GV>), dim3((unsigned)nbfa), dim3(SFP_T), 0, fst, c.g, sfv,                \
+                         c.st_coef, c.st_slot, xpad, y, pf, c.cg, c.st_list, stn, I, c.vi_bdict, c.vi_exc);    \
     else if (nbfa)                                                                                                \
       hipLaunchKernelGGL((k_spmv_face<DV, GV, false>), dim3((unsigned)nbfa), dim3(SFP_T), 0, fst, c.g,              \
-                         c.st_faces, c.st_coef, c.st_slot, xpad, y, pf, c.cg, c.st_list, c.st_n, I, c.vi_bdict,   \
+                         sfv, c.st_coef, c.st_slot, xpad, y, pf, c.cg, c.st_list, stn, I, c.vi_bdict,   \
                          c.vi_exc);                                                                               \
     if (fs) {                                                                                                     \
       (void)hipEventRecord(c.ev_fd, fst);                                                                         \

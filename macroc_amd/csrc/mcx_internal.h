@@ -305,6 +305,7 @@ struct Ctx {
   int split_dense = 1;       // corrections beyond split_maxq quads: 1 = all 120 slots + a second pass, 0 = AIJ blocks
   bool split_declined = false;  // a correction was not exact (or dense ones are refused): assemble AIJ blocks directly
   int split_dbg = 0;         // timing-only diagnostics of the split SpMV (option split_dbg)
+  int face_dbg = 0;          // timing-only: k_spmv_face without (1) listed rows, (2) x-face, (4) y/z-face patches
   int split_wide = 0;        // force f32 corrections (testing the wide path)
   int split_tx = 0;          // AIJ-split tile width (0: by subdomain width, 4 rows; else 1024 / split_tx rows)
   int split_ty = 0;          // AIJ-split: 2 with split_tx 256 selects 256x2 tiles (option split_ty)
