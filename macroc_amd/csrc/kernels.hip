@@ -3073,15 +3073,34 @@ __device__ __forceinline__ void st_tail(const Geo& g, const int* __restrict__ li
   lds_double* tab = (lds_double*)tabg;  // (the ring's LDS: ds_read, not flat loads)
   const int me = threadIdx.x;
   if (lo >= hi) return;  // (uniform) no share: no dictionary staging
-  for (int q = me; q < VI_MAX * VIB_STRIDE; q += T) tab[q] = bdict[q];
+  // the first node's list entry and index words are loaded before the dictionary staging and its
+  // barrier (which waits for LDS only), so their round trips overlap the staging's
+  int n = 0;
+  u32x4 w0 = {0u, 0u, 0u, 0u}, w1 = {0u, 0u, 0u, 0u};
+  auto fetch = [&](int64_t t) {
+    if (t < hi) {
+      n = list[t];
+      const u32x4* ip = I + (int64_t)(n >> 6) * (2 * 64) + (n & 63);
+      w0 = ip[0];
+      w1 = ip[64];
+    }
+  };
+  fetch(lo + me);
+  {
+    constexpr int ND = (VI_MAX * VIB_STRIDE + T - 1) / T;
+    double dv[ND];  // all the staging loads in flight before the LDS stores
+#pragma unroll
+    for (int m = 0; m < ND; m++) dv[m] = me + m * T < VI_MAX * VIB_STRIDE ? bdict[me + m * T] : 0.;
+#pragma unroll
+    for (int m = 0; m < ND; m++)
+      if (me + m * T < VI_MAX * VIB_STRIDE) tab[me + m * T] = dv[m];
+  }
   __syncthreads();
   const int PX = g.PX, PXY = g.PX * g.PY;
   for (int64_t t = lo + me; t < hi; t += T) {
-    const int n = list[t];
+    if (t != lo + me) fetch(t);
     int i, j, k;
     node_ijk(g, n, i, j, k);
-    const u32x4* ip = I + (int64_t)(n >> 6) * (2 * 64) + (n & 63);
-    const u32x4 w0 = ip[0], w1 = ip[64];
     const unsigned slot = w1[3];  // exception slot + 1
     const double* eb = exc + exc_base(slot ? slot - 1 : 0);
     double y0 = 0., y1 = 0., y2 = 0., xc0 = 0., xc1 = 0., xc2 = 0.;
@@ -5434,13 +5453,15 @@ static ZTiling sp_tiling(const Ctx& c) {
   return t;
 }
 
-// the listed rows 16 lanes per node (st_tail16) while they fill at most a fifth of a resident round
-// of the device (1,024 threads per CU); beyond that one thread per node (st_tail): 16 lanes issue
-// every row's 27 FMAs nine times over, which a long list pays in VALU time (128^3 sweep: config 5's
-// few thousand listed rows, face kernel 12.0 vs 24.4 us; 3-7 % exception nodes, CG iteration
-// 0.183-0.252 vs 0.168-0.203 ms, profiles/r06zb_*, r06zc_*).  Option vi_st_l16: 1 / 0 force, -1 = this rule
+// the listed rows 16 lanes per node (st_tail16) while they fill at most half a resident round of the
+// device (1,024 threads per CU: 8,192 rows on 256 CUs); beyond that one thread per node (st_tail):
+// 16 lanes issue every row's 27 FMAs nine times over, which a long list pays in VALU time.  Measured:
+// config 5's few thousand listed rows at 128^3, face kernel 12.0 vs 24.4 us (profiles/r06zb_*);
+// 256^3's 6,370, SpMV 0.2635 vs 0.2666 ms, CG iteration 0.7704 vs 0.7735 ms (r06h2_*); 32,768 or
+// more exception nodes at 128^3, CG iteration 0.159-0.184 vs 0.142-0.175 ms (r06zc_*, r06zd_*,
+// r06h2_*).  Option vi_st_l16: 1 / 0 force, -1 = this rule
 static bool st_l16(const Ctx& c) {
-  return c.vi_st_l16 > 0 || (c.vi_st_l16 < 0 && (int64_t)ST16 * c.st_n * 5 <= (int64_t)c.g.ncu * 1024);
+  return c.vi_st_l16 > 0 || (c.vi_st_l16 < 0 && (int64_t)ST16 * c.st_n * 2 <= (int64_t)c.g.ncu * 1024);
 }
 
 // k_spmv_face's blocks (the face phase and the listed rows as a kernel of their own: vi_st_tail 0)
