@@ -5217,11 +5217,17 @@ __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ part
                                                  double* __restrict__ out, int mode, CgState* cg,
                                                  double* __restrict__ hist, int gated, const CgState* cg_src) {
   __shared__ double sh[16];
+  // the gate and the partials are loaded together, one round trip: the partials are read even by a
+  // finished solve's launch (nothing is written then)
+  // the gate as a vector (buffer) load: waited for with the partials' loads (vmcnt, in order), where a
+  // scalar load's wait (lgkmcnt(0)) would come first, with the kernel arguments'
+  const int reason = (int)__builtin_amdgcn_raw_buffer_load_b32(
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<CgState*>(cg_src), (short)0, (int)sizeof(CgState), 0x00020000),
+      (unsigned)offsetof(CgState, reason), 0, 0);
   if (cg_src != cg && threadIdx.x == 0) *cg = *cg_src;  // read by thread 0 only below
-  if (gated && cg_src->reason) return;
   double res[2] = {0., 0.};
   reduce_parts(part, nparts, nvals, sh, res);
-  if (threadIdx.x) return;
+  if (threadIdx.x || (gated && reason)) return;
   for (int v = 0; v < nvals; v++) out[v] = res[v];
   if (mode == RED_INIT) cg_logic_init(cg, res[0], res[1], hist);
   else if (mode == RED_ALPHA) cg_logic_alpha(cg, res[0]);
