@@ -3068,11 +3068,12 @@ template <int T>
 __device__ __forceinline__ void st_tail(const Geo& g, const int* __restrict__ list, int64_t lo, int64_t hi,
                                         const u32x4* __restrict__ I, const double* __restrict__ bdict,
                                         const double* __restrict__ exc, const double* __restrict__ x,
-                                        double* __restrict__ y, double2* tabg, double& dot) {
+                                        double* __restrict__ y, double2* tabg, double& dot, int nd = VI_MAX) {
   typedef __attribute__((address_space(3))) double lds_double;
   lds_double* tab = (lds_double*)tabg;  // (the ring's LDS: ds_read, not flat loads)
   const int me = threadIdx.x;
   if (lo >= hi) return;  // (uniform) no share: no dictionary staging
+  const int ndv = min(nd, VI_MAX) * VIB_STRIDE;  // staged dictionary doubles (the blocks in use)
   // the first node's list entry and index words are loaded before the dictionary staging and its
   // barrier (which waits for LDS only), so their round trips overlap the staging's
   int n = 0;
@@ -3090,10 +3091,10 @@ __device__ __forceinline__ void st_tail(const Geo& g, const int* __restrict__ li
     constexpr int ND = (VI_MAX * VIB_STRIDE + T - 1) / T;
     double dv[ND];  // all the staging loads in flight before the LDS stores
 #pragma unroll
-    for (int m = 0; m < ND; m++) dv[m] = me + m * T < VI_MAX * VIB_STRIDE ? bdict[me + m * T] : 0.;
+    for (int m = 0; m < ND; m++) dv[m] = me + m * T < ndv ? bdict[me + m * T] : 0.;
 #pragma unroll
     for (int m = 0; m < ND; m++)
-      if (me + m * T < VI_MAX * VIB_STRIDE) tab[me + m * T] = dv[m];
+      if (me + m * T < ndv) tab[me + m * T] = dv[m];
   }
   __syncthreads();
   const int PX = g.PX, PXY = g.PX * g.PY;
@@ -3161,13 +3162,14 @@ template <int T>
 __device__ __forceinline__ void st_tail16(const Geo& g, const int* __restrict__ list, int64_t lo, int64_t hi,
                                           const u32x4* __restrict__ I, const double* __restrict__ bdict,
                                           const double* __restrict__ exc, const double* __restrict__ x,
-                                          double* __restrict__ y, double2* tabg, double& dot) {
+                                          double* __restrict__ y, double2* tabg, double& dot, int nd = VI_MAX) {
   typedef __attribute__((address_space(3))) double lds_double;
   lds_double* tab = (lds_double*)tabg;
   const int me = threadIdx.x;
   if (lo >= hi) return;  // (uniform)
   const int PX = g.PX, PXY = g.PX * g.PY;
   const int g9 = me & (ST16 - 1);
+  const int ndv = min(nd, VI_MAX) * VIB_STRIDE;  // staged dictionary doubles (the blocks in use)
   // a pass's global loads (list entry, x row, index words): the first pass's are issued before the
   // dictionary staging and its barrier, so the two round trips overlap (k_spmv_face gives a block
   // one pass; the barrier waits for LDS only, the loads stay in flight)
@@ -3198,10 +3200,10 @@ __device__ __forceinline__ void st_tail16(const Geo& g, const int* __restrict__ 
     constexpr int ND = (VI_MAX * VIB_STRIDE + T - 1) / T;
     double dv[ND];  // all the staging loads in flight before the LDS stores
 #pragma unroll
-    for (int m = 0; m < ND; m++) dv[m] = me + m * T < VI_MAX * VIB_STRIDE ? bdict[me + m * T] : 0.;
+    for (int m = 0; m < ND; m++) dv[m] = me + m * T < ndv ? bdict[me + m * T] : 0.;
 #pragma unroll
     for (int m = 0; m < ND; m++)
-      if (me + m * T < VI_MAX * VIB_STRIDE) tab[me + m * T] = dv[m];
+      if (me + m * T < ndv) tab[me + m * T] = dv[m];
   }
   __syncthreads();
   for (int64_t t0 = lo; t0 < hi; t0 += T / ST16) {  // (uniform)
@@ -3642,7 +3644,8 @@ __global__ __launch_bounds__(SFP_T) void k_spmv_face(Geo g, StFaces sf, const do
                                                    double* __restrict__ y, double* __restrict__ part,
                                                    const CgState* __restrict__ cg, const int* __restrict__ list,
                                                    int64_t cnt, const u32x4* __restrict__ I,
-                                                   const double* __restrict__ bdict, const double* __restrict__ exc) {
+                                                   const double* __restrict__ bdict, const double* __restrict__ exc,
+                                                   int nd = VI_MAX) {
   static_assert(SFP_N >= VI_MAX * VIB_STRIDE, "the dictionary fits the patch's LDS");
   __shared__ __attribute__((aligned(16))) double S[SFP_N];
   __shared__ double sh[SFP_T / 64];
@@ -3659,8 +3662,8 @@ __global__ __launch_bounds__(SFP_T) void k_spmv_face(Geo g, StFaces sf, const do
     sf_rows(g, q, coef, slot, S, y, dot, threadIdx.x);
   } else {
     const int64_t lo = (int64_t)blockIdx.x * LPB;
-    if (L16) st_tail16<SFP_T>(g, list, lo, min(cnt, lo + LPB), I, bdict, exc, x, y, reinterpret_cast<double2*>(S), dot);
-    else st_tail<SFP_T>(g, list, lo, min(cnt, lo + LPB), I, bdict, exc, x, y, reinterpret_cast<double2*>(S), dot);
+    if (L16) st_tail16<SFP_T>(g, list, lo, min(cnt, lo + LPB), I, bdict, exc, x, y, reinterpret_cast<double2*>(S), dot, nd);
+    else st_tail<SFP_T>(g, list, lo, min(cnt, lo + LPB), I, bdict, exc, x, y, reinterpret_cast<double2*>(S), dot, nd);
   }
   if (DOT) {
     const double sm = block_sum<SFP_T>(dot, sh);
@@ -6343,6 +6346,7 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
           nbfa = sfv.u[6] + (stn + lpb - 1) / lpb;
         }
         double* pf = c.partials + nb;
+        const int ndict = c.vi_nblocks > 0 ? c.vi_nblocks : VI_MAX;  // the listed rows stage only the blocks in use
 #define MCX_SP_DBG(DV, GV) sp_dbg<DV, GV>(c, nb, xpad, y, zt)
 #define MCX_ST(DV, GV)                                                                                             \
   do {                                                                                                            \
@@ -6373,11 +6377,11 @@ void launch_spmv(Ctx& c, const double* xpad, double* y, bool dot, bool gated) {
     if (fs) (void)hipStreamWaitEvent(fst, c.ev_fx, 0);                                                            \
     if (nbfa && st_l16(c))                                                                                        \
       hipLaunchKernelGGL((k_spmv_face<DV, GV>), dim3((unsigned)nbfa), dim3(SFP_T), 0, fst, c.g, sfv,                \
-                         c.st_coef, c.st_slot, xpad, y, pf, c.cg, c.st_list, stn, I, c.vi_bdict, c.vi_exc);    \
+                         c.st_coef, c.st_slot, xpad, y, pf, c.cg, c.st_list, stn, I, c.vi_bdict, c.vi_exc, ndict); \
     else if (nbfa)                                                                                                \
       hipLaunchKernelGGL((k_spmv_face<DV, GV, false>), dim3((unsigned)nbfa), dim3(SFP_T), 0, fst, c.g,              \
                          sfv, c.st_coef, c.st_slot, xpad, y, pf, c.cg, c.st_list, stn, I, c.vi_bdict,   \
-                         c.vi_exc);                                                                               \
+                         c.vi_exc, ndict);                                                                        \
     if (fs) {                                                                                                     \
       (void)hipEventRecord(c.ev_fd, fst);                                                                         \
       (void)hipStreamWaitEvent(c.stream, c.ev_fd, 0);                                                             \
